@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark of the DSM hot path: pages diffed + applied per second (4 KiB pages).
+
+One step = diff of every page of the shard (TWIN vs CURRENT -> canonical run stream, SPEC §3)
++ apply of that stream to the REPLICA arena (SPEC §4); for N > 1 the records whose home shard
+is another rank are exchanged over RCCL (all-to-all) between the two (gallocy_amd/exchange.py).
+
+Workload (BASELINE.json configs[1]): 1M x 4 KiB pages per GPU, 1 % random 8-byte word writes,
+synthetic (SPEC §6), inputs resident in HBM before the timed region. Weak scaling: every rank
+owns 1M pages.
+
+Prints ONE JSON line on rank 0 (contract in the task statement); everything else -> stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pages", type=int, default=1 << 20, help="pages per GPU")
+    ap.add_argument("--mode", choices=["uniform", "clustered"], default="uniform")
+    ap.add_argument("--ppm", type=int, default=None, help="write density in parts per million")
+    ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def payload_bytes(rec_off: np.ndarray, data: np.ndarray) -> int:
+    """Sum of run lengths (|P|) of a host diff stream, vectorised."""
+    sizes = np.diff(rec_off)
+    dirty = np.flatnonzero(sizes)
+    if len(dirty) == 0:
+        return 0
+    w = data.view("<u4") if len(data) % 4 == 0 else np.frombuffer(data.tobytes(), "<u4")
+    starts = rec_off[dirty] // 4
+    nr = w[starts].astype(np.int64)
+    first_hdr = np.repeat(starts + 1, nr)
+    within = np.arange(nr.sum()) - np.repeat(np.cumsum(nr) - nr, nr)
+    return int((w[first_hdr + within] >> 16).astype(np.int64).sum())
+
+
+def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
+    """The C oracle (oracle/liboracle.so, single thread) on a bounded sample of the workload."""
+    from oracle import oracle
+    n = 32768
+    twin, cur = oracle.gen_pages(n, seed=seed, mode=mode, ppm=ppm)
+    rep = twin.copy()
+    ro, data = oracle.diff_pages(twin, cur)  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        ro, data = oracle.diff_pages(twin, cur, cap=int(ro[-1]))
+        oracle.apply(rep, ro, data)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    assert np.array_equal(rep, cur)
+    out = {"value": round(n * reps / dt, 1), "unit": "pages/s", "cores": 1, "kind": "port",
+           "sample": f"{n} pages x {reps} passes of the same workload (seed {seed}), "
+                     f"oracle/gdsm_oracle.c diff+apply, 1 thread, {dt:.1f} s"}
+    drv = oracle.REF_DRIVER
+    if drv.exists():
+        try:
+            r = subprocess.run([str(drv), "time", "1024", "3"], capture_output=True, text=True,
+                               timeout=120, check=True).stdout.split()
+            s, cells = float(r[0]), int(r[1])
+            out["reference_nw_diff"] = {
+                "cells_per_s": round(cells / s, 1), "n": 1024, "seconds_per_call": s,
+                "extrapolated_seconds_per_4KiB_page": round(4096 * 4096 / (cells / s), 4),
+                "note": "reference diff() (gallocy/utils/diff.cpp:73-167) compiled -O0 from its "
+                        "sources (oracle/_ref); extrapolated, the reference crashes at 4 KiB"}
+        except Exception as e:  # noqa: BLE001
+            out["reference_nw_diff"] = {"error": str(e)[:200]}
+    try:
+        import platform
+        out["host_cpu"] = platform.processor() or open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
+    except Exception:  # noqa: BLE001
+        pass
+    return out
+
+
+def read_traffic():
+    """Per-launch HBM bytes of diff_pages_kernel from the committed PMC summary, if any."""
+    for p in sorted((ROOT / "profiles").glob("*traffic*.json"), reverse=True):
+        try:
+            j = json.loads(p.read_text())
+            return j.get("diff_pages_kernel_bytes_per_launch"), p.name
+        except Exception:  # noqa: BLE001
+            continue
+    return None, None
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import gallocy_amd as ga
+    from gallocy_amd import exchange
+
+    mode = ga.GEN_UNIFORM if args.mode == "uniform" else ga.GEN_CLUSTERED
+    ppm = args.ppm if args.ppm is not None else (10000 if mode == ga.GEN_UNIFORM else 100000)
+    n = args.pages
+    if n % world:
+        raise SystemExit("--pages must be a multiple of the GPU count")
+    ctx = ga.Context(n, device=local)
+    # writer(p) = p mod G, home(p) = p // n (gallocy_amd/exchange.py); N = 1 is the identity
+    ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank, stride=world,
+                  arenas=("twin", "current"))
+    ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n, stride=1,
+                  arenas=("replica",))
+    cap = n * (256 if mode == ga.GEN_UNIFORM else 1024)
+    runs = ga.Runs(ctx, n, cap=cap)
+    shard = exchange.Shard(ctx, runs, rank, world, n) if world > 1 else None
+    if shard is not None:
+        shard.gen_args = (args.seed, mode, ppm)
+
+    def step():
+        ctx.diff(out=runs)
+        if shard is None:
+            ctx.apply(runs)
+        else:
+            shard.exchange_and_apply()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    total = runs.total()  # raises ENOSPC if the capacity was too small
+    host = runs.to_host()
+    pay = payload_bytes(host.rec_off, host.data)
+    del host
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    ctx.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    prof = ctx.prof_read()
+    ctx.prof_enable(False)
+    dt = t1 - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # correctness of the measured work: REPLICA == CURRENT afterwards (diff of the two is empty)
+    chk = ga.Runs(ctx, n, cap=1 << 20)
+    ws = ctx.buffer(ga.gdsm.lib().gdsm_diff_workspace_bytes(n))
+    rc = ga.gdsm.lib().gdsm_diff_raw(ctx.arena_ptr("replica"), ctx.arena_ptr("current"), None, n,
+                                     chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes,
+                                     ctx.stream)
+    replica_ok = rc == 0 and chk.total() == 0 if shard is None else shard.verify()
+
+    diff_ms, diff_launches = prof["diff"]
+    avg_diff_ms = diff_ms / max(1, diff_launches)
+    diff_bytes = n * 8192 + total  # algorithmic: twin + current read, records written
+    achieved = diff_bytes / (avg_diff_ms * 1e-3) / 1e9
+    step_bytes = n * 8192 + 2 * total + pay  # B_page summed
+    ms_step = dt / args.steps * 1e3
+    value = world * n * args.steps / dt
+    traffic, traffic_src = read_traffic()
+
+    if rank == 0:
+        stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
+                  for k, v in prof.items() if v[1]}
+        res = {
+            "metric": "pages diffed+applied/sec (4 KiB)",
+            "value": round(value, 1),
+            "unit": "pages/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (counter-hash pages, docs/SPEC.md §6)",
+            "config": {"workload": f"{n} x 4 KiB pages per GPU, {args.mode} {ppm / 1e4:g}% "
+                                   f"{'8-B word' if mode == ga.GEN_UNIFORM else '64-B cluster'} writes, "
+                                   f"diff+apply" + (", RCCL all-to-all exchange" if world > 1 else ""),
+                       "pages_per_gpu": n, "seed": args.seed, "parallelism": f"page-shard x{world}",
+                       "diff_bytes_per_step": int(total), "payload_bytes_per_step": int(pay)},
+            "step_hbm_gbs": round(step_bytes * args.steps / dt / 1e9, 1),
+            "roofline": {"bound": "hbm", "kernel": "diff_pages_kernel",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": int(diff_bytes),
+                         "avg_launch_ms": round(avg_diff_ms, 4)},
+            "stages": stages,
+            "replica_equals_current": bool(replica_ok),
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(mode, ppm, args.seed, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

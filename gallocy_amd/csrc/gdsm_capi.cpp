@@ -1,0 +1,465 @@
+// C-ABI of libgdsm.so (include/gdsm.h): context, arenas, streams, error mapping.
+// Host C++ only; kernels are launched through gdsm_launch.h.
+#include <errno.h>
+#include <hip/hip_runtime_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <set>
+
+#include "gdsm.h"
+#include "gdsm_launch.h"
+
+struct gdsm_ctx {
+  int device = 0;
+  uint64_t n_pages = 0;
+  hipStream_t stream = nullptr;
+  uint8_t* arena[3] = {nullptr, nullptr, nullptr};
+  uint32_t* err = nullptr;       // device error word (bit 0: malformed record, bit 1: bad events)
+  uint8_t* diff_ws = nullptr;    // diff workspace
+  uint64_t diff_ws_bytes = 0;
+  uint8_t* coh_ws = nullptr;
+  uint64_t coh_ws_bytes = 0;
+  uint32_t* coh_state = nullptr;
+  uint32_t* coh_faults = nullptr;
+  uint64_t* coh_totals = nullptr;  // device 10 x u64
+  uint32_t n_nodes = 0;
+  std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks
+  gdsm::Prof prof;
+  gdsm::Prof* P() { return prof.on ? &prof : nullptr; }
+};
+
+namespace {
+
+int map_err(hipError_t e) {
+  switch (e) {
+    case hipSuccess: return 0;
+    case hipErrorOutOfMemory: return -ENOMEM;
+    case hipErrorInvalidValue: return -EINVAL;
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice: return -ENODEV;
+    default: return -EIO;
+  }
+}
+
+#define GDSM_TRY(expr)                 \
+  do {                                 \
+    hipError_t e_ = (expr);            \
+    if (e_ != hipSuccess) return map_err(e_); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int ensure(uint8_t** buf, uint64_t* have, uint64_t need) {
+  if (*have >= need) return 0;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *have = 0;
+  GDSM_TRY(hipMalloc(reinterpret_cast<void**>(buf), need));
+  *have = need;
+  return 0;
+}
+
+int check_and_clear_err(gdsm_ctx* ctx) {
+  uint32_t h = 0;
+  GDSM_TRY(hipMemcpyAsync(&h, ctx->err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  GDSM_TRY(hipMemsetAsync(ctx->err, 0, 4, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  return h ? -EINVAL : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gdsm_version(void) { return "gdsm 0.1.0 (gfx950)"; }
+
+int gdsm_device_count(int* count) {
+  if (!count) return -EINVAL;
+  *count = 0;
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) {
+    *count = 0;
+    return -ENODEV;
+  }
+  return 0;
+}
+
+int gdsm_init(gdsm_ctx** out, int device, uint64_t n_pages, uint32_t flags) {
+  if (!out) return -EINVAL;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return -ENODEV;
+  if (device < 0 || device >= count) return -EINVAL;
+  if (flags == 0) flags = GDSM_WANT_TWIN | GDSM_WANT_CURRENT | GDSM_WANT_REPLICA;
+  if (flags & GDSM_NO_ARENAS) flags = 0;
+  gdsm_ctx* ctx = new (std::nothrow) gdsm_ctx();
+  if (!ctx) return -ENOMEM;
+  ctx->device = device;
+  ctx->n_pages = n_pages;
+  DeviceGuard g(device);
+  int rc = 0;
+  do {
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->err), 256) != hipSuccess) {
+      rc = -ENOMEM;
+      break;
+    }
+    (void)hipMemset(ctx->err, 0, 256);
+    for (int a = 0; a < 3 && !rc; ++a) {
+      if (!(flags & (1u << a)) || n_pages == 0) continue;
+      if (hipMalloc(reinterpret_cast<void**>(&ctx->arena[a]), n_pages * GDSM_PAGE_SZ) !=
+          hipSuccess)
+        rc = -ENOMEM;
+    }
+  } while (0);
+  if (rc) {
+    gdsm_fini(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return 0;
+}
+
+int gdsm_fini(gdsm_ctx* ctx) {
+  if (!ctx) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& a : ctx->arena)
+    if (a) (void)hipFree(a);
+  for (void* p : ctx->allocs) (void)hipFree(p);
+  if (ctx->err) (void)hipFree(ctx->err);
+  if (ctx->diff_ws) (void)hipFree(ctx->diff_ws);
+  if (ctx->coh_ws) (void)hipFree(ctx->coh_ws);
+  if (ctx->coh_state) (void)hipFree(ctx->coh_state);
+  if (ctx->coh_faults) (void)hipFree(ctx->coh_faults);
+  if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return 0;
+}
+
+int gdsm_arena(gdsm_ctx* ctx, int which, void** dev_ptr) {
+  if (!ctx || !dev_ptr || which < 0 || which > 2 || !ctx->arena[which]) return -EINVAL;
+  *dev_ptr = ctx->arena[which];
+  return 0;
+}
+
+uint64_t gdsm_n_pages(const gdsm_ctx* ctx) { return ctx ? ctx->n_pages : 0; }
+
+void* gdsm_stream(gdsm_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int gdsm_sync(gdsm_ctx* ctx) {
+  if (!ctx) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  return check_and_clear_err(ctx);
+}
+
+static int page_copy(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void* host, bool up) {
+  if (!ctx || which < 0 || which > 2 || !ctx->arena[which] || (!host && n)) return -EINVAL;
+  if (first > ctx->n_pages || n > ctx->n_pages - first) return -EINVAL;
+  if (n == 0) return 0;
+  DeviceGuard g(ctx->device);
+  uint8_t* dev = ctx->arena[which] + first * GDSM_PAGE_SZ;
+  const uint64_t bytes = n * GDSM_PAGE_SZ;
+  if (up)
+    GDSM_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+  else
+    GDSM_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gdsm_upload(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, const void* host) {
+  return page_copy(ctx, which, first, n, const_cast<void*>(host), true);
+}
+
+int gdsm_download(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void* host) {
+  return page_copy(ctx, which, first, n, host, false);
+}
+
+int gdsm_dev_alloc(gdsm_ctx* ctx, uint64_t bytes, void** dev_ptr) {
+  if (!ctx || !dev_ptr) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  void* p = nullptr;
+  GDSM_TRY(hipMalloc(&p, bytes ? bytes : 16));
+  ctx->allocs.insert(p);
+  *dev_ptr = p;
+  return 0;
+}
+
+int gdsm_dev_free(gdsm_ctx* ctx, void* dev_ptr) {
+  if (!ctx || !dev_ptr || !ctx->allocs.count(dev_ptr)) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  ctx->allocs.erase(dev_ptr);
+  GDSM_TRY(hipFree(dev_ptr));
+  return 0;
+}
+
+int gdsm_memcpy_h2d(gdsm_ctx* ctx, void* dev, const void* host, uint64_t bytes) {
+  if (!ctx || (bytes && (!dev || !host))) return -EINVAL;
+  if (!bytes) return 0;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gdsm_memcpy_d2h(gdsm_ctx* ctx, void* host, const void* dev, uint64_t bytes) {
+  if (!ctx || (bytes && (!dev || !host))) return -EINVAL;
+  if (!bytes) return 0;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gdsm_prof_enable(gdsm_ctx* ctx, int on) {
+  if (!ctx) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->prof.resolve();
+  ctx->prof.clear();
+  ctx->prof.on = on != 0;
+  return 0;
+}
+
+int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches) {
+  if (!ctx || !ms || !launches) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->prof.resolve();
+  for (int i = 0; i < GDSM_PROF_STAGES; ++i) {
+    ms[i] = ctx->prof.ms[i];
+    launches[i] = ctx->prof.launches[i];
+  }
+  ctx->prof.clear();
+  return 0;
+}
+
+int gdsm_gen_pages(gdsm_ctx* ctx, uint32_t arenas, uint64_t first_global, uint64_t stride,
+                   uint64_t seed, int mode, uint32_t ppm) {
+  if (!ctx) return -EINVAL;
+  if (arenas == 0) arenas = 7u;
+  if (arenas & ~7u) return -EINVAL;
+  for (int a = 0; a < 3; ++a)
+    if ((arenas & (1u << a)) && !ctx->arena[a]) return -EINVAL;
+  if (mode != GDSM_GEN_UNIFORM && mode != GDSM_GEN_CLUSTERED) return -EINVAL;
+  if (ppm > 1000000u) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  auto pick = [&](int a) { return (arenas & (1u << a)) ? ctx->arena[a] : nullptr; };
+  GDSM_TRY(gdsm::launch_gen_pages(pick(GDSM_TWIN), pick(GDSM_CURRENT), pick(GDSM_REPLICA),
+                                  ctx->n_pages, first_global, stride, seed, mode, ppm,
+                                  ctx->stream));
+  return 0;
+}
+
+int gdsm_gen_pages_raw(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint64_t n,
+                       uint64_t first_global, uint64_t stride, uint64_t seed, int mode,
+                       uint32_t ppm, void* stream) {
+  if (mode != GDSM_GEN_UNIFORM && mode != GDSM_GEN_CLUSTERED) return -EINVAL;
+  if (ppm > 1000000u) return -EINVAL;
+  GDSM_TRY(gdsm::launch_gen_pages(twin, cur, replica, n, first_global, stride, seed, mode, ppm,
+                                  static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int gdsm_twin(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n) {
+  if (!ctx || !ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
+  if (!ids && n > ctx->n_pages) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(gdsm::launch_twin(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
+                             ctx->stream, ctx->P()));
+  return 0;
+}
+
+int gdsm_runs_alloc(gdsm_ctx* ctx, uint64_t n, uint64_t cap, gdsm_runs* out) {
+  if (!ctx || !out) return -EINVAL;
+  if (cap == 0) cap = n * (uint64_t)GDSM_MAX_RECORD;
+  cap = (cap + 15) & ~15ull;
+  DeviceGuard g(ctx->device);
+  memset(out, 0, sizeof(*out));
+  void* ro = nullptr;
+  void* d = nullptr;
+  GDSM_TRY(hipMalloc(&ro, (n + 1) * sizeof(uint64_t)));
+  if (hipMalloc(&d, cap ? cap : 16) != hipSuccess) {
+    (void)hipFree(ro);
+    return -ENOMEM;
+  }
+  ctx->allocs.insert(ro);
+  ctx->allocs.insert(d);
+  out->n = n;
+  out->rec_off = static_cast<uint64_t*>(ro);
+  out->data = static_cast<uint8_t*>(d);
+  out->cap = cap;
+  out->owned = 1;
+  return 0;
+}
+
+int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs) {
+  if (!ctx || !runs || !runs->owned) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (void* p : {static_cast<void*>(runs->rec_off), static_cast<void*>(runs->data)}) {
+    if (ctx->allocs.erase(p)) (void)hipFree(p);
+  }
+  memset(runs, 0, sizeof(*runs));
+  return 0;
+}
+
+int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
+  if (!ctx || !out || !out->rec_off || (!out->data && out->cap)) return -EINVAL;
+  if (!ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
+  if (!ids && n > ctx->n_pages) return -EINVAL;
+  if (out->n < n && out->owned) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
+  int rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk ? chunk : 1));
+  if (rc) return rc;
+  out->n = n;
+  GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
+                             out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
+                             ctx->stream, ctx->P()));
+  return 0;
+}
+
+int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total) {
+  if (!ctx || !runs || !total || !runs->rec_off) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  uint64_t t = 0;
+  GDSM_TRY(hipMemcpyAsync(&t, runs->rec_off + runs->n, 8, hipMemcpyDeviceToHost, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  *total = t;
+  return t > runs->cap ? -ENOSPC : 0;
+}
+
+int gdsm_apply(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_runs* in) {
+  if (!ctx || !in || target < 0 || target > 2 || !ctx->arena[target]) return -EINVAL;
+  if (!ids && in->n > ctx->n_pages) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(gdsm::launch_apply(ctx->arena[target], ids, in->n, in->rec_off, in->data, ctx->err,
+                              ctx->stream, ctx->P()));
+  return 0;
+}
+
+uint64_t gdsm_diff_workspace_bytes(uint64_t n) {
+  const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
+  return gdsm::diff_workspace_bytes(chunk ? chunk : 1);
+}
+
+int gdsm_diff_raw(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
+                  uint64_t* rec_off, uint8_t* data, uint64_t cap, void* workspace,
+                  uint64_t workspace_bytes, void* stream) {
+  if (!twin || !cur || !rec_off || !workspace || (!data && cap)) return -EINVAL;
+  GDSM_TRY(gdsm::launch_diff(twin, cur, ids, n, rec_off, data, cap,
+                             static_cast<uint8_t*>(workspace), workspace_bytes,
+                             static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int gdsm_apply_raw(uint8_t* target, const uint32_t* ids, uint64_t n, const uint64_t* rec_off,
+                   const uint8_t* data, void* stream) {
+  if (!target || !rec_off || (!data && n)) return -EINVAL;
+  static uint32_t* err_word = nullptr;  // raw calls share one device error word per process
+  static std::mutex mu;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!err_word) GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&err_word), 4));
+    GDSM_TRY(hipMemsetAsync(err_word, 0, 4, static_cast<hipStream_t>(stream)));
+  }
+  GDSM_TRY(gdsm::launch_apply(target, ids, n, rec_off, data, err_word,
+                              static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int gdsm_twin_raw(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
+                  void* stream) {
+  if (!twin || !cur) return -EINVAL;
+  GDSM_TRY(gdsm::launch_twin(twin, cur, ids, n, static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+// ---- coherence -------------------------------------------------------------------------
+int gdsm_coh_init(gdsm_ctx* ctx, uint32_t n_nodes) {
+  if (!ctx || n_nodes == 0 || n_nodes > GDSM_MAX_NODES) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  if (!ctx->coh_state) {
+    const uint64_t bytes = (ctx->n_pages ? ctx->n_pages : 1) * 4;
+    GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_state), bytes));
+    GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_faults), bytes));
+    GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_totals), 10 * sizeof(uint64_t)));
+  }
+  ctx->n_nodes = n_nodes;
+  GDSM_TRY(gdsm::launch_coh_init(ctx->coh_state, ctx->coh_faults, ctx->n_pages, n_nodes,
+                                 ctx->stream));
+  return 0;
+}
+
+int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_events,
+                               uint64_t* totals_dev) {
+  if (!ctx || !ctx->coh_state || !totals_dev || (!events && n_events)) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  int rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
+  if (rc) return rc;
+  GDSM_TRY(gdsm::launch_coherence(ctx->coh_state, ctx->coh_faults, ctx->n_pages, events,
+                                  n_events, totals_dev, ctx->coh_ws, ctx->coh_ws_bytes, ctx->err,
+                                  ctx->stream, ctx->P()));
+  return 0;
+}
+
+int gdsm_coherence_batch(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_events,
+                         uint64_t* totals) {
+  if (!ctx || !totals) return -EINVAL;
+  int rc = gdsm_coherence_batch_async(ctx, events, n_events, ctx->coh_totals);
+  if (rc) return rc;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(hipMemcpyAsync(totals, ctx->coh_totals, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          ctx->stream));
+  return gdsm_sync(ctx);
+}
+
+int gdsm_coh_download(gdsm_ctx* ctx, uint32_t* state, uint32_t* faults) {
+  if (!ctx || !ctx->coh_state) return -EINVAL;
+  int rc = 0;
+  if (state) rc = gdsm_memcpy_d2h(ctx, state, ctx->coh_state, ctx->n_pages * 4);
+  if (!rc && faults) rc = gdsm_memcpy_d2h(ctx, faults, ctx->coh_faults, ctx->n_pages * 4);
+  return rc;
+}
+
+int gdsm_coh_upload(gdsm_ctx* ctx, const uint32_t* state, const uint32_t* faults) {
+  if (!ctx || !ctx->coh_state) return -EINVAL;
+  int rc = 0;
+  if (state) rc = gdsm_memcpy_h2d(ctx, ctx->coh_state, state, ctx->n_pages * 4);
+  if (!rc && faults) rc = gdsm_memcpy_h2d(ctx, ctx->coh_faults, faults, ctx->n_pages * 4);
+  return rc;
+}
+
+int gdsm_gen_events(gdsm_ctx* ctx, uint64_t* events, const uint64_t* offsets, uint64_t first_page,
+                    uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct) {
+  if (!ctx || (n && (!events || !offsets)) || n_nodes == 0 || n_nodes > GDSM_MAX_NODES ||
+      write_pct > 100)
+    return -EINVAL;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(gdsm::launch_gen_events(events, offsets, first_page, n, seed, n_nodes, write_pct,
+                                   ctx->stream));
+  return 0;
+}
+
+}  // extern "C"

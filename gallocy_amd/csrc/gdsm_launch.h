@@ -1,0 +1,42 @@
+// Host-side launchers for the gdsm kernels (internal; the public ABI is include/gdsm.h).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "gdsm_prof.h"
+
+namespace gdsm {
+
+// Diff geometry: one 256-thread workgroup (4 waves) diffs kDiffPagesPerBlock pages.
+constexpr uint32_t kDiffPagesPerBlock = 64;
+// Largest chunk of pages one diff pass handles with its workspace (the API loops over chunks).
+constexpr uint64_t kDiffChunk = 1ull << 20;
+
+uint64_t diff_workspace_bytes(uint64_t n_chunk);
+
+hipError_t launch_gen_pages(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint64_t n,
+                            uint64_t first_global, uint64_t stride, uint64_t seed, int mode,
+                            uint32_t ppm, hipStream_t s);
+hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
+                       hipStream_t s, Prof* prof = nullptr);
+// Full diff of n pages (chunked internally): rec_off[n+1], data[cap].
+hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
+                       uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
+                       uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr);
+hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
+                        const uint64_t* rec_off, const uint8_t* data, uint32_t* err,
+                        hipStream_t s, Prof* prof = nullptr);
+
+// Coherence (SPEC §5).
+uint64_t coh_workspace_bytes(uint64_t n_events);
+hipError_t launch_coh_init(uint32_t* state, uint32_t* faults, uint64_t n_pages, uint32_t n_nodes,
+                           hipStream_t s);
+hipError_t launch_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages,
+                            const uint64_t* events, uint64_t n_events, uint64_t* totals,
+                            uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
+                            Prof* prof = nullptr);
+hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,
+                             uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,
+                             hipStream_t s);
+
+}  // namespace gdsm

@@ -1,0 +1,322 @@
+"""Host-side mirror of the gdsm C-ABI (include/gdsm.h) for Python callers and tests.
+
+Names follow the reference's domain: pages, twins, diffs (run records), replicas, the page
+table. `diff()` keeps the reference utility's name and meaning
+(gallocy/utils/diff.cpp:73-167); the page-level engine is `Context`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import GdsmError, GdsmRuns, check
+
+PAGE_SZ = 4096
+MAX_RUNS = 2048
+MAX_RECORD = 10244
+TWIN, CURRENT, REPLICA = 0, 1, 2
+GEN_UNIFORM, GEN_CLUSTERED = 0, 1
+_ARENA = {"twin": TWIN, "current": CURRENT, "replica": REPLICA,
+          TWIN: TWIN, CURRENT: CURRENT, REPLICA: REPLICA}
+
+
+def lib():
+    return _lib.load()
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib().gdsm_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def version() -> str:
+    return lib().gdsm_version().decode()
+
+
+class DeviceBuffer:
+    """A device allocation owned by a Context (freed with it, or by .free())."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(lib().gdsm_dev_alloc(ctx.handle, self.nbytes, C.byref(p)), "gdsm_dev_alloc")
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(arr)
+        if a.nbytes > self.nbytes:
+            raise ValueError("array larger than the device buffer")
+        check(lib().gdsm_memcpy_h2d(self.ctx.handle, self.ptr, a.ctypes.data, a.nbytes), "h2d")
+        return self
+
+    def download(self, dtype, count: int) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes > self.nbytes:
+            raise ValueError("read past the device buffer")
+        check(lib().gdsm_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr, out.nbytes), "d2h")
+        return out
+
+    def free(self):
+        if self.ptr and self.ctx.handle:
+            check(lib().gdsm_dev_free(self.ctx.handle, self.ptr), "gdsm_dev_free")
+        self.ptr = None
+
+
+@dataclass
+class HostRuns:
+    """A diff stream on the host: rec_off[n+1] (uint64) and data (uint8), SPEC §3."""
+    rec_off: np.ndarray
+    data: np.ndarray
+
+    @property
+    def n(self) -> int:
+        return len(self.rec_off) - 1
+
+    def record(self, i: int) -> bytes:
+        return self.data[self.rec_off[i]:self.rec_off[i + 1]].tobytes()
+
+    def runs(self, i: int):
+        """[(off, len, payload bytes)] of record i."""
+        r = self.record(i)
+        if not r:
+            return []
+        nr = int(np.frombuffer(r[:4], "<u4")[0])
+        hdr = np.frombuffer(r[4:4 + 4 * nr], "<u4")
+        out, p = [], 4 + 4 * nr
+        for h in hdr:
+            o, ln = int(h & 0xFFFF), int(h >> 16)
+            out.append((o, ln, r[p:p + ln]))
+            p += ln
+        return out
+
+
+class Runs:
+    """A device diff stream (gdsm_runs)."""
+
+    def __init__(self, ctx: "Context", n: int, cap: int = 0):
+        self.ctx = ctx
+        self.s = GdsmRuns()
+        check(lib().gdsm_runs_alloc(ctx.handle, n, cap, C.byref(self.s)), "gdsm_runs_alloc")
+
+    @property
+    def n(self) -> int:
+        return self.s.n
+
+    @property
+    def cap(self) -> int:
+        return self.s.cap
+
+    def total(self) -> int:
+        t = C.c_uint64(0)
+        rc = lib().gdsm_runs_total(self.ctx.handle, C.byref(self.s), C.byref(t))
+        if rc == -28:
+            raise GdsmError(28, f"diff stream needs {t.value} bytes, capacity {self.cap}")
+        check(rc, "gdsm_runs_total")
+        return t.value
+
+    def to_host(self) -> HostRuns:
+        total = self.total()
+        ro = np.empty(self.n + 1, np.uint64)
+        check(lib().gdsm_memcpy_d2h(self.ctx.handle, ro.ctypes.data, self.s.rec_off, ro.nbytes), "d2h")
+        data = np.empty(total, np.uint8)
+        if total:
+            check(lib().gdsm_memcpy_d2h(self.ctx.handle, data.ctypes.data, self.s.data, total), "d2h")
+        return HostRuns(ro, data)
+
+    @classmethod
+    def from_host(cls, ctx: "Context", host: HostRuns, cap: Optional[int] = None) -> "Runs":
+        r = cls(ctx, host.n, cap if cap is not None else max(16, len(host.data)))
+        ro = np.ascontiguousarray(host.rec_off, dtype=np.uint64)
+        check(lib().gdsm_memcpy_h2d(ctx.handle, r.s.rec_off, ro.ctypes.data, ro.nbytes), "h2d")
+        if len(host.data):
+            d = np.ascontiguousarray(host.data, dtype=np.uint8)
+            check(lib().gdsm_memcpy_h2d(ctx.handle, r.s.data, d.ctypes.data, d.nbytes), "h2d")
+        return r
+
+    def free(self):
+        if self.s.owned:
+            check(lib().gdsm_runs_free(self.ctx.handle, C.byref(self.s)), "gdsm_runs_free")
+
+
+class Context:
+    """One shard of pages on one GPU: TWIN / CURRENT / REPLICA arenas + the page table."""
+
+    def __init__(self, n_pages: int, device: int = 0, arenas: Sequence = ("twin", "current", "replica")):
+        flags = 0
+        for a in arenas:
+            flags |= 1 << _ARENA[a]
+        if not flags:
+            flags = 1 << 31  # GDSM_NO_ARENAS: page-table-only context
+        h = C.c_void_p()
+        check(lib().gdsm_init(C.byref(h), device, n_pages, flags), "gdsm_init")
+        self.handle = h.value
+        self.n_pages = n_pages
+        self.device = device
+
+    # -- lifetime
+    def close(self):
+        if self.handle:
+            lib().gdsm_fini(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- plumbing
+    def arena_ptr(self, which) -> int:
+        p = C.c_void_p()
+        check(lib().gdsm_arena(self.handle, _ARENA[which], C.byref(p)), "gdsm_arena")
+        return p.value
+
+    @property
+    def stream(self) -> int:
+        return lib().gdsm_stream(self.handle)
+
+    def sync(self):
+        check(lib().gdsm_sync(self.handle), "gdsm_sync")
+
+    PROF_STAGES = ("diff", "scan", "pack", "apply", "twin", "coh_tail", "coh_scan", "coh_apply",
+                   "coh_reduce")
+
+    def prof_enable(self, on: bool = True):
+        check(lib().gdsm_prof_enable(self.handle, int(on)), "gdsm_prof_enable")
+
+    def prof_read(self) -> dict:
+        """{stage: (total_ms, launches)} from HIP events on the context stream."""
+        ms = (C.c_double * 9)()
+        ln = (C.c_uint64 * 9)()
+        check(lib().gdsm_prof_read(self.handle, ms, ln), "gdsm_prof_read")
+        return {k: (ms[i], ln[i]) for i, k in enumerate(self.PROF_STAGES)}
+
+    def upload(self, which, pages: np.ndarray, first: int = 0):
+        a = np.ascontiguousarray(pages, dtype=np.uint8).reshape(-1, PAGE_SZ)
+        check(lib().gdsm_upload(self.handle, _ARENA[which], first, a.shape[0], a.ctypes.data), "upload")
+
+    def download(self, which, first: int = 0, n: Optional[int] = None) -> np.ndarray:
+        n = self.n_pages - first if n is None else n
+        out = np.empty((n, PAGE_SZ), np.uint8)
+        check(lib().gdsm_download(self.handle, _ARENA[which], first, n, out.ctypes.data), "download")
+        return out
+
+    def buffer(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def ids(self, page_ids) -> DeviceBuffer:
+        a = np.ascontiguousarray(page_ids, dtype=np.uint32)
+        return DeviceBuffer(self, max(4, a.nbytes)).upload(a)
+
+    @staticmethod
+    def _ptr(ids) -> Optional[int]:
+        if ids is None:
+            return None
+        if isinstance(ids, DeviceBuffer):
+            return ids.ptr
+        return int(ids)
+
+    # -- hot path
+    def gen_pages(self, seed: int, mode: int = GEN_UNIFORM, ppm: int = 10000, first_global: int = 0,
+                  stride: int = 1, arenas: Sequence = ()):
+        """SPEC §6 synthetic pages; arena page i is global page first_global + i * stride."""
+        mask = 0
+        for a in arenas:
+            mask |= 1 << _ARENA[a]
+        check(lib().gdsm_gen_pages(self.handle, mask, first_global, stride, seed, mode, ppm),
+              "gdsm_gen_pages")
+
+    def twin(self, ids=None, n: Optional[int] = None):
+        n = self._count(ids, n)
+        check(lib().gdsm_twin(self.handle, self._ptr(ids), n), "gdsm_twin")
+
+    def diff(self, ids=None, n: Optional[int] = None, out: Optional[Runs] = None, cap: int = 0) -> Runs:
+        n = self._count(ids, n)
+        out = out or Runs(self, n, cap)
+        check(lib().gdsm_diff(self.handle, self._ptr(ids), n, C.byref(out.s)), "gdsm_diff")
+        return out
+
+    def apply(self, runs: Runs, target="replica", ids=None):
+        check(lib().gdsm_apply(self.handle, _ARENA[target], self._ptr(ids), C.byref(runs.s)), "gdsm_apply")
+
+    def _count(self, ids, n):
+        if n is not None:
+            return int(n)
+        if ids is None:
+            return self.n_pages
+        if isinstance(ids, DeviceBuffer):
+            return ids.nbytes // 4
+        raise ValueError("pass n= with a raw device pointer")
+
+    # -- page table (coherence)
+    def coh_init(self, n_nodes: int = 8):
+        check(lib().gdsm_coh_init(self.handle, n_nodes), "gdsm_coh_init")
+
+    def coherence_batch(self, events) -> dict:
+        """events: a DeviceBuffer of uint64 (page-sorted) or a numpy array (uploaded here)."""
+        tmp = None
+        if isinstance(events, np.ndarray):
+            ev = np.ascontiguousarray(events, dtype=np.uint64)
+            tmp = DeviceBuffer(self, max(8, ev.nbytes)).upload(ev)
+            ptr, n = tmp.ptr, len(ev)
+        else:
+            ptr, n = events.ptr, events.nbytes // 8
+        tot = (C.c_uint64 * 10)()
+        try:
+            check(lib().gdsm_coherence_batch(self.handle, ptr, n, tot), "gdsm_coherence_batch")
+        finally:
+            if tmp is not None:
+                tmp.free()
+        t = list(tot)
+        return {"invalidations": t[0], "transfers": t[1], "node_faults": t[2:10]}
+
+    def coh_download(self):
+        st = np.empty(self.n_pages, np.uint32)
+        fl = np.empty(self.n_pages, np.uint32)
+        check(lib().gdsm_coh_download(self.handle, st.ctypes.data, fl.ctypes.data), "gdsm_coh_download")
+        return st, fl
+
+    def coh_upload(self, state: np.ndarray, faults: np.ndarray):
+        s = np.ascontiguousarray(state, np.uint32)
+        f = np.ascontiguousarray(faults, np.uint32)
+        check(lib().gdsm_coh_upload(self.handle, s.ctypes.data, f.ctypes.data), "gdsm_coh_upload")
+
+    def gen_events(self, counts: np.ndarray, seed: int, n_nodes: int = 8, write_pct: int = 20,
+                   first_page: int = 0) -> DeviceBuffer:
+        counts = np.ascontiguousarray(counts, dtype=np.uint64)
+        offs = np.zeros(len(counts) + 1, np.uint64)
+        np.cumsum(counts, out=offs[1:])
+        total = int(offs[-1])
+        d_off = DeviceBuffer(self, offs.nbytes).upload(offs)
+        ev = DeviceBuffer(self, max(8, total * 8))
+        check(lib().gdsm_gen_events(self.handle, ev.ptr, d_off.ptr, first_page, len(counts), seed,
+                                    n_nodes, write_pct), "gdsm_gen_events")
+        self.sync()
+        d_off.free()
+        ev.count = total
+        return ev
+
+
+def diff(mem1: bytes, mem2: bytes):
+    """The reference diff() (gallocy/utils/diff.cpp:73-167): NW alignment -> (out1, out2)."""
+    L = lib()
+    o1, o2, n = C.c_void_p(), C.c_void_p(), C.c_size_t(0)
+    check(L.gdsm_nw_diff(mem1, len(mem1), C.byref(o1), mem2, len(mem2), C.byref(o2), C.byref(n)), "diff")
+    try:
+        return C.string_at(o1, n.value), C.string_at(o2, n.value)
+    finally:
+        libc = C.CDLL(None)
+        libc.free(o1)
+        libc.free(o2)

@@ -1,0 +1,180 @@
+/*
+ * gdsm — MI355X-native engine for gallocy's DSM hot path (page twin / run diff / apply /
+ * batched coherence). C ABI: plain pointers and sizes, no torch or HIP types in signatures.
+ * Semantics are frozen in docs/SPEC.md.
+ *
+ * Where each entry point sits in the reference (/root/reference, gallocy 0.0.438):
+ *   - The reference has no plugin or operator registry; its hot-path "interface" is the leaf
+ *     utility `int diff(const char*, size_t, char*&, const char*, size_t, char*&)`
+ *     (gallocy/include/gallocy/utils/diff.h:9-11, gallocy/utils/diff.cpp:73-167) plus the
+ *     page-tracking hooks of the allocator stack that were never written:
+ *     `PageTableHeap<Super>` (gallocy/include/gallocy/heaplayers/pagetableheap.h:12-29, only a
+ *     LOG_DEBUG) and the per-page record `ApplicationMemory`
+ *     (gallocy/include/gallocy/models.h:171-213, declared, never defined).
+ *   - gdsm_diff / gdsm_apply / gdsm_twin replace the twin/diff/apply steps of the
+ *     fault → negotiate → "copy over the latest contents" flow that the reference describes but
+ *     does not implement (resources/NUTSHELL.md:59-69, resources/IMPLEMENTATION.md:246-249);
+ *     the run record is the (offset, bytes) edit of print_diff (gallocy/utils/diff.cpp:43-70).
+ *   - gdsm_coh_* replace the ApplicationMemory table (`dirty, owner, permissions, faults`,
+ *     models.h:171-213) and the missing page-table application step of Raft's `try_apply`
+ *     (gallocy/consensus/state.cpp:308-316).
+ *   - gdsm_nw_diff is the reference diff() with the alignment length returned (the reference
+ *     drops it, diff.h:9-11); the unchanged legacy C++ symbol `diff` is declared at the bottom.
+ *   - The allocator hooks gdsm_set_allocator mirror internal_malloc/internal_free
+ *     (gallocy/include/gallocy/allocators/internal.h:75-82), which own diff()'s outputs.
+ *
+ * Conventions: every function returns 0 or a negative errno (-EINVAL -22, -ENOMEM -12,
+ * -EIO -5 for a HIP failure, -ENOSPC -28, -ENODEV -19) and never aborts. Device work is
+ * enqueued on the context's HIP stream and is asynchronous unless the comment says it
+ * synchronises. One context per host thread, or external synchronisation.
+ */
+#ifndef GDSM_H_
+#define GDSM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GDSM_PAGE_SZ 4096u
+#define GDSM_MAX_RUNS 2048u
+#define GDSM_MAX_NODES 8u
+/* Largest record: 4 + 4*2048 + 2048 (alternating bytes), SPEC §3. */
+#define GDSM_MAX_RECORD 10244u
+
+enum gdsm_arena_kind { GDSM_TWIN = 0, GDSM_CURRENT = 1, GDSM_REPLICA = 2 };
+enum gdsm_gen_mode { GDSM_GEN_UNIFORM = 0, GDSM_GEN_CLUSTERED = 1 };
+/* gdsm_init flags: which arenas the context allocates (all three when 0). */
+enum gdsm_init_flags {
+  GDSM_WANT_TWIN = 1u << 0,
+  GDSM_WANT_CURRENT = 1u << 1,
+  GDSM_WANT_REPLICA = 1u << 2,
+  GDSM_NO_ARENAS = 1u << 31, /* page-table-only context */
+};
+/* Per-kernel stages timed by gdsm_prof_* (HIP events on the context stream). */
+enum gdsm_prof_stage {
+  GDSM_PROF_DIFF = 0, /* diff_pages_kernel: the dominant kernel of the hot path */
+  GDSM_PROF_SCAN,
+  GDSM_PROF_PACK,
+  GDSM_PROF_APPLY,
+  GDSM_PROF_TWIN,
+  GDSM_PROF_COH_TAIL,
+  GDSM_PROF_COH_SCAN,
+  GDSM_PROF_COH_APPLY,
+  GDSM_PROF_COH_REDUCE,
+  GDSM_PROF_STAGES
+};
+
+typedef struct gdsm_ctx gdsm_ctx;
+
+/* A diff stream (SPEC §3). All pointers are device pointers. */
+typedef struct gdsm_runs {
+  uint64_t n;        /* records */
+  uint64_t* rec_off; /* n + 1 */
+  uint8_t* data;     /* cap bytes */
+  uint64_t cap;
+  uint32_t owned;    /* 1 if allocated by gdsm_runs_alloc */
+  uint32_t _pad;
+} gdsm_runs;
+
+/* ---- context ------------------------------------------------------------------------- */
+int gdsm_device_count(int* count);
+/* Allocates the arenas (n_pages × 4 KiB each) on `device` and one HIP stream. */
+int gdsm_init(gdsm_ctx** out, int device, uint64_t n_pages, uint32_t flags);
+int gdsm_fini(gdsm_ctx* ctx);
+int gdsm_arena(gdsm_ctx* ctx, int which, void** dev_ptr);
+uint64_t gdsm_n_pages(const gdsm_ctx* ctx);
+/* The context's hipStream_t, as an opaque pointer. */
+void* gdsm_stream(gdsm_ctx* ctx);
+/* Waits for all enqueued work; reports a device-side failure recorded since the last sync. */
+int gdsm_sync(gdsm_ctx* ctx);
+/* Synchronous host <-> arena copies of pages [first, first+n). */
+int gdsm_upload(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, const void* host);
+int gdsm_download(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void* host);
+/* Device scratch owned by the context (freed by gdsm_fini). */
+int gdsm_dev_alloc(gdsm_ctx* ctx, uint64_t bytes, void** dev_ptr);
+int gdsm_dev_free(gdsm_ctx* ctx, void* dev_ptr);
+int gdsm_memcpy_h2d(gdsm_ctx* ctx, void* dev, const void* host, uint64_t bytes);
+int gdsm_memcpy_d2h(gdsm_ctx* ctx, void* host, const void* dev, uint64_t bytes);
+
+/* Per-kernel timing: when enabled, every kernel the context launches is bracketed by HIP events
+ * on its stream; gdsm_prof_read synchronises and returns the summed milliseconds and launch
+ * counts per stage (arrays of GDSM_PROF_STAGES), then clears them. */
+int gdsm_prof_enable(gdsm_ctx* ctx, int on);
+int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches);
+
+/* ---- synthetic inputs (SPEC §6) ------------------------------------------------------- */
+/* Fills the arenas named in `arenas` (bit 1<<GDSM_TWIN | 1<<GDSM_CURRENT | 1<<GDSM_REPLICA,
+ * 0 = all) for every page; arena page i has global id first_global + i * stride (stride 0 = 1).
+ * REPLICA gets the page's TWIN content. */
+int gdsm_gen_pages(gdsm_ctx* ctx, uint32_t arenas, uint64_t first_global, uint64_t stride,
+                   uint64_t seed, int mode, uint32_t ppm);
+int gdsm_gen_pages_raw(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint64_t n,
+                       uint64_t first_global, uint64_t stride, uint64_t seed, int mode,
+                       uint32_t ppm, void* stream);
+
+/* ---- twin / diff / apply (SPEC §2-4) ------------------------------------------------- */
+/* `ids` is a device array of n page ids, or NULL for the identity range [0, n). */
+int gdsm_twin(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n);
+/* Allocates a stream for n records with `cap` data bytes (cap 0: worst case n*10244). */
+int gdsm_runs_alloc(gdsm_ctx* ctx, uint64_t n, uint64_t cap, gdsm_runs* out);
+int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs);
+/* Diffs TWIN against CURRENT for the listed pages into `out` (out->n must be >= n; out->n is
+ * set to n). Asynchronous; use gdsm_runs_total to learn the size. */
+int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out);
+/* Synchronises, returns rec_off[n] in *total; -ENOSPC if it exceeded runs->cap. */
+int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total);
+/* Applies `in` to arena `target` (normally GDSM_REPLICA) for the listed pages (ids unique). */
+int gdsm_apply(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_runs* in);
+
+/* ---- raw entry points (caller-owned device memory, e.g. tensors; stream = hipStream_t) ---- */
+uint64_t gdsm_diff_workspace_bytes(uint64_t n);
+int gdsm_diff_raw(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
+                  uint64_t* rec_off, uint8_t* data, uint64_t cap, void* workspace,
+                  uint64_t workspace_bytes, void* stream);
+int gdsm_apply_raw(uint8_t* target, const uint32_t* ids, uint64_t n, const uint64_t* rec_off,
+                   const uint8_t* data, void* stream);
+int gdsm_twin_raw(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
+                  void* stream);
+
+/* ---- batched coherence (SPEC §5) ------------------------------------------------------- */
+/* Allocates and initialises the page table (state + faults) for n_nodes <= 8. */
+int gdsm_coh_init(gdsm_ctx* ctx, uint32_t n_nodes);
+/* Applies one batch of page-sorted events (device array). Synchronises and writes
+ * totals[10] = {invalidations, transfers, node_faults[8]}; -EINVAL if the batch is not sorted
+ * by page or names a page/node out of range (the page table is then unspecified). */
+int gdsm_coherence_batch(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_events,
+                         uint64_t* totals);
+/* Asynchronous variant: totals stay on the device (10 x u64, written at the end). */
+int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_events,
+                               uint64_t* totals_dev);
+int gdsm_coh_download(gdsm_ctx* ctx, uint32_t* state, uint32_t* faults);
+int gdsm_coh_upload(gdsm_ctx* ctx, const uint32_t* state, const uint32_t* faults);
+/* Fills events from per-page counts: offsets is a device array of n+1 exclusive-scan offsets. */
+int gdsm_gen_events(gdsm_ctx* ctx, uint64_t* events, const uint64_t* offsets, uint64_t first_page,
+                    uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct);
+
+/* ---- reference diff() (NW alignment), CPU ----------------------------------------------- */
+/* out1/out2 are allocated with the installed allocator (default malloc); *len = alignment
+ * length, which the legacy symbol cannot return. */
+int gdsm_nw_diff(const char* mem1, size_t mem1_len, char** out1, const char* mem2,
+                 size_t mem2_len, char** out2, size_t* len);
+/* Installs the allocator used for diff()/gdsm_nw_diff outputs: gallocy passes
+ * internal_malloc/internal_free so callers keep freeing with internal_free. */
+int gdsm_set_allocator(void* (*alloc_fn)(size_t), void (*free_fn)(void*));
+
+const char* gdsm_version(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+
+/* Legacy drop-in, C++ linkage, mangled _Z4diffPKcmRPcS0_mS2_ exactly like
+ * gallocy/include/gallocy/utils/diff.h:9-11. Bit-exact with the reference for
+ * mem1_len, mem2_len <= 1180 (the reference crashes beyond). Always returns 0. */
+int diff(const char* mem1, size_t mem1_len, char*& mem1_alignment, const char* mem2,
+         size_t mem2_len, char*& mem2_alignment);
+#endif
+
+#endif /* GDSM_H_ */

@@ -1,0 +1,128 @@
+"""ctypes wrapper of the C oracle (oracle/liboracle.so). TEST INFRASTRUCTURE ONLY: imported by
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the product."""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+REF_DRIVER = HERE / "_ref" / "ref_nw_driver"
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            subprocess.run(["make", "-s", "-C", str(HERE), "oracle"], check=True)
+        L = C.CDLL(str(LIB))
+        vp, u64 = C.c_void_p, C.c_uint64
+        L.or_hash3.restype = u64
+        L.or_hash3.argtypes = [u64, u64, u64]
+        L.or_gen_pages.argtypes = [vp, vp, vp, u64, u64, u64, u64, C.c_int, C.c_uint32]
+        L.or_diff_pages.restype = u64
+        L.or_diff_pages.argtypes = [vp, vp, vp, u64, vp, vp, u64]
+        L.or_apply.argtypes = [vp, vp, u64, vp, vp]
+        L.or_twin.argtypes = [vp, vp, vp, u64]
+        L.or_nw_diff.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p,
+                                 C.c_char_p, C.POINTER(C.c_size_t)]
+        L.or_coh_init.argtypes = [vp, vp, u64, C.c_uint32]
+        L.or_coherence.argtypes = [vp, vp, u64, vp, u64, vp]
+        L.or_gen_events.argtypes = [vp, vp, u64, u64, u64, C.c_uint32, C.c_uint32]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def gen_pages(n, seed, mode=0, ppm=10000, first_page=0, replica=False, stride=1):
+    twin = np.empty((n, 4096), np.uint8)
+    cur = np.empty((n, 4096), np.uint8)
+    rep = np.empty((n, 4096), np.uint8) if replica else None
+    lib().or_gen_pages(_p(twin), _p(cur), _p(rep), first_page, stride, n, seed, mode, ppm)
+    return (twin, cur, rep) if replica else (twin, cur)
+
+
+def diff_pages(twin, cur, ids=None, cap=None):
+    """Returns (rec_off uint64[n+1], data uint8[total])."""
+    n = len(ids) if ids is not None else twin.shape[0]
+    ids_a = None if ids is None else np.ascontiguousarray(ids, np.uint32)
+    rec_off = np.empty(n + 1, np.uint64)
+    if cap is None:
+        cap = n * 10244
+    data = np.empty(max(cap, 1), np.uint8)
+    total = lib().or_diff_pages(_p(np.ascontiguousarray(twin)), _p(np.ascontiguousarray(cur)),
+                                _p(ids_a), n, _p(rec_off), _p(data), cap)
+    return rec_off, data[:min(total, cap)].copy()
+
+
+def apply(target, rec_off, data, ids=None):
+    n = len(rec_off) - 1
+    ids_a = None if ids is None else np.ascontiguousarray(ids, np.uint32)
+    d = np.ascontiguousarray(data, np.uint8)
+    if d.size == 0:
+        d = np.zeros(1, np.uint8)
+    return lib().or_apply(_p(target), _p(ids_a), n, _p(np.ascontiguousarray(rec_off, np.uint64)), _p(d))
+
+
+def nw_diff(a: bytes, b: bytes):
+    n = len(a) + len(b) + 1
+    o1, o2 = C.create_string_buffer(n), C.create_string_buffer(n)
+    L = C.c_size_t(0)
+    rc = lib().or_nw_diff(a, len(a), b, len(b), o1, o2, C.byref(L))
+    assert rc == 0
+    return o1.raw[:L.value], o2.raw[:L.value]
+
+
+def coh_init(n_pages, n_nodes=8):
+    st = np.empty(n_pages, np.uint32)
+    fl = np.empty(n_pages, np.uint32)
+    lib().or_coh_init(_p(st), _p(fl), n_pages, n_nodes)
+    return st, fl
+
+
+def coherence(state, faults, events):
+    ev = np.ascontiguousarray(events, np.uint64)
+    tot = np.zeros(10, np.uint64)
+    rc = lib().or_coherence(_p(state), _p(faults), len(state), _p(ev) if len(ev) else None, len(ev), _p(tot))
+    return rc, {"invalidations": int(tot[0]), "transfers": int(tot[1]),
+                "node_faults": [int(x) for x in tot[2:]]}
+
+
+def gen_events(counts, seed, n_nodes=8, write_pct=20, first_page=0):
+    counts = np.ascontiguousarray(counts, np.uint64)
+    offs = np.zeros(len(counts) + 1, np.uint64)
+    np.cumsum(counts, out=offs[1:])
+    ev = np.empty(int(offs[-1]), np.uint64)
+    lib().or_gen_events(_p(ev) if len(ev) else None, _p(offs), first_page, len(counts), seed, n_nodes, write_pct)
+    return ev
+
+
+def ref_available() -> bool:
+    return REF_DRIVER.exists()
+
+
+def ref_nw_batch(cases):
+    """Runs the REFERENCE diff() (oracle/_ref) on [(a, b)] (no NUL bytes) -> [(out1, out2)]."""
+    import struct
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        cin, cout = Path(d) / "in.bin", Path(d) / "out.bin"
+        with open(cin, "wb") as f:
+            for a, b in cases:
+                f.write(struct.pack("<II", len(a), len(b)) + a + b)
+        subprocess.run([str(REF_DRIVER), "run", str(cin), str(cout)], check=True)
+        raw = cout.read_bytes()
+    out, i = [], 0
+    while i < len(raw):
+        (L,) = struct.unpack_from("<I", raw, i)
+        i += 4
+        out.append((raw[i:i + L], raw[i + L:i + 2 * L]))
+        i += 2 * L
+    return out

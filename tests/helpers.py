@@ -1,0 +1,82 @@
+"""Shared test helpers: independent pure-numpy restatements used to cross-check the C oracle."""
+from __future__ import annotations
+
+import numpy as np
+
+
+def np_runs(twin_page: np.ndarray, cur_page: np.ndarray):
+    """Maximal runs of differing bytes, by numpy (independent of oracle/gdsm_oracle.c)."""
+    d = (twin_page != cur_page).astype(np.int8)
+    edges = np.diff(np.concatenate([[0], d, [0]]))
+    starts = np.flatnonzero(edges == 1)
+    ends = np.flatnonzero(edges == -1)
+    return [(int(s), int(e - s)) for s, e in zip(starts, ends)]
+
+
+def np_record(twin_page, cur_page) -> bytes:
+    runs = np_runs(twin_page, cur_page)
+    if not runs:
+        return b""
+    hdr = np.array([o | (ln << 16) for o, ln in runs], "<u4").tobytes()
+    pay = b"".join(cur_page[o:o + ln].tobytes() for o, ln in runs)
+    pay += b"\0" * ((-len(pay)) % 4)
+    return np.array([len(runs)], "<u4").tobytes() + hdr + pay
+
+
+def np_diff(twin, cur, ids=None):
+    ids = range(twin.shape[0]) if ids is None else ids
+    recs = [np_record(twin[p], cur[p]) for p in ids]
+    off = np.zeros(len(recs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(r) for r in recs])
+    return off, np.frombuffer(b"".join(recs), np.uint8)
+
+
+def mix64(z):
+    M = (1 << 64) - 1
+    z ^= z >> 30
+    z = (z * 0xBF58476D1CE4E5B9) & M
+    z ^= z >> 27
+    z = (z * 0x94D049BB133111EB) & M
+    z ^= z >> 31
+    return z
+
+
+def hash3(s, a, b):
+    M = (1 << 64) - 1
+    return mix64((mix64(s ^ ((a * 0x9E3779B97F4A7C15) & M)) + b * 0xC2B2AE3D27D4EB4F + 0x165667B19E3779F9) & M)
+
+
+def py_coherence(state, faults, events, n_pages):
+    """Pure-Python sequential fold of docs/SPEC.md §5 (small cases only)."""
+    tot = [0] * 10
+    for e in events.tolist():
+        p, node, wr = e >> 4, (e >> 1) & 7, e & 1
+        s = int(state[p])
+        cs, owner, st, dirty = s & 0xFF, (s >> 8) & 0xFF, (s >> 16) & 3, (s >> 18) & 1
+        bit = 1 << node
+        if not wr:
+            if not cs & bit:
+                faults[p] += 1
+                tot[2 + node] += 1
+                cs |= bit
+                if st == 2:
+                    st = 1
+        else:
+            dirty = 1
+            if not (st == 2 and owner == node):
+                faults[p] += 1
+                tot[2 + node] += 1
+                tot[0] += bin(cs & ~bit).count("1")
+                tot[1] += owner != node
+            owner, cs, st = node, bit, 2
+        state[p] = cs | (owner << 8) | (st << 16) | (dirty << 18)
+    return tot
+
+
+def zipf_counts(n_pages, total, s=0.8, seed=0):
+    """Per-page event counts ~ Zipf(s) over a seeded page permutation (host side, float64)."""
+    rng = np.random.default_rng(seed)
+    ranks = rng.permutation(n_pages) + 1
+    w = ranks.astype(np.float64) ** (-s)
+    w /= w.sum()
+    return rng.multinomial(total, w).astype(np.uint64)

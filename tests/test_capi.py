@@ -1,0 +1,99 @@
+"""CPU checks of the C-ABI boundary (no GPU compute): libgdsm.so loads, exports every entry point
+include/gdsm.h declares plus the legacy C++ `diff` symbol, and fails cleanly without a GPU."""
+import ctypes as C
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "gdsm.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gdsm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_header():
+    from gallocy_amd import _lib
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+
+
+@pytest.mark.skipif(shutil.which("nm") is None, reason="nm missing")
+def test_legacy_diff_symbol_has_reference_mangling():
+    from gallocy_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], check=True,
+                         capture_output=True, text=True).stdout
+    # gallocy/include/gallocy/utils/diff.h:9-11, mangled name measured in SURVEY §8b
+    assert re.search(r"\bT _Z4diffPKcmRPcS0_mS2_\b", out)
+    for n in declared_functions():
+        assert re.search(rf"\bT {n}\b", out), n
+
+
+def test_legacy_diff_through_cxx_symbol():
+    """Calls the C++-linkage `diff` exactly as test/test_diff.cpp does (char*& out-params)."""
+    from gallocy_amd import _lib
+    lib = _lib.load()
+    fn = getattr(lib, _lib.LEGACY_DIFF_SYMBOL)
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_char_p), C.c_char_p, C.c_size_t,
+                   C.POINTER(C.c_char_p)]
+    for a, b, o1, o2 in [(b"GGAATGG", b"ATG", b"GGAATGG", b"---AT-G"),
+                         (b"FOO BOP BOOP", b"FOOO BOOP BOP", b"F-OO B-OP BOOP", b"FOOO BOOP B-OP")]:
+        r1, r2 = C.c_char_p(), C.c_char_p()
+        assert fn(a, len(a), C.byref(r1), b, len(b), C.byref(r2)) == 0
+        assert (r1.value, r2.value) == (o1, o2)
+
+
+def test_nw_diff_matches_reference_vectors(golden):
+    import gallocy_amd as ga
+    g = golden["nw_ref"]
+    blob = g["blob"].tobytes()
+    i = 0
+    for n, m, L in g["lens"]:
+        a, b = blob[i:i + n], blob[i + n:i + n + m]
+        i += n + m
+        assert ga.diff(a, b) == (blob[i:i + L], blob[i + L:i + 2 * L])
+        i += 2 * L
+
+
+def test_nw_diff_beyond_reference_limit():
+    """The reference crashes from 1181 B on; ours aligns a whole 4 KiB page."""
+    import gallocy_amd as ga
+    rng = np.random.default_rng(3)
+    a = bytes(rng.integers(1, 256, 4096, dtype=np.uint8))
+    b = bytearray(a)
+    b[100] ^= 0x11
+    b[2000:2003] = b"xyz"
+    o1, o2 = ga.diff(a, bytes(b))
+    assert o1 == a and o2 == bytes(b)
+
+
+def test_no_gpu_is_reported_not_crashed():
+    from gallocy_amd import _lib
+    lib = _lib.load()
+    n = C.c_int(-1)
+    rc = lib.gdsm_device_count(C.byref(n))
+    if n.value > 0:
+        pytest.skip("a GPU is visible")
+    assert rc in (0, -19) and n.value == 0
+    h = C.c_void_p()
+    assert lib.gdsm_init(C.byref(h), 0, 16, 0) == -19  # -ENODEV
+    assert lib.gdsm_sync(None) == -22
+
+
+def test_workspace_sizing():
+    from gallocy_amd import _lib
+    lib = _lib.load()
+    assert lib.gdsm_diff_workspace_bytes(1) >= 10244
+    assert lib.gdsm_diff_workspace_bytes(1 << 24) == lib.gdsm_diff_workspace_bytes(1 << 20)

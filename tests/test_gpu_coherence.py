@@ -1,0 +1,112 @@
+"""GPU parity of the batched page-coherence state machine (docs/SPEC.md §5) against the C oracle
+fold, through the C-ABI. Bit-exact: page-table words, per-page faults and the batch totals."""
+import numpy as np
+import pytest
+
+import gallocy_amd as ga
+from gallocy_amd.gdsm import GdsmError
+from oracle import oracle
+from tests.helpers import zipf_counts
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_both(n_pages, batches, n_nodes=8):
+    with ga.Context(n_pages, arenas=()) as c:
+        c.coh_init(n_nodes)
+        st, fl = oracle.coh_init(n_pages, n_nodes)
+        for ev in batches:
+            tot = c.coherence_batch(ev)
+            rc, otot = oracle.coherence(st, fl, ev)
+            assert rc == 0
+            assert tot == otot
+        gst, gfl = c.coh_download()
+        assert np.array_equal(gst, st), np.flatnonzero(gst != st)[:10]
+        assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
+
+
+def test_golden_batch(golden):
+    g = golden["coherence"]
+    with ga.Context(64, arenas=()) as c:
+        c.coh_init(8)
+        tot = c.coherence_batch(g["events"])
+        assert [tot["invalidations"], tot["transfers"], *tot["node_faults"]] == g["totals"].tolist()
+        st, fl = c.coh_download()
+        assert np.array_equal(st, g["state"]) and np.array_equal(fl, g["faults"])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_uniform_counts(seed):
+    rng = np.random.default_rng(seed)
+    n = 20000
+    counts = rng.integers(0, 30, n).astype(np.uint64)
+    ev = oracle.gen_events(counts, seed=seed, write_pct=20)
+    _run_both(n, [ev])
+
+
+def test_zipf_with_pages_spanning_many_blocks():
+    n = 50000
+    counts = zipf_counts(n, 400000, s=0.8, seed=4)
+    counts[17] = 50000  # a hot page spanning ~12 blocks of 4096 events
+    ev = oracle.gen_events(counts, seed=9, write_pct=20)
+    _run_both(n, [ev])
+
+
+def test_block_boundary_alignment_and_write_mix():
+    n = 64
+    for counts in ([4096, 4096, 1, 4095, 4097], [1] * 5000, [8191, 0, 0, 1]):
+        cts = np.zeros(n, np.uint64)
+        cts[:len(counts)] = counts
+        for wp in (0, 50, 100):
+            ev = oracle.gen_events(cts, seed=len(counts) + wp, write_pct=wp)
+            _run_both(n, [ev])
+
+
+def test_multi_batch_persistence_and_fewer_nodes():
+    n = 3000
+    rng = np.random.default_rng(8)
+    batches = []
+    for b in range(4):
+        counts = rng.integers(0, 12, n).astype(np.uint64)
+        batches.append(oracle.gen_events(counts, seed=100 + b, n_nodes=3, write_pct=30))
+    _run_both(n, batches, n_nodes=3)
+
+
+def test_single_and_empty_batches():
+    _run_both(10, [np.array([(4 << 4) | (3 << 1) | 1], np.uint64), np.zeros(0, np.uint64)])
+
+
+def test_unsorted_batch_is_rejected():
+    with ga.Context(16, arenas=()) as c:
+        c.coh_init(8)
+        with pytest.raises(GdsmError) as ei:
+            c.coherence_batch(np.array([5 << 4, 2 << 4], np.uint64))
+        assert ei.value.errno == 22
+        with pytest.raises(GdsmError):
+            c.coherence_batch(np.array([99 << 4], np.uint64))  # page out of range
+
+
+def test_device_event_generation_matches_oracle():
+    n = 4000
+    counts = zipf_counts(n, 60000, seed=2)
+    with ga.Context(n, arenas=()) as c:
+        ev = c.gen_events(counts, seed=21, n_nodes=8, write_pct=20)
+        got = ev.download(np.uint64, ev.count)
+    assert np.array_equal(got, oracle.gen_events(counts, seed=21, n_nodes=8, write_pct=20))
+
+
+def test_config4_scaled_parity():
+    """Config 4 shape (Zipf 0.8 over the pages, 8 nodes, 20 % writes) at 1M pages x 16M events,
+    generated on the device, checked against the oracle fold of the same events."""
+    n = 1 << 20
+    counts = zipf_counts(n, 16 << 20, s=0.8, seed=44)
+    with ga.Context(n, arenas=()) as c:
+        ev = c.gen_events(counts, seed=44)
+        c.coh_init(8)
+        tot = c.coherence_batch(ev)
+        host_ev = ev.download(np.uint64, ev.count)
+        gst, gfl = c.coh_download()
+    st, fl = oracle.coh_init(n, 8)
+    rc, otot = oracle.coherence(st, fl, host_ev)
+    assert rc == 0 and tot == otot
+    assert np.array_equal(gst, st) and np.array_equal(gfl, fl)

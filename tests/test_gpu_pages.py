@@ -1,0 +1,252 @@
+"""GPU parity of the page hot path (twin / run diff / apply) against the C oracle, through the
+C-ABI (libgdsm.so). Bit-exact: this is byte work, docs/SPEC.md §2-4."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import gallocy_amd as ga
+from gallocy_amd import _lib
+from gallocy_amd.gdsm import GdsmError, HostRuns, Runs
+from oracle import oracle
+from tests.helpers import np_diff
+
+pytestmark = pytest.mark.gpu
+
+
+def _eq_runs(host: HostRuns, ro, data):
+    assert np.array_equal(host.rec_off, ro), "rec_off differs"
+    assert np.array_equal(host.data, data), "data differs"
+
+
+@pytest.fixture(scope="module")
+def ctx64():
+    with ga.Context(64) as c:
+        yield c
+
+
+def test_gen_matches_oracle(ctx64):
+    ctx64.gen_pages(seed=1, mode=ga.GEN_UNIFORM, ppm=10000, first_global=7)
+    ctx64.sync()
+    t, c, r = oracle.gen_pages(64, seed=1, mode=0, ppm=10000, first_page=7, replica=True)
+    assert np.array_equal(ctx64.download("twin"), t)
+    assert np.array_equal(ctx64.download("current"), c)
+    assert np.array_equal(ctx64.download("replica"), r)
+    ctx64.gen_pages(seed=4, mode=ga.GEN_CLUSTERED, ppm=100000, first_global=1 << 30)
+    t, c = oracle.gen_pages(64, seed=4, mode=1, ppm=100000, first_page=1 << 30)
+    assert np.array_equal(ctx64.download("current"), c)
+
+
+def test_config1_diff_apply_bit_exact(ctx64, golden):
+    """BASELINE config 1 (64 x 4 KiB, 1 % word writes, seed 1) on the GPU."""
+    ctx64.gen_pages(seed=1, mode=ga.GEN_UNIFORM, ppm=10000)
+    runs = ctx64.diff()
+    h = runs.to_host()
+    _eq_runs(h, golden["pages"]["c1_rec_off"], golden["pages"]["c1_data"])
+    ctx64.apply(runs)
+    ctx64.sync()
+    assert np.array_equal(ctx64.download("replica"), ctx64.download("current"))
+    runs.free()
+
+
+def test_edge_pages_golden(golden):
+    g = golden["pages"]
+    n = g["edge_twin"].shape[0]
+    with ga.Context(n) as c:
+        c.upload("twin", g["edge_twin"])
+        c.upload("current", g["edge_cur"])
+        c.upload("replica", g["edge_twin"])
+        runs = c.diff()
+        _eq_runs(runs.to_host(), g["edge_rec_off"], g["edge_data"])
+        c.apply(runs)
+        c.sync()
+        assert np.array_equal(c.download("replica"), g["edge_cur"])
+
+
+@pytest.mark.parametrize("density", [0.001, 0.05, 0.3, 0.5, 0.9, 1.0])
+def test_random_byte_density(density):
+    rng = np.random.default_rng(int(density * 1000) + 1)
+    n = 700  # not a multiple of the 64-page block
+    twin = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    cur = twin.copy()
+    mask = rng.random((n, 4096)) < density
+    cur[mask] ^= rng.integers(1, 256, int(mask.sum()), dtype=np.uint8)
+    with ga.Context(n) as c:
+        c.upload("twin", twin)
+        c.upload("current", cur)
+        c.upload("replica", twin)
+        runs = c.diff()
+        ro, data = oracle.diff_pages(twin, cur)
+        _eq_runs(runs.to_host(), ro, data)
+        c.apply(runs)
+        c.sync()
+        assert np.array_equal(c.download("replica"), cur)
+
+
+def test_page_id_lists_and_duplicates():
+    n = 300
+    t, cur = oracle.gen_pages(n, seed=8, mode=1, ppm=100000)
+    rng = np.random.default_rng(5)
+    ids = rng.integers(0, n, 513).astype(np.uint32)  # duplicates allowed for diff (read only)
+    with ga.Context(n) as c:
+        c.upload("twin", t)
+        c.upload("current", cur)
+        d_ids = c.ids(ids)
+        runs = c.diff(d_ids)
+        ro, data = oracle.diff_pages(t, cur, ids=ids)
+        _eq_runs(runs.to_host(), ro, data)
+        # apply needs unique ids: apply a permutation into CURRENT-shaped replica
+        perm = rng.permutation(n).astype(np.uint32)
+        d_perm = c.ids(perm)
+        runs2 = c.diff(d_perm)
+        c.upload("replica", t)
+        c.apply(runs2, "replica", d_perm)
+        c.sync()
+        assert np.array_equal(c.download("replica"), cur)
+        # twin(ids): snapshot only the listed pages
+        few = np.array([3, 10, 299], np.uint32)
+        c.twin(c.ids(few))
+        c.sync()
+        tw = c.download("twin")
+        assert np.array_equal(tw[few], cur[few])
+        rest = np.setdiff1d(np.arange(n), few)
+        assert np.array_equal(tw[rest], t[rest])
+
+
+def test_chunked_diff_small_workspace():
+    """The diff loops over chunks when its workspace is small (raw C-ABI entry point)."""
+    n = 1000
+    t, cur = oracle.gen_pages(n, seed=12, mode=0, ppm=40000)
+    L = _lib.load()
+    with ga.Context(n) as c:
+        c.upload("twin", t)
+        c.upload("current", cur)
+        ws_bytes = L.gdsm_diff_workspace_bytes(128)
+        ws = c.buffer(ws_bytes)
+        ro_buf = c.buffer((n + 1) * 8)
+        cap = n * 2048
+        data_buf = c.buffer(cap)
+        rc = L.gdsm_diff_raw(c.arena_ptr("twin"), c.arena_ptr("current"), None, n, ro_buf.ptr,
+                             data_buf.ptr, cap, ws.ptr, ws_bytes, c.stream)
+        assert rc == 0
+        c.sync()
+        ro_h = ro_buf.download(np.uint64, n + 1)
+        ro, data = oracle.diff_pages(t, cur)
+        assert np.array_equal(ro_h, ro)
+        assert np.array_equal(data_buf.download(np.uint8, int(ro[-1])), data)
+
+
+def test_capacity_overflow_reports_enospc():
+    n = 64
+    t, cur = oracle.gen_pages(n, seed=3, mode=1, ppm=300000)
+    with ga.Context(n) as c:
+        c.upload("twin", t)
+        c.upload("current", cur)
+        ro, data = oracle.diff_pages(t, cur)
+        cap = int(ro[n // 2]) + 16
+        runs = c.diff(cap=cap)
+        with pytest.raises(GdsmError) as ei:
+            runs.total()
+        assert ei.value.errno == 28
+        got = np.empty(n + 1, np.uint64)
+        L = _lib.load()
+        assert L.gdsm_memcpy_d2h(c.handle, got.ctypes.data, runs.s.rec_off, got.nbytes) == 0
+        assert np.array_equal(got, ro)  # rec_off is complete even when data overflowed
+
+
+def test_apply_rejects_malformed_stream():
+    n = 8
+    t, cur = oracle.gen_pages(n, seed=2, mode=0, ppm=50000)
+    ro, data = oracle.diff_pages(t, cur)
+    bad = data.copy()
+    i = int(np.flatnonzero(np.diff(ro))[0])
+    bad[int(ro[i]):int(ro[i]) + 4] = np.frombuffer(np.uint32(4000).tobytes(), np.uint8)  # nruns
+    with ga.Context(n) as c:
+        c.upload("replica", t)
+        r = Runs.from_host(c, HostRuns(ro, bad))
+        c.apply(r)
+        with pytest.raises(GdsmError) as ei:
+            c.sync()
+        assert ei.value.errno == 22
+        # the good records were still applied; the bad page was left alone
+        rep = c.download("replica")
+        good = [k for k in range(n) if k != i and ro[k + 1] > ro[k]]
+        assert np.array_equal(rep[good], cur[good])
+        assert np.array_equal(rep[i], t[i])
+
+
+def test_empty_batch():
+    with ga.Context(4) as c:
+        runs = c.diff(n=0)
+        assert runs.total() == 0
+        c.apply(runs)
+        c.sync()
+
+
+def _sample_parity(c, n, seed, mode, ppm, k=64):
+    """Diff of a random sample of pages (by id) equals the oracle on the same global pages."""
+    rng = np.random.default_rng(seed)
+    ids = np.sort(rng.choice(n, k, replace=False)).astype(np.uint32)
+    runs = c.diff(c.ids(ids), cap=k * 10244)
+    h = runs.to_host()
+    for j, p in enumerate(ids):
+        t, cur = oracle.gen_pages(1, seed=seed, mode=mode, ppm=ppm, first_page=int(p))
+        ro, data = oracle.diff_pages(t, cur)
+        assert h.record(j) == data.tobytes()
+    runs.free()
+
+
+def test_config2_full_size_properties():
+    """BASELINE config 2 at full size: 1M pages, 1 % word writes. Size-independent checks:
+    sampled records equal the oracle, apply makes REPLICA == CURRENT (diff(REPLICA, CURRENT) is
+    empty), a second apply is idempotent, and twin() empties the diff."""
+    n = 1 << 20
+    L = _lib.load()
+    with ga.Context(n) as c:
+        c.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+        runs = c.diff(cap=256 << 20)
+        total = runs.total()
+        # E|D| ~ 61 B/page at this density
+        assert 50 * n < total < 72 * n
+        ro = np.empty(n + 1, np.uint64)
+        assert L.gdsm_memcpy_d2h(c.handle, ro.ctypes.data, runs.s.rec_off, ro.nbytes) == 0
+        assert ro[0] == 0 and np.all(np.diff(ro.astype(np.int64)) >= 0) and ro[-1] == total
+        assert np.all(np.diff(ro) % 4 == 0)
+        dirty = int((np.diff(ro) > 0).sum())
+        assert abs(dirty / n - (1 - 0.99 ** 512)) < 0.002  # 99.4 % of pages dirty
+        c.apply(runs)
+        c.apply(runs)
+        c.sync()
+        chk = ga.Runs(c, n, cap=1 << 20)
+        ws = c.buffer(L.gdsm_diff_workspace_bytes(n))
+        rc = L.gdsm_diff_raw(c.arena_ptr("replica"), c.arena_ptr("current"), None, n,
+                             chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes, c.stream)
+        assert rc == 0 and chk.total() == 0
+        _sample_parity(c, n, 2026, 0, 10000)
+        c.twin()
+        assert c.diff(cap=1 << 20).total() == 0
+
+
+def test_config3_shard_properties():
+    """BASELINE config 3 shard shape (2M pages = 16M / 8 GPUs, clustered 10 %), one GPU."""
+    n = 2 << 20
+    with ga.Context(n) as c:
+        c.gen_pages(seed=77, mode=ga.GEN_CLUSTERED, ppm=100000, first_global=3 * n)
+        runs = c.diff(cap=2 << 30)
+        total = runs.total()
+        assert 300 * n < total < 600 * n
+        c.apply(runs)
+        c.sync()
+        L = _lib.load()
+        chk = ga.Runs(c, n, cap=1 << 20)
+        ws = c.buffer(L.gdsm_diff_workspace_bytes(n))
+        assert L.gdsm_diff_raw(c.arena_ptr("replica"), c.arena_ptr("current"), None, n,
+                               chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes,
+                               c.stream) == 0
+        assert chk.total() == 0
+        rng = np.random.default_rng(1)
+        ids = np.sort(rng.choice(n, 32, replace=False)).astype(np.uint32)
+        h = c.diff(c.ids(ids), cap=32 * 10244).to_host()
+        for j, p in enumerate(ids):
+            t, cur = oracle.gen_pages(1, seed=77, mode=1, ppm=100000, first_page=3 * n + int(p))
+            assert h.record(j) == oracle.diff_pages(t, cur)[1].tobytes()
