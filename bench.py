@@ -54,7 +54,7 @@ def payload_bytes(rec_off: np.ndarray, data: np.ndarray) -> int:
     if len(dirty) == 0:
         return 0
     w = data.view("<u4") if len(data) % 4 == 0 else np.frombuffer(data.tobytes(), "<u4")
-    starts = rec_off[dirty] // 4
+    starts = (rec_off[dirty] // 4).astype(np.int64)
     nr = w[starts].astype(np.int64)
     first_hdr = np.repeat(starts + 1, nr)
     within = np.arange(nr.sum()) - np.repeat(np.cumsum(nr) - nr, nr)

@@ -86,6 +86,11 @@ extern "C" {
 
 const char* gdsm_version(void) { return "gdsm 0.1.0 (gfx950)"; }
 
+int gdsm_tune(const char* key, int64_t value) {
+  if (!key) return -EINVAL;
+  return gdsm::tune(key, value) == 0 ? 0 : -EINVAL;
+}
+
 int gdsm_device_count(int* count) {
   if (!count) return -EINVAL;
   *count = 0;

@@ -21,22 +21,51 @@ __device__ __forceinline__ uint4 ld_nt16(const void* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// ---- wave64 cross-lane primitives on DPP (VALU, no LDS traffic) -------------------------
+// gfx9-family DPP controls: row_shr:n = 0x110+n, row_bcast:15 = 0x142, row_bcast:31 = 0x143,
+// wave_shl:1 = 0x130, wave_shr:1 = 0x138. Lanes whose source is out of range (or whose row is
+// masked off) read 0, which is the identity of every scan below.
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xF, false);
+}
+
 // Inclusive prefix sum across the 64 lanes of a wave.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += t;
-  }
-  return v;
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += dpp0<0x111>(x);
+  x += dpp0<0x112>(x);
+  x += dpp0<0x114>(x);
+  x += dpp0<0x118>(x);
+  x += dpp0<0x142, 0xA>(x);
+  x += dpp0<0x143, 0xC>(x);
+  return x;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-  return __shfl(wave_incl_sum(v), 63, 64);
+// Inclusive prefix maximum across lanes (values >= 0; 0 is the identity).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  x = max(x, dpp0<0x111>(x));
+  x = max(x, dpp0<0x112>(x));
+  x = max(x, dpp0<0x114>(x));
+  x = max(x, dpp0<0x118>(x));
+  x = max(x, dpp0<0x142, 0xA>(x));
+  x = max(x, dpp0<0x143, 0xC>(x));
+  return x;
 }
 
-// Inclusive suffix minimum across lanes (lane l gets min over lanes >= l).
+__device__ __forceinline__ uint32_t lane_bcast(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint64_t lane_bcast64(uint64_t v, int lane) {
+  return (uint64_t)lane_bcast((uint32_t)v, lane) | ((uint64_t)lane_bcast((uint32_t)(v >> 32), lane) << 32);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_bcast(wave_incl_sum(v), 63); }
+
+// Value of lane l-1 (lane 0 gets 0) / of lane l+1 (lane 63 gets 0).
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) { return dpp0<0x138>(v); }
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) { return dpp0<0x130>(v); }
+
+// Inclusive suffix minimum across lanes (lane l gets min over lanes >= l); bpermute based.
 __device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v) {
   const uint32_t lane = lane_id();
 #pragma unroll

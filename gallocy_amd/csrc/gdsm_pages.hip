@@ -17,6 +17,9 @@
 #include "gdsm_common.h"
 #include "gdsm_launch.h"
 
+#include <stdlib.h>
+#include <string.h>
+
 namespace gdsm {
 
 // ------------------------------------------------------------------------- synthetic pages
@@ -95,19 +98,21 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, uint32_t b) {
   return (uint32_t)(h >> ((b & 7u) * 8)) & 0xFFu;
 }
 
-// Writes the headers of the runs starting in chunk `ch` and the chunk's changed bytes.
-// (Called once per k with scalars, so no per-thread array is ever indexed at run time.)
+// Writes the headers of the runs ENDING in chunk `ch` and the chunk's changed bytes. A run's
+// start is the last run start at or before its end: inside this chunk, or `ps` - 1 where `ps` is
+// the exclusive prefix maximum of (last start + 1) over the earlier chunks. (Called once per k
+// with scalars, so no per-thread array is ever indexed at run time.)
 __device__ __forceinline__ void emit_chunk(uint32_t ch, uint32_t s, uint32_t e, uint32_t m,
-                                           uint32_t ne, uint32_t excl, const uint4 c,
+                                           uint32_t ps, uint32_t excl, const uint4 c,
                                            uint32_t* __restrict__ hdr, uint8_t* __restrict__ pay) {
   const uint32_t pos = ch * 16u;
   uint32_t r = excl & 0xFFFFu;
-  while (s) {
-    const uint32_t b = (uint32_t)__builtin_ctz(s);
-    s &= s - 1;
-    const uint32_t later = (e >> b) << b;
-    const uint32_t end = later ? pos + (uint32_t)__builtin_ctz(later) : ne;
-    hdr[r++] = (pos + b) | ((end - pos - b + 1u) << 16);
+  while (e) {
+    const uint32_t b = (uint32_t)__builtin_ctz(e);
+    e &= e - 1;
+    const uint32_t upto = s & ((2u << b) - 1u);
+    const uint32_t start = upto ? pos + 31u - (uint32_t)__builtin_clz(upto) : ps - 1u;
+    hdr[r++] = start | ((pos + b - start + 1u) << 16);
   }
   uint32_t q = excl >> 16;
   while (m) {
@@ -117,79 +122,95 @@ __device__ __forceinline__ void emit_chunk(uint32_t ch, uint32_t s, uint32_t e, 
   }
 }
 
+__device__ __forceinline__ void load_page(const uint8_t* __restrict__ twin,
+                                          const uint8_t* __restrict__ cur, uint64_t p,
+                                          uint32_t lane, uint4 (&t)[4], uint4 (&c)[4]) {
+  const uint4* T = reinterpret_cast<const uint4*>(twin + p * kPage);
+  const uint4* C = reinterpret_cast<const uint4*>(cur + p * kPage);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    t[k] = ld_nt16(T + k * 64 + lane);
+    c[k] = ld_nt16(C + k * 64 + lane);
+  }
+}
+
+// Diffs one page held in registers (chunk (k, lane) = bytes [(64k + lane) * 16, +16), page
+// order = (k, lane)); writes its record to `out` and returns the record size (wave-uniform).
+__device__ __forceinline__ uint32_t diff_one(const uint4 (&t)[4], const uint4 (&c)[4],
+                                             uint32_t lane, uint8_t* __restrict__ out) {
+  uint32_t m[4], s[4], e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m[k] = diffmask16(t[k], c[k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // neighbour chunks' edge bytes: lane-1 / lane+1 of the same k, wrapping across k
+    uint32_t up = from_prev_lane(m[k]);
+    uint32_t dn = from_next_lane(m[k]);
+    if (k > 0 && lane == 0) up = lane_bcast(m[k > 0 ? k - 1 : 0], 63);
+    if (k < 3 && lane == 63) dn = lane_bcast(m[k < 3 ? k + 1 : 3], 0);
+    s[k] = m[k] & ~((m[k] << 1) | ((up >> 15) & 1u)) & 0xFFFFu;   // first byte of a run
+    e[k] = m[k] & ~((m[k] >> 1) | ((dn & 1u) << 15)) & 0xFFFFu;   // last byte of a run
+  }
+  // Ranks: runs (counted at their ends) in the low 16 bits, payload bytes in the high 16.
+  uint32_t excl[4], ps[4], carry = 0, cmax = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t v = (uint32_t)__popc(e[k]) | ((uint32_t)__popc(m[k]) << 16);
+    const uint32_t inc = wave_incl_sum(v);
+    excl[k] = carry + inc - v;
+    carry += lane_bcast(inc, 63);
+    const uint32_t pos = (uint32_t)(k * 64 + lane) * 16u;
+    const uint32_t ls = s[k] ? pos + 32u - (uint32_t)__builtin_clz(s[k]) : 0u;  // last start + 1
+    const uint32_t mx = wave_incl_max(ls);
+    ps[k] = max(cmax, from_prev_lane(mx));
+    cmax = max(cmax, lane_bcast(mx, 63));
+  }
+  const uint32_t NR = carry & 0xFFFFu, NP = carry >> 16;
+  if (NR == 0) return 0;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(out + 4);
+  uint8_t* pay = out + 4 + 4 * NR;
+  if (lane == 0) {
+    *reinterpret_cast<uint32_t*>(out) = NR;
+    for (uint32_t q = NP; q & 3u; ++q) pay[q] = 0;  // zero padding
+  }
+  emit_chunk(0 * 64 + lane, s[0], e[0], m[0], ps[0], excl[0], c[0], hdr, pay);
+  emit_chunk(1 * 64 + lane, s[1], e[1], m[1], ps[1], excl[1], c[1], hdr, pay);
+  emit_chunk(2 * 64 + lane, s[2], e[2], m[2], ps[2], excl[2], c[2], hdr, pay);
+  emit_chunk(3 * 64 + lane, s[3], e[3], m[3], ps[3], excl[3], c[3], hdr, pay);
+  return 4u + 4u * NR + ((NP + 3u) & ~3u);
+}
+
+// One workgroup = 4 waves = kDiffPagesPerBlock consecutive pages (wave w takes w, w+4, ...).
+// kPrefetch: the next page's 8 loads are issued before the current page is processed.
+template <bool kPrefetch>
 __global__ __launch_bounds__(256) void diff_pages_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
   __shared__ uint32_t wsum[4];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock;
   uint32_t acc = 0;
+  uint4 t[4], c[4];
+  if (kPrefetch && b0 + wave < n)
+    load_page(twin, cur, ids ? ids[first + b0 + wave] : first + b0 + wave, lane, t, c);
   for (uint32_t j = wave; j < kDiffPagesPerBlock; j += 4) {
-    const uint64_t i = (uint64_t)blockIdx.x * kDiffPagesPerBlock + j;  // index within chunk
+    const uint64_t i = b0 + j;  // index within chunk
     if (i >= n) break;
-    const uint64_t p = ids ? ids[first + i] : first + i;
-    const uint4* T = reinterpret_cast<const uint4*>(twin + p * kPage);
-    const uint4* C = reinterpret_cast<const uint4*>(cur + p * kPage);
-    uint4 t[4], c[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      t[k] = ld_nt16(T + k * 64 + lane);
-      c[k] = ld_nt16(C + k * 64 + lane);
-    }
-    // Chunk (k, lane) covers bytes [(64k + lane) * 16, +16): page order = (k, lane).
-    uint32_t m[4], s[4], e[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) m[k] = diffmask16(t[k], c[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t up = __shfl_up(m[k], 1, 64);
-      const uint32_t dn = __shfl_down(m[k], 1, 64);
-      const uint32_t wrap_prev = (k > 0) ? __shfl(m[k > 0 ? k - 1 : 0], 63, 64) : 0u;
-      const uint32_t wrap_next = (k < 3) ? __shfl(m[k < 3 ? k + 1 : 3], 0, 64) : 0u;
-      const uint32_t prev_top = ((lane == 0 ? wrap_prev : up) >> 15) & 1u;
-      const uint32_t next_low = (lane == 63 ? wrap_next : dn) & 1u;
-      s[k] = m[k] & ~((m[k] << 1) | prev_top) & 0xFFFFu;           // first byte of a run
-      e[k] = m[k] & ~((m[k] >> 1) | (next_low << 15)) & 0xFFFFu;   // last byte of a run
-    }
-    // Packed counts: runs in the low 16 bits, payload bytes in the high 16 (totals <= 4096).
-    uint32_t excl[4], carry = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t v = (uint32_t)__popc(s[k]) | ((uint32_t)__popc(m[k]) << 16);
-      const uint32_t inc = wave_incl_sum(v);
-      excl[k] = carry + inc - v;
-      carry += __shfl(inc, 63, 64);
-    }
-    const uint32_t NR = carry & 0xFFFFu, NP = carry >> 16;
-    const uint32_t size = NR ? 4u + 4u * NR + ((NP + 3u) & ~3u) : 0u;
+    if (!kPrefetch) load_page(twin, cur, ids ? ids[first + i] : first + i, lane, t, c);
+    uint4 tn[4], cn[4];
+    const bool nx = kPrefetch && j + 4 < kDiffPagesPerBlock && i + 4 < n;
+    if (nx) load_page(twin, cur, ids ? ids[first + i + 4] : first + i + 4, lane, tn, cn);
+    const uint32_t size = diff_one(t, c, lane, ws + i * kRecSlot);
     if (lane == 0) sizes[i] = size;
     acc += size;
-    if (NR == 0) continue;  // wave-uniform
-
-    // Next run end after each chunk: suffix minimum of the chunks' first end positions.
-    uint32_t ne[4];
-    uint32_t emin = 0xFFFFu;
+    if (kPrefetch) {
 #pragma unroll
-    for (int k = 3; k >= 0; --k) {
-      const uint32_t pos = (uint32_t)(k * 64 + lane) * 16u;
-      const uint32_t fe = e[k] ? pos + (uint32_t)__builtin_ctz(e[k]) : 0xFFFFu;
-      const uint32_t sm = wave_incl_suffix_min(fe);
-      uint32_t after = __shfl_down(sm, 1, 64);
-      if (lane == 63) after = 0xFFFFu;
-      ne[k] = min(after, emin);
-      emin = min(emin, __shfl(sm, 0, 64));
+      for (int k = 0; k < 4; ++k) {
+        t[k] = tn[k];
+        c[k] = cn[k];
+      }
     }
-    uint8_t* out = ws + i * kRecSlot;
-    uint32_t* hdr = reinterpret_cast<uint32_t*>(out + 4);
-    uint8_t* pay = out + 4 + 4 * NR;
-    if (lane == 0) {
-      *reinterpret_cast<uint32_t*>(out) = NR;
-      for (uint32_t q = NP; q & 3u; ++q) pay[q] = 0;  // zero padding
-    }
-    emit_chunk(0 * 64 + lane, s[0], e[0], m[0], ne[0], excl[0], c[0], hdr, pay);
-    emit_chunk(1 * 64 + lane, s[1], e[1], m[1], ne[1], excl[1], c[1], hdr, pay);
-    emit_chunk(2 * 64 + lane, s[2], e[2], m[2], ne[2], excl[2], c[2], hdr, pay);
-    emit_chunk(3 * 64 + lane, s[3], e[3], m[3], ne[3], excl[3], c[3], hdr, pay);
   }
   if (lane == 0) wsum[wave] = acc;
   __syncthreads();
@@ -222,116 +243,219 @@ __global__ __launch_bounds__(1024) void scan_blocks_kernel(const uint32_t* __res
   }
 }
 
+// Per workgroup (64 pages): page offsets inside the block -> rec_off; then every thread copies
+// output dwords of the block's packed range, finding each dword's record by binary search over
+// the 65 block-relative offsets in LDS (all loads independent, stores contiguous).
 __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ ws,
                                                    const uint32_t* __restrict__ sizes,
                                                    const uint64_t* __restrict__ block_off,
                                                    uint64_t first, uint64_t n,
                                                    uint64_t* __restrict__ rec_off,
                                                    uint8_t* __restrict__ data, uint64_t cap) {
-  __shared__ uint64_t off[kDiffPagesPerBlock];
+  __shared__ uint32_t off[kDiffPagesPerBlock + 1];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t b0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock;
+  const uint64_t base = block_off[blockIdx.x];
   if (wave == 0) {
     const uint64_t i = b0 + lane;
     const uint32_t sz = (i < n) ? sizes[i] : 0u;
     const uint32_t inc = wave_incl_sum(sz);
-    const uint64_t base = block_off[blockIdx.x];
-    off[lane] = base + inc - sz;
+    off[lane] = inc - sz;
+    if (lane == 63) off[64] = inc;
     if (i < n) rec_off[first + i + 1] = base + inc;
     if (first == 0 && blockIdx.x == 0 && lane == 0) rec_off[0] = 0;
   }
   __syncthreads();
-  for (uint32_t j = wave; j < kDiffPagesPerBlock; j += 4) {
-    const uint64_t i = b0 + j;
-    if (i >= n) break;
-    const uint32_t sz = sizes[i];
-    const uint64_t o = off[j];
-    if (sz == 0 || o + sz > cap) continue;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(ws + i * kRecSlot);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(data + o);
-    for (uint32_t q = lane; q < sz / 4; q += 64) dst[q] = src[q];
+  // Only records that end inside the capacity are copied.
+  uint32_t limit = off[64];
+  if (base + limit > cap) {
+    limit = 0;
+    for (uint32_t r = 0; r < kDiffPagesPerBlock; ++r)
+      if (base + off[r + 1] <= cap) limit = off[r + 1];
+  }
+  uint32_t* dst = reinterpret_cast<uint32_t*>(data + base);
+  for (uint32_t g = threadIdx.x; g < limit / 4; g += 256) {
+    const uint32_t byte = g * 4;
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+      if (off[r + step] <= byte) r += step;
+    const uint32_t* src =
+        reinterpret_cast<const uint32_t*>(ws + (b0 + r) * kRecSlot + (byte - off[r]));
+    dst[g] = *src;
   }
 }
 
 // ------------------------------------------------------------------------- apply (SPEC §4)
-// One wave per record. The run list is turned back into the page's 4096-bit dirty mask by
-// toggling a bit at every run start and end in LDS and taking a prefix-XOR (lane l owns bits
-// [64l, 64l+64)); payload index of a byte = popcount of the dirty bits before it. Each lane
-// then rewrites its four 16-byte chunks (read-modify-write only for partly dirty chunks).
+// A wave takes 64 consecutive records. It stages as many of them as fit in an 8 KiB LDS window
+// with coalesced loads (one global round trip for the whole window), then handles them one by
+// one out of LDS: the run list becomes the page's 4096-bit dirty mask by toggling a bit at each
+// run start and end and taking a prefix-XOR (lane l owns bytes [64l, 64l+64)); the payload index
+// of a byte is the popcount of the dirty bits before it. The replica is only STORED to (16-B
+// stores for whole chunks, dword stores for whole dwords, byte stores otherwise), never read, so
+// no wave ever waits on a replica load. A record larger than the window is read from global.
+constexpr uint32_t kApplyWin = 8192;  // bytes of records staged per wave
+
+// Stores the payload bytes selected by `mask` (16 bits, chunk of 16 B at dst) from pay[pp..].
+template <typename P8>
+__device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint32_t mask, P8 pay,
+                                            uint32_t pp) {
+  if (mask == 0xFFFFu) {
+    uint32_t w[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      w[d] = (uint32_t)pay[pp + 4 * d] | ((uint32_t)pay[pp + 4 * d + 1] << 8) |
+             ((uint32_t)pay[pp + 4 * d + 2] << 16) | ((uint32_t)pay[pp + 4 * d + 3] << 24);
+    *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t nib = (mask >> (4 * d)) & 0xFu;
+    if (nib == 0xFu) {
+      const uint32_t v = (uint32_t)pay[pp] | ((uint32_t)pay[pp + 1] << 8) |
+                         ((uint32_t)pay[pp + 2] << 16) | ((uint32_t)pay[pp + 3] << 24);
+      *reinterpret_cast<uint32_t*>(dst + 4 * d) = v;
+      pp += 4;
+    } else if (nib) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((nib >> k) & 1u) dst[4 * d + k] = pay[pp++];
+    }
+  }
+}
+
+// Applies one record (whole wave). rec32/rec8 point at the record (LDS or global). Returns false
+// on a malformed record (nothing written).
+template <typename P32, typename P8>
+__device__ __forceinline__ bool apply_record(uint8_t* __restrict__ page, P32 rec32, P8 rec8,
+                                             uint32_t size, uint32_t* __restrict__ bm) {
+  const uint32_t lane = lane_id();
+  const uint32_t nr = rec32[0];
+  if (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr) return false;
+  bm[lane] = 0;
+  bm[lane + 64] = 0;
+  wave_lds_sync();
+  uint32_t paysum = 0, badrun = 0;
+  for (uint32_t r = lane; r < nr; r += 64) {
+    const uint32_t h = rec32[1 + r];
+    const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
+    if (len == 0 || end > kPage) {
+      badrun = 1;
+      continue;
+    }
+    paysum += len;
+    atomicXor(&bm[off >> 5], 1u << (off & 31));
+    if (end < kPage) atomicXor(&bm[end >> 5], 1u << (end & 31));
+  }
+  paysum = wave_sum(paysum);
+  badrun = wave_sum(badrun);
+  if (badrun || size != 4u + 4u * nr + ((paysum + 3u) & ~3u)) return false;
+  wave_lds_sync();
+  uint64_t w = (uint64_t)bm[2 * lane] | ((uint64_t)bm[2 * lane + 1] << 32);
+  const uint32_t par = (uint32_t)__popcll(w) & 1u;
+  w ^= w << 1;
+  w ^= w << 2;
+  w ^= w << 4;
+  w ^= w << 8;
+  w ^= w << 16;
+  w ^= w << 32;
+  const uint32_t pinc = wave_incl_sum(par);
+  const uint64_t D = ((pinc - par) & 1u) ? ~w : w;
+  const uint32_t cnt = (uint32_t)__popcll(D);
+  const uint32_t pbase = 4u + 4u * nr + wave_incl_sum(cnt) - cnt;
+  uint8_t* dst = page + (uint64_t)lane * 64;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t mq = (uint32_t)(D >> (16 * q)) & 0xFFFFu;
+    if (!mq) continue;
+    const uint32_t pp = pbase + (q ? (uint32_t)__popcll(D & ((1ull << (16 * q)) - 1)) : 0u);
+    store_chunk(dst + 16 * q, mq, rec8, pp);
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target,
                                                     const uint32_t* __restrict__ ids, uint64_t n,
                                                     const uint64_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ data,
                                                     uint32_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) uint32_t win_all[4][kApplyWin / 4];
   __shared__ uint32_t bm_all[4][128];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* win = win_all[wave];
   uint32_t* bm = bm_all[wave];
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + wave; i < n; i += (uint64_t)gridDim.x * 4) {
-    const uint64_t r0 = rec_off[i], r1 = rec_off[i + 1];
-    if (r0 == r1) continue;
-    const uint32_t* rec = reinterpret_cast<const uint32_t*>(data + r0);
-    const uint32_t nr = rec[0];
-    bool bad = (nr == 0) || (nr > kMaxRuns) || (r1 < r0) || (r1 - r0 < 4u + 4u * (uint64_t)nr);
-    if (bad) {
-      if (lane == 0) atomicOr(err, 1u);
-      continue;
-    }
-    bm[lane] = 0;
-    bm[lane + 64] = 0;
-    wave_lds_sync();
-    uint32_t paysum = 0, badrun = 0;
-    for (uint32_t r = lane; r < nr; r += 64) {
-      const uint32_t h = rec[1 + r];
-      const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
-      if (len == 0 || end > kPage) { badrun = 1; continue; }
-      paysum += len;
-      atomicXor(&bm[off >> 5], 1u << (off & 31));
-      if (end < kPage) atomicXor(&bm[end >> 5], 1u << (end & 31));
-    }
-    paysum = wave_sum(paysum);
-    badrun = wave_sum(badrun);
-    if (badrun || (r1 - r0) != 4u + 4u * (uint64_t)nr + ((paysum + 3u) & ~3u)) {
-      if (lane == 0) atomicOr(err, 1u);
-      continue;
-    }
-    wave_lds_sync();
-    uint64_t w = (uint64_t)bm[2 * lane] | ((uint64_t)bm[2 * lane + 1] << 32);
-    const uint32_t par = (uint32_t)__popcll(w) & 1u;
-    w ^= w << 1;
-    w ^= w << 2;
-    w ^= w << 4;
-    w ^= w << 8;
-    w ^= w << 16;
-    w ^= w << 32;
-    const uint32_t pinc = wave_incl_sum(par);
-    const uint64_t D = ((pinc - par) & 1u) ? ~w : w;
-    const uint32_t cnt = (uint32_t)__popcll(D);
-    const uint32_t pbase = wave_incl_sum(cnt) - cnt;
-    const uint8_t* pay = reinterpret_cast<const uint8_t*>(rec + 1 + nr);
-    const uint64_t p = ids ? ids[i] : i;
-    uint8_t* dst = target + p * kPage + (uint64_t)lane * 64;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t mq = (uint32_t)(D >> (16 * q)) & 0xFFFFu;
-      if (!mq) continue;
-      const uint32_t pp = pbase + (q ? (uint32_t)__popcll(D & ((1ull << (16 * q)) - 1)) : 0u);
-      uint4* d4 = reinterpret_cast<uint4*>(dst + 16 * q);
-      uint4 v = (mq == 0xFFFFu) ? make_uint4(0, 0, 0, 0) : *d4;
-      uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if ((mq >> j) & 1u) {
-          const uint32_t src = pp + (uint32_t)__popc(mq & ((1u << j) - 1u));
-          const uint32_t byte = pay[src];
-          wv[j >> 2] = (wv[j >> 2] & ~(0xFFu << ((j & 3) * 8))) | (byte << ((j & 3) * 8));
+  const uint64_t ntask = (n + 63) / 64;
+  uint32_t bad = 0;
+  for (uint64_t task = (uint64_t)blockIdx.x * 4 + wave; task < ntask;
+       task += (uint64_t)gridDim.x * 4) {
+    const uint64_t a = task * 64;
+    const uint32_t cnt = (uint32_t)min((uint64_t)64, n - a);
+    const uint64_t my_off = rec_off[a + min(lane, cnt)];  // lane l: start of record a+l
+    const uint64_t end_off = rec_off[a + cnt];
+    uint32_t j = 0;
+    while (j < cnt) {
+      const uint64_t start = lane_bcast64(my_off, j);
+      // records j..k-1 fit the window: rec_off[a+k] - start <= kApplyWin
+      const bool fits = lane > j && lane <= cnt && (my_off - start) <= kApplyWin;
+      const uint64_t fm = __ballot(fits);
+      uint32_t k = fm ? 63u - (uint32_t)__clzll(fm) : j;  // highest lane whose offset fits
+      if (cnt == 64 && (end_off - start) <= kApplyWin) k = 64;
+      if (k == j) {  // record j alone exceeds the window: straight from global
+        const uint64_t r0 = start, r1 = (j + 1 < 64) ? lane_bcast64(my_off, j + 1) : end_off;
+        if (r1 > r0) {
+          const uint64_t p = ids ? ids[a + j] : a + j;
+          const uint8_t* rec = data + r0;
+          if (!apply_record(target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec,
+                            (uint32_t)(r1 - r0), bm))
+            bad = 1;
         }
+        ++j;
+        continue;
       }
-      *d4 = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      const uint64_t stop = (k == 64) ? end_off : lane_bcast64(my_off, k);
+      const uint32_t words = (uint32_t)((stop - start) >> 2);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(data + start);
+      for (uint32_t q = lane; q < words; q += 64) win[q] = src[q];
+      wave_lds_sync();
+      const uint8_t* win8 = reinterpret_cast<const uint8_t*>(win);
+      for (uint32_t jj = j; jj < k; ++jj) {
+        const uint64_t r0 = lane_bcast64(my_off, jj);
+        const uint64_t r1 = (jj + 1 == k) ? stop : lane_bcast64(my_off, jj + 1);
+        if (r1 == r0) continue;
+        const uint32_t base = (uint32_t)(r0 - start);
+        const uint64_t p = ids ? ids[a + jj] : a + jj;
+        if (!apply_record(target + p * kPage, win + base / 4, win8 + base, (uint32_t)(r1 - r0),
+                          bm))
+          bad = 1;
+      }
+      wave_lds_sync();
+      j = k;
     }
   }
+  if (bad && lane == 0) atomicOr(err, 1u);
 }
 
 // ------------------------------------------------------------------------- launchers
+// Diff kernel variant: without (default; 64 VGPRs, 8 waves/SIMD: 1.56 ms for config 2 on
+// MI355X) or with a next-page prefetch (105 VGPRs, 4 waves/SIMD: 1.62 ms). Set through gdsm_tune
+// ("diff_prefetch") or GDSM_DIFF_PREFETCH=0/1; used for in-process A/B measurements.
+static int g_diff_prefetch = -1;
+static bool diff_prefetch() {
+  if (g_diff_prefetch < 0) {
+    const char* e = getenv("GDSM_DIFF_PREFETCH");
+    g_diff_prefetch = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_diff_prefetch == 1;
+}
+int tune(const char* key, int64_t value) {
+  if (!strcmp(key, "diff_prefetch")) {
+    g_diff_prefetch = value ? 1 : 0;
+    return 0;
+  }
+  return -1;
+}
+
 uint64_t diff_workspace_bytes(uint64_t n_chunk) {
   const uint64_t nb = (n_chunk + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
   return n_chunk * kRecSlot + n_chunk * 4 + nb * 4 + nb * 8 + 64;
@@ -382,8 +506,12 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
     const uint64_t nb = (m + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
     {
       ProfScope ps(prof, 0, s);
-      hipLaunchKernelGGL(diff_pages_kernel, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids,
-                         first, m, slots, sizes, block_sum);
+      if (diff_prefetch())
+        hipLaunchKernelGGL(diff_pages_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, twin,
+                           cur, ids, first, m, slots, sizes, block_sum);
+      else
+        hipLaunchKernelGGL(diff_pages_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, twin,
+                           cur, ids, first, m, slots, sizes, block_sum);
     }
     {
       ProfScope ps(prof, 1, s);

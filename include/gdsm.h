@@ -166,6 +166,8 @@ int gdsm_nw_diff(const char* mem1, size_t mem1_len, char** out1, const char* mem
 int gdsm_set_allocator(void* (*alloc_fn)(size_t), void (*free_fn)(void*));
 
 const char* gdsm_version(void);
+/* Process-wide kernel-variant knobs for measurement, e.g. ("diff_prefetch", 0|1). */
+int gdsm_tune(const char* key, int64_t value);
 
 #ifdef __cplusplus
 }  /* extern "C" */

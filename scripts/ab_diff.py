@@ -1,0 +1,37 @@
+"""In-process A/B of diff kernel variants (interleaved rounds, one device): per-launch time of
+diff_pages_kernel from HIP events, for BASELINE config 2 (1M pages, 1 % word writes)."""
+import statistics
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import gallocy_amd as ga  # noqa: E402
+from gallocy_amd import gdsm  # noqa: E402
+
+KEY = sys.argv[1] if len(sys.argv) > 1 else "diff_prefetch"
+VALUES = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1"])]
+ROUNDS, REPS = 6, 10
+n = 1 << 20
+ctx = ga.Context(n)
+ctx.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+runs = ga.Runs(ctx, n, cap=n * 256)
+total = None
+res = {v: [] for v in VALUES}
+for r in range(ROUNDS):
+    for v in VALUES:
+        assert gdsm.lib().gdsm_tune(KEY.encode(), v) == 0
+        ctx.diff(out=runs)
+        ctx.sync()
+        ctx.prof_enable(True)
+        for _ in range(REPS):
+            ctx.diff(out=runs)
+        p = ctx.prof_read()
+        ctx.prof_enable(False)
+        res[v].append(p["diff"][0] / p["diff"][1])
+        t = runs.total()
+        assert total is None or t == total
+        total = t
+for v in VALUES:
+    ms = res[v]
+    gbs = (n * 8192 + total) / (statistics.median(ms) * 1e-3) / 1e9
+    print(f"{KEY}={v}: median {statistics.median(ms):.4f} ms  min {min(ms):.4f} ms  -> {gbs:.0f} GB/s")

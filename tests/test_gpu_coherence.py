@@ -53,8 +53,8 @@ def test_zipf_with_pages_spanning_many_blocks():
 
 
 def test_block_boundary_alignment_and_write_mix():
-    n = 64
     for counts in ([4096, 4096, 1, 4095, 4097], [1] * 5000, [8191, 0, 0, 1]):
+        n = max(64, len(counts))
         cts = np.zeros(n, np.uint64)
         cts[:len(counts)] = counts
         for wp in (0, 50, 100):
