@@ -325,52 +325,77 @@ __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint32_t 
   }
 }
 
-// Applies one record (whole wave). rec32/rec8 point at the record (LDS or global). Returns false
-// on a malformed record (nothing written).
+// Stores the run bytes that fall into one 16-B destination chunk: chunk [cs, cs+16) of `page`,
+// run [off, end), payload of the run starting at pay[pp].
+template <typename P8>
+__device__ __forceinline__ void store_run_chunk(uint8_t* __restrict__ page, uint32_t cs,
+                                                uint32_t off, uint32_t end, P8 pay, uint32_t pp) {
+  const uint32_t lo = max(off, cs), hi = min(end, cs + 16u);
+  const uint32_t mask = ((hi - cs >= 16u) ? 0xFFFFu : ((1u << (hi - cs)) - 1u)) &
+                        ~((1u << (lo - cs)) - 1u);
+  store_chunk(page + cs, mask, pay, pp + (lo - off));
+}
+
+// Applies one record (whole wave), one lane per run. Pass 1 validates every header (length,
+// bounds, sorted and non-overlapping, total size) so a malformed record writes nothing. Pass 2
+// stores: runs touching <= 2 chunks are stored by their own lane; otherwise the group's
+// (run, chunk) pairs are spread over the lanes (binary search over the runs' pair offsets in
+// LDS), so a 4096-byte run costs 4 wave iterations, not 256 lane iterations.
 template <typename P32, typename P8>
 __device__ __forceinline__ bool apply_record(uint8_t* __restrict__ page, P32 rec32, P8 rec8,
-                                             uint32_t size, uint32_t* __restrict__ bm) {
+                                             uint32_t size, uint32_t* __restrict__ scratch) {
   const uint32_t lane = lane_id();
   const uint32_t nr = rec32[0];
   if (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr) return false;
-  bm[lane] = 0;
-  bm[lane + 64] = 0;
-  wave_lds_sync();
-  uint32_t paysum = 0, badrun = 0;
-  for (uint32_t r = lane; r < nr; r += 64) {
-    const uint32_t h = rec32[1 + r];
+  uint32_t pay_total = 0, prev_end = 0, bad = 0;
+  for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    const uint32_t h = (r < nr) ? rec32[1 + r] : 0u;
     const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
-    if (len == 0 || end > kPage) {
-      badrun = 1;
+    uint32_t pe = from_prev_lane(end);
+    if (lane == 0) pe = prev_end;
+    if (r < nr && (len == 0 || end > kPage || off < pe)) bad = 1;
+    pay_total += wave_sum(len);
+    prev_end = lane_bcast(end, 63);
+  }
+  if (wave_sum(bad) || size != 4u + 4u * nr + ((pay_total + 3u) & ~3u)) return false;
+
+  const uint32_t pay0 = 4u + 4u * nr;  // payload start inside the record
+  uint32_t pcarry = 0;
+  uint32_t* ci = scratch;        // [64] exclusive (run, chunk) pair offsets of the group
+  uint32_t* ppa = scratch + 64;  // [64] payload offsets of the group's runs
+  for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    const uint32_t h = (r < nr) ? rec32[1 + r] : 0u;
+    const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
+    const uint32_t pinc = wave_incl_sum(len);
+    const uint32_t pp = pay0 + pcarry + pinc - len;  // payload of this run
+    pcarry += lane_bcast(pinc, 63);
+    const uint32_t nch = len ? ((end - 1u) >> 4) - (off >> 4) + 1u : 0u;
+    const uint32_t cmax = lane_bcast(wave_incl_max(nch), 63);
+    if (cmax <= 2) {
+      for (uint32_t q = 0; q < nch; ++q)
+        store_run_chunk(page, ((off >> 4) + q) << 4, off, end, rec8, pp);
       continue;
     }
-    paysum += len;
-    atomicXor(&bm[off >> 5], 1u << (off & 31));
-    if (end < kPage) atomicXor(&bm[end >> 5], 1u << (end & 31));
-  }
-  paysum = wave_sum(paysum);
-  badrun = wave_sum(badrun);
-  if (badrun || size != 4u + 4u * nr + ((paysum + 3u) & ~3u)) return false;
-  wave_lds_sync();
-  uint64_t w = (uint64_t)bm[2 * lane] | ((uint64_t)bm[2 * lane + 1] << 32);
-  const uint32_t par = (uint32_t)__popcll(w) & 1u;
-  w ^= w << 1;
-  w ^= w << 2;
-  w ^= w << 4;
-  w ^= w << 8;
-  w ^= w << 16;
-  w ^= w << 32;
-  const uint32_t pinc = wave_incl_sum(par);
-  const uint64_t D = ((pinc - par) & 1u) ? ~w : w;
-  const uint32_t cnt = (uint32_t)__popcll(D);
-  const uint32_t pbase = 4u + 4u * nr + wave_incl_sum(cnt) - cnt;
-  uint8_t* dst = page + (uint64_t)lane * 64;
+    const uint32_t cinc = wave_incl_sum(nch);
+    const uint32_t T = lane_bcast(cinc, 63);
+    ci[lane] = cinc - nch;
+    ppa[lane] = pp;
+    wave_lds_sync();
+    for (uint32_t g = lane; g < T; g += 64) {
+      uint32_t i = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t mq = (uint32_t)(D >> (16 * q)) & 0xFFFFu;
-    if (!mq) continue;
-    const uint32_t pp = pbase + (q ? (uint32_t)__popcll(D & ((1ull << (16 * q)) - 1)) : 0u);
-    store_chunk(dst + 16 * q, mq, rec8, pp);
+      for (uint32_t step = 32; step; step >>= 1)
+        if (i + step < 64 && ci[i + step] <= g) i += step;
+      // lane i's run: fetch its header and payload offset from the lane that owns it
+      const uint32_t hi = rec32[1 + r0 + i];
+      const uint32_t o = hi & 0xFFFFu, e = o + (hi >> 16);
+      const uint32_t ppi = ppa[i];
+      const uint32_t cs = ((o >> 4) + (g - ci[i])) << 4;
+      store_run_chunk(page, cs, o, e, rec8, ppi);
+    }
+    wave_lds_sync();
   }
   return true;
 }

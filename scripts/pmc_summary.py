@@ -1,0 +1,34 @@
+"""Turns rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes per kernel,
+with the gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB)
+reports exactly half of a wide coalesced streaming read, so it is doubled; WRITE_SIZE (KB) is
+exact for 16-B-per-lane streaming stores. Usage: pmc_summary.py <fetch.csv> <write.csv> <out.json>"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            acc[name].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+write = per_kernel(sys.argv[2], "WRITE_SIZE")
+out = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes, "
+                 "bench.py --steps 5 --warmup 1 (1M pages, 1% word writes)",
+       "correction": "hbm_bytes = 2 * FETCH_SIZE_KB * 1024 + WRITE_SIZE_KB * 1024 (gfx950)",
+       "kernels": {}}
+for k in sorted(set(fetch) | set(write)):
+    f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+    out["kernels"][k] = {"fetch_kb_raw": f, "write_kb": w,
+                         "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024)}
+d = out["kernels"].get("gdsm::diff_pages_kernel<false>")
+if d:
+    out["diff_pages_kernel_bytes_per_launch"] = d["hbm_bytes_per_launch"]
+json.dump(out, open(sys.argv[3], "w"), indent=1)
+print(json.dumps(out, indent=1))

@@ -250,3 +250,55 @@ def test_config3_shard_properties():
         for j, p in enumerate(ids):
             t, cur = oracle.gen_pages(1, seed=77, mode=1, ppm=100000, first_page=3 * n + int(p))
             assert h.record(j) == oracle.diff_pages(t, cur)[1].tobytes()
+
+
+def _one_record(runs, pay_fill=0xAB):
+    hdr = [o | (ln << 16) for o, ln in runs]
+    pay = bytes([pay_fill]) * sum(max(0, ln) for _, ln in runs)
+    pay += b"\0" * ((-len(pay)) % 4)
+    rec = np.array([len(runs)] + hdr, "<u4").tobytes() + pay
+    return np.array([0, len(rec)], np.uint64), np.frombuffer(rec, np.uint8).copy()
+
+
+@pytest.mark.parametrize("runs", [
+    [(100, 8), (50, 8)],          # unsorted
+    [(100, 8), (104, 8)],         # overlapping
+    [(10, 0)],                    # empty run
+    [(4090, 8)],                  # past the page end
+])
+def test_apply_rejects_bad_runs_like_oracle(runs):
+    ro, data = _one_record(runs)
+    page = np.zeros((1, 4096), np.uint8)
+    assert oracle.apply(page.copy(), ro, data) == -22
+    with ga.Context(1) as c:
+        c.upload("replica", page)
+        c.apply(Runs.from_host(c, HostRuns(ro, data)))
+        with pytest.raises(GdsmError):
+            c.sync()
+        assert not c.download("replica").any()
+
+
+def test_apply_many_runs_and_long_runs():
+    """Records mixing long runs (many chunks, pair-spread path) and dense short runs."""
+    rng = np.random.default_rng(17)
+    n = 257
+    twin = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    cur = twin.copy()
+    for i in range(n):
+        kind = i % 4
+        if kind == 0:    # a few long runs at odd offsets
+            for _ in range(3):
+                o = int(rng.integers(0, 3000))
+                cur[i, o:o + int(rng.integers(17, 1000))] ^= 0xFF
+        elif kind == 1:  # 70..300 short runs (more than one 64-run group)
+            pos = np.sort(rng.choice(2048, int(rng.integers(70, 300)), replace=False)) * 2
+            cur[i, pos] ^= 0x5A
+        elif kind == 2:  # one run over the whole page
+            cur[i] ^= 0x01
+        # kind 3: clean
+    ro, data = oracle.diff_pages(twin, cur)
+    with ga.Context(n) as c:
+        c.upload("replica", twin)
+        c.apply(Runs.from_host(c, HostRuns(ro, data)))
+        c.sync()
+        assert np.array_equal(c.download("replica"), cur)
