@@ -136,8 +136,11 @@ __device__ __forceinline__ void load_page(const uint8_t* __restrict__ twin,
 
 // Diffs one page held in registers (chunk (k, lane) = bytes [(64k + lane) * 16, +16), page
 // order = (k, lane)); writes its record to `out` and returns the record size (wave-uniform).
+constexpr uint32_t kDiffStage = 2048;  // per-wave LDS record stage (bytes)
+
 __device__ __forceinline__ uint32_t diff_one(const uint4 (&t)[4], const uint4 (&c)[4],
-                                             uint32_t lane, uint8_t* __restrict__ out) {
+                                             uint32_t lane, uint8_t* __restrict__ out,
+                                             uint32_t* __restrict__ stage) {
   uint32_t m[4], s[4], e[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) m[k] = diffmask16(t[k], c[k]);
@@ -167,28 +170,42 @@ __device__ __forceinline__ uint32_t diff_one(const uint4 (&t)[4], const uint4 (&
   }
   const uint32_t NR = carry & 0xFFFFu, NP = carry >> 16;
   if (NR == 0) return 0;
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(out + 4);
-  uint8_t* pay = out + 4 + 4 * NR;
+  const uint32_t size = 4u + 4u * NR + ((NP + 3u) & ~3u);
+  // Assemble the record in the wave's LDS stage when it fits, then write it with 16-B stores
+  // (a handful of VMEM instructions instead of one per header and per payload byte).
+  const bool staged = stage != nullptr && size <= kDiffStage;
+  uint8_t* rec = staged ? reinterpret_cast<uint8_t*>(stage) : out;
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(rec + 4);
+  uint8_t* pay = rec + 4 + 4 * NR;
   if (lane == 0) {
-    *reinterpret_cast<uint32_t*>(out) = NR;
+    *reinterpret_cast<uint32_t*>(rec) = NR;
     for (uint32_t q = NP; q & 3u; ++q) pay[q] = 0;  // zero padding
   }
   emit_chunk(0 * 64 + lane, s[0], e[0], m[0], ps[0], excl[0], c[0], hdr, pay);
   emit_chunk(1 * 64 + lane, s[1], e[1], m[1], ps[1], excl[1], c[1], hdr, pay);
   emit_chunk(2 * 64 + lane, s[2], e[2], m[2], ps[2], excl[2], c[2], hdr, pay);
   emit_chunk(3 * 64 + lane, s[3], e[3], m[3], ps[3], excl[3], c[3], hdr, pay);
-  return 4u + 4u * NR + ((NP + 3u) & ~3u);
+  if (staged) {
+    wave_lds_sync();
+    const uint4* src = reinterpret_cast<const uint4*>(stage);
+    uint4* dst = reinterpret_cast<uint4*>(out);
+    for (uint32_t q = lane; q < (size + 15u) / 16u; q += 64) dst[q] = src[q];
+    wave_lds_sync();
+  }
+  return size;
 }
 
 // One workgroup = 4 waves = kDiffPagesPerBlock consecutive pages (wave w takes w, w+4, ...).
 // kPrefetch: the next page's 8 loads are issued before the current page is processed.
-template <bool kPrefetch>
+template <bool kPrefetch, bool kStage>
 __global__ __launch_bounds__(256) void diff_pages_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
   __shared__ uint32_t wsum[4];
+  __shared__ __attribute__((aligned(16))) uint32_t stage_all[kStage ? 4 : 1][kDiffStage / 4];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* stage = kStage ? stage_all[kStage ? wave : 0] : nullptr;
   const uint64_t b0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock;
   uint32_t acc = 0;
   uint4 t[4], c[4];
@@ -201,7 +218,7 @@ __global__ __launch_bounds__(256) void diff_pages_kernel(
     uint4 tn[4], cn[4];
     const bool nx = kPrefetch && j + 4 < kDiffPagesPerBlock && i + 4 < n;
     if (nx) load_page(twin, cur, ids ? ids[first + i + 4] : first + i + 4, lane, tn, cn);
-    const uint32_t size = diff_one(t, c, lane, ws + i * kRecSlot);
+    const uint32_t size = diff_one(t, c, lane, ws + i * kRecSlot, stage);
     if (lane == 0) sizes[i] = size;
     acc += size;
     if (kPrefetch) {
@@ -473,9 +490,16 @@ static bool diff_prefetch() {
   }
   return g_diff_prefetch == 1;
 }
+// Record assembly in LDS + 16-B stores (default) or direct per-lane global stores.
+static int g_diff_stage = 1;
+static bool diff_stage() { return g_diff_stage == 1; }
 int tune(const char* key, int64_t value) {
   if (!strcmp(key, "diff_prefetch")) {
     g_diff_prefetch = value ? 1 : 0;
+    return 0;
+  }
+  if (!strcmp(key, "diff_stage")) {
+    g_diff_stage = value ? 1 : 0;
     return 0;
   }
   return -1;
@@ -531,12 +555,12 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
     const uint64_t nb = (m + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
     {
       ProfScope ps(prof, 0, s);
-      if (diff_prefetch())
-        hipLaunchKernelGGL(diff_pages_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, twin,
-                           cur, ids, first, m, slots, sizes, block_sum);
-      else
-        hipLaunchKernelGGL(diff_pages_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, twin,
-                           cur, ids, first, m, slots, sizes, block_sum);
+      auto kern = diff_prefetch() ? (diff_stage() ? diff_pages_kernel<true, true>
+                                                  : diff_pages_kernel<true, false>)
+                                  : (diff_stage() ? diff_pages_kernel<false, true>
+                                                  : diff_pages_kernel<false, false>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids, first, m,
+                         slots, sizes, block_sum);
     }
     {
       ProfScope ps(prof, 1, s);
