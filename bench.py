@@ -44,6 +44,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=2026)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", choices=["pages", "coherence"], default="pages",
+                    help="pages: BASELINE configs[1]/[2] (the headline); coherence: configs[3]")
+    ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
+    ap.add_argument("--coh-pages", type=int, default=16 << 20, help="coherence: pages")
+    ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
     return ap.parse_args()
 
 
@@ -112,8 +117,83 @@ def read_traffic():
     return None, None
 
 
+def run_coherence(args):
+    """BASELINE configs[3]: batched coherence, 16M pages, 8 nodes, 1B events (Zipf 0.8 or
+    uniform pages, 20 % writes), one GPU. A step = one whole batch through the page table."""
+    import torch
+
+    import gallocy_amd as ga
+    from gallocy_amd.workloads import event_counts
+    torch.cuda.set_device(0)
+    n, E = args.coh_pages, args.events
+    counts = event_counts(n, E, args.dist, seed=args.seed)
+    ctx = ga.Context(n, arenas=())
+    ev = ctx.gen_events(counts, seed=args.seed, n_nodes=8, write_pct=20)
+    touched = int((counts > 0).sum())
+    ctx.coh_init(8)
+    tot_dev = ctx.buffer(80)
+    L = ga.gdsm.lib()
+
+    def step():
+        rc = L.gdsm_coherence_batch_async(ctx.handle, ev.ptr, ev.count, tot_dev.ptr)
+        if rc:
+            raise RuntimeError(f"gdsm_coherence_batch_async {rc}")
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    ctx.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    prof = ctx.prof_read()
+    totals = tot_dev.download(np.uint64, 10)
+    main_ms = prof["coh_apply"][0] / max(1, prof["coh_apply"][1])
+    alg = ev.count * 8 + touched * 16  # events read + state/faults words read and written
+    achieved = alg / (main_ms * 1e-3) / 1e9
+    stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]} for k, v in prof.items() if v[1]}
+    res = {"metric": "coherence events/sec", "value": round(ev.count * args.steps / dt, 1),
+           "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": f"synthetic ({args.dist} page popularity, SPEC §6 events)",
+           "config": {"workload": f"{n} pages, 8 nodes, {ev.count} events/batch, {args.dist}, 20% writes",
+                      "touched_pages": touched},
+           "roofline": {"bound": "hbm", "kernel": "coh_apply_kernel", "achieved": round(achieved, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": None, "algorithmic_bytes_per_launch": int(alg),
+                        "avg_launch_ms": round(main_ms, 4)},
+           "stages": stages,
+           "last_batch_totals": {"invalidations": int(totals[0]), "transfers": int(totals[1]),
+                                 "node_faults": [int(x) for x in totals[2:]]},
+           "cpu_baseline": None}
+    if not args.no_cpu:
+        from oracle import oracle
+        m = 1 << 20
+        sub = event_counts(m, 1 << 26, args.dist, seed=args.seed)
+        hev = oracle.gen_events(sub, seed=args.seed)
+        st, fl = oracle.coh_init(m, 8)
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds or reps == 0:
+            oracle.coherence(st, fl, hev)
+            reps += 1
+        cdt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(len(hev) * reps / cdt, 1), "unit": "events/s",
+                               "cores": 1, "kind": "port",
+                               "sample": f"{len(hev)} events over {m} pages ({args.dist}), "
+                                         f"{reps} batches, oracle or_coherence, 1 thread"}
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.workload == "coherence":
+        return run_coherence(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -73,10 +73,4 @@ def py_coherence(state, faults, events, n_pages):
     return tot
 
 
-def zipf_counts(n_pages, total, s=0.8, seed=0):
-    """Per-page event counts ~ Zipf(s) over a seeded page permutation (host side, float64)."""
-    rng = np.random.default_rng(seed)
-    ranks = rng.permutation(n_pages) + 1
-    w = ranks.astype(np.float64) ** (-s)
-    w /= w.sum()
-    return rng.multinomial(total, w).astype(np.uint64)
+from gallocy_amd.workloads import zipf_counts  # noqa: E402,F401

@@ -1,0 +1,49 @@
+"""The multi-GPU step machinery on one real GPU: a 1-rank RCCL (torch 'nccl') group drives
+gallocy_amd.exchange.Shard — device tensors aliasing libgdsm buffers, the context stream as
+torch's current stream, all_to_all_single, gdsm_apply_raw — and the home REPLICA must end equal
+to CURRENT. (N > 1 runs in the driver's multi-GPU bench; tests/test_exchange.py covers 2-4 ranks
+of the same code over gloo.)"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+import gallocy_amd as ga
+from gallocy_amd import exchange
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_step_single_rank_rccl():
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = 1 << 14
+        with ga.Context(n) as ctx:
+            ctx.gen_pages(seed=5, mode=ga.GEN_CLUSTERED, ppm=100000, first_global=0, stride=1,
+                          arenas=("twin", "current"))
+            ctx.gen_pages(seed=5, mode=ga.GEN_CLUSTERED, ppm=100000, first_global=0, stride=1,
+                          arenas=("replica",))
+            runs = ga.Runs(ctx, n, cap=n * 1024)
+            shard = exchange.Shard(ctx, runs, 0, 1, n)
+            shard.gen_args = (5, ga.GEN_CLUSTERED, 100000)
+            for _ in range(2):
+                ctx.diff(out=runs)
+                shard.exchange_and_apply()
+            ctx.sync()
+            torch.cuda.synchronize()
+            assert shard.received == runs.total() > 0
+            assert shard.verify()
+    finally:
+        dist.destroy_process_group()
