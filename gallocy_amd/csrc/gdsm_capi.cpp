@@ -22,8 +22,7 @@ struct gdsm_ctx {
   uint64_t diff_ws_bytes = 0;
   uint8_t* coh_ws = nullptr;
   uint64_t coh_ws_bytes = 0;
-  uint32_t* coh_state = nullptr;
-  uint32_t* coh_faults = nullptr;
+  uint64_t* coh_pt = nullptr;      // page table: state | faults << 32 per page
   uint64_t* coh_totals = nullptr;  // device 10 x u64
   uint32_t n_nodes = 0;
   std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks
@@ -151,8 +150,7 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->err) (void)hipFree(ctx->err);
   if (ctx->diff_ws) (void)hipFree(ctx->diff_ws);
   if (ctx->coh_ws) (void)hipFree(ctx->coh_ws);
-  if (ctx->coh_state) (void)hipFree(ctx->coh_state);
-  if (ctx->coh_faults) (void)hipFree(ctx->coh_faults);
+  if (ctx->coh_pt) (void)hipFree(ctx->coh_pt);
   if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -405,27 +403,25 @@ int gdsm_twin_raw(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64
 int gdsm_coh_init(gdsm_ctx* ctx, uint32_t n_nodes) {
   if (!ctx || n_nodes == 0 || n_nodes > GDSM_MAX_NODES) return -EINVAL;
   DeviceGuard g(ctx->device);
-  if (!ctx->coh_state) {
-    const uint64_t bytes = (ctx->n_pages ? ctx->n_pages : 1) * 4;
-    GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_state), bytes));
-    GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_faults), bytes));
+  if (!ctx->coh_pt) {
+    GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_pt),
+                       (ctx->n_pages ? ctx->n_pages : 1) * 8));
     GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_totals), 10 * sizeof(uint64_t)));
   }
   ctx->n_nodes = n_nodes;
-  GDSM_TRY(gdsm::launch_coh_init(ctx->coh_state, ctx->coh_faults, ctx->n_pages, n_nodes,
-                                 ctx->stream));
+  GDSM_TRY(gdsm::launch_coh_init(ctx->coh_pt, ctx->n_pages, n_nodes, ctx->stream));
   return 0;
 }
 
 int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_events,
                                uint64_t* totals_dev) {
-  if (!ctx || !ctx->coh_state || !totals_dev || (!events && n_events)) return -EINVAL;
+  if (!ctx || !ctx->coh_pt || !totals_dev || (!events && n_events)) return -EINVAL;
   DeviceGuard g(ctx->device);
   int rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
   if (rc) return rc;
-  GDSM_TRY(gdsm::launch_coherence(ctx->coh_state, ctx->coh_faults, ctx->n_pages, events,
-                                  n_events, totals_dev, ctx->coh_ws, ctx->coh_ws_bytes, ctx->err,
-                                  ctx->stream, ctx->P()));
+  GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, events, n_events, totals_dev,
+                                  ctx->coh_ws, ctx->coh_ws_bytes, ctx->err, ctx->stream,
+                                  ctx->P()));
   return 0;
 }
 
@@ -440,20 +436,36 @@ int gdsm_coherence_batch(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_event
   return gdsm_sync(ctx);
 }
 
+// The page table is interleaved on the device (u64 = state | faults << 32); these copy the two
+// word columns to / from the caller's separate arrays with strided (2-D) copies.
 int gdsm_coh_download(gdsm_ctx* ctx, uint32_t* state, uint32_t* faults) {
-  if (!ctx || !ctx->coh_state) return -EINVAL;
-  int rc = 0;
-  if (state) rc = gdsm_memcpy_d2h(ctx, state, ctx->coh_state, ctx->n_pages * 4);
-  if (!rc && faults) rc = gdsm_memcpy_d2h(ctx, faults, ctx->coh_faults, ctx->n_pages * 4);
-  return rc;
+  if (!ctx || !ctx->coh_pt) return -EINVAL;
+  if (ctx->n_pages == 0) return 0;
+  DeviceGuard g(ctx->device);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(ctx->coh_pt);
+  if (state)
+    GDSM_TRY(hipMemcpy2DAsync(state, 4, base, 8, 4, ctx->n_pages, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  if (faults)
+    GDSM_TRY(hipMemcpy2DAsync(faults, 4, base + 1, 8, 4, ctx->n_pages, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
 }
 
 int gdsm_coh_upload(gdsm_ctx* ctx, const uint32_t* state, const uint32_t* faults) {
-  if (!ctx || !ctx->coh_state) return -EINVAL;
-  int rc = 0;
-  if (state) rc = gdsm_memcpy_h2d(ctx, ctx->coh_state, state, ctx->n_pages * 4);
-  if (!rc && faults) rc = gdsm_memcpy_h2d(ctx, ctx->coh_faults, faults, ctx->n_pages * 4);
-  return rc;
+  if (!ctx || !ctx->coh_pt) return -EINVAL;
+  if (ctx->n_pages == 0) return 0;
+  DeviceGuard g(ctx->device);
+  uint32_t* base = reinterpret_cast<uint32_t*>(ctx->coh_pt);
+  if (state)
+    GDSM_TRY(hipMemcpy2DAsync(base, 8, state, 4, 4, ctx->n_pages, hipMemcpyHostToDevice,
+                              ctx->stream));
+  if (faults)
+    GDSM_TRY(hipMemcpy2DAsync(base + 1, 8, faults, 4, 4, ctx->n_pages, hipMemcpyHostToDevice,
+                              ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
 }
 
 int gdsm_gen_events(gdsm_ctx* ctx, uint64_t* events, const uint64_t* offsets, uint64_t first_page,

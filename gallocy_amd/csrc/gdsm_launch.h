@@ -31,12 +31,11 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
 
 // Coherence (SPEC §5).
 uint64_t coh_workspace_bytes(uint64_t n_events);
-hipError_t launch_coh_init(uint32_t* state, uint32_t* faults, uint64_t n_pages, uint32_t n_nodes,
-                           hipStream_t s);
-hipError_t launch_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages,
-                            const uint64_t* events, uint64_t n_events, uint64_t* totals,
-                            uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
-                            Prof* prof = nullptr);
+// Page table: one u64 per page, state | faults << 32.
+hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hipStream_t s);
+hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* events,
+                            uint64_t n_events, uint64_t* totals, uint8_t* ws, uint64_t ws_bytes,
+                            uint32_t* err, hipStream_t s, Prof* prof = nullptr);
 hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,
                              uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,
                              hipStream_t s);
