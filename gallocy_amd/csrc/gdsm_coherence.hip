@@ -17,14 +17,15 @@
 // Kernels (no workgroup ever waits on another; events are blocked by kCohBlock = 2048):
 //   A coh_tail_kernel   one wave per block: the block's aggregate transform. If the block's last
 //                       64 events hold a segment head only that tail is read; otherwise (a hot
-//                       page covering most of the block) the wave folds the whole block, 32
-//                       events per lane. Records the last head's page-table word so pass C never
-//                       reads a word another block writes.
+//                       page covering most of the block) the wave folds the whole block in
+//                       coalesced 64-event steps. Records the last head's page-table word so
+//                       pass C never reads a word another block writes.
 //   B coh_group/_top/_rescan  exclusive scan of the block aggregates (groups of 1024 blocks).
-//   C coh_apply_kernel  per block: events staged in LDS, 8 events per thread, block scan with
-//                       the carry-in, per-event faults, segmented fault sums, final words
-//                       written at segment ends (atomics only for segments split across
-//                       blocks), one partial row of totals per block.
+//   C coh_apply_kernel  persistent workgroups, 8 consecutive events per thread in registers
+//                       (next block prefetched), block scan with the carry-in, per-event
+//                       faults, segmented fault sums, final words written at segment ends
+//                       (atomics only for segments split across blocks), one partial row of
+//                       totals per block.
 //   D coh_reduce_kernel partial rows -> the 10 batch totals.
 #include "gdsm_common.h"
 #include "gdsm_launch.h"
@@ -37,16 +38,14 @@ constexpr uint32_t kCohBlock = 256 * kCohK;     // events per block
 constexpr uint32_t kCohGroup = 1024;            // blocks per scan group
 constexpr uint32_t kNoHead = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t tcompose(uint32_t a, uint32_t b) {  // a, then b
-  if (b & kConst) return b;
+// a, then b. Branch-free: for a READ b the copyset gains R, and a CONST(EXCLUSIVE) a turns
+// SHARED (state bits 10 -> 01) when R holds a node outside its copyset.
+__device__ __forceinline__ uint32_t tcompose(uint32_t a, uint32_t b) {
   const uint32_t R = b & 0xFFu;
-  if (a & kConst) {
-    const uint32_t cs = a & 0xFFu;
-    uint32_t st = (a >> 16) & 3u;
-    if ((R & ~cs) && st == 2u) st = 1u;
-    return (a & ~(0xFFu | (3u << 16))) | (cs | R) | (st << 16);
-  }
-  return a | R;
+  const bool excl = ((a >> 16) & 3u) == 2u;
+  const bool flip = (a & kConst) && excl && (R & ~a & 0xFFu);
+  const uint32_t rr = (a | R) ^ (flip ? 0x30000u : 0u);
+  return (b & kConst) ? b : rr;
 }
 
 __device__ __forceinline__ uint32_t ev_transform(uint64_t e) {
@@ -155,32 +154,41 @@ __global__ __launch_bounds__(256) void coh_tail_kernel(const uint64_t* __restric
     lh = (uint32_t)(wlo + hl - lo);
     hp = lane_bcast64(hp, (int)hl);
   } else {
-    // 2) no head in the tail: fold the whole block, lane l takes a contiguous share
-    const uint32_t cnt = (uint32_t)(hi - lo);
-    const uint32_t per = (cnt + 63) / 64;
-    const uint32_t a0 = min(cnt, lane * per), a1 = min(cnt, a0 + per);
-    uint32_t f = 0, mylh = kNoHead;
-    uint64_t myhp = 0;
-    uint64_t prev = (lo + a0 > 0 && a0 < a1) ? ev[lo + a0 - 1] : 0;
-    for (uint32_t x = a0; x < a1; ++x) {
-      const uint64_t ex = ev[lo + x];
-      const uint32_t te = ev_transform(ex);
-      if (lo + x == 0 || ev_page(ex) != ev_page(prev)) {
-        const uint64_t p = ev_page(ex);
-        myhp = (p < n_pages) ? pt[p] : 0ull;
-        mylh = x;
-        f = tcompose(kConst | (uint32_t)myhp, te);
-      } else {
-        f = tcompose(f, te);
+    // 2) no head in the tail: the block is (mostly) one hot page. Fold it in 64-event steps of
+    //    coalesced loads (8 steps in flight at a time), one ordered wave reduction per step.
+    acc = 0;
+    uint64_t carry_ev = (lo > 0) ? ev[lo - 1] : 0;  // event before the current step's lane 0
+    for (uint64_t j0 = lo; j0 < hi; j0 += 512) {
+      uint64_t x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t ix = j0 + 64 * q + lane;
+        x[q] = (ix < hi) ? ev[ix] : 0ull;
       }
-      prev = ex;
-    }
-    acc = wave_reduce_compose(f);
-    const uint64_t any = __ballot(mylh != kNoHead);
-    if (any) {
-      const uint32_t src = 63u - (uint32_t)__clzll(any);
-      lh = lane_bcast(mylh, (int)src);
-      hp = lane_bcast64(myhp, (int)src);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t ix = j0 + 64 * q + lane;
+        const bool v = ix < hi;
+        uint64_t pv = (uint64_t)from_prev_lane((uint32_t)x[q]) |
+                      ((uint64_t)from_prev_lane((uint32_t)(x[q] >> 32)) << 32);
+        if (lane == 0) pv = carry_ev;
+        const bool hd = v && (ix == 0 || ev_page(x[q]) != ev_page(pv));
+        uint32_t te = v ? ev_transform(x[q]) : 0u;
+        uint64_t w = 0;
+        if (hd) {
+          const uint64_t p = ev_page(x[q]);
+          w = (p < n_pages) ? pt[p] : 0ull;
+          te = tcompose(kConst | (uint32_t)w, te);
+        }
+        acc = tcompose(acc, wave_reduce_compose(te));
+        const uint64_t hb = __ballot(hd);
+        if (hb) {
+          const uint32_t src = 63u - (uint32_t)__clzll(hb);
+          lh = (uint32_t)(j0 + 64 * q + src - lo);
+          hp = lane_bcast64(w, (int)src);
+        }
+        carry_ev = lane_bcast64(x[q], 63);
+      }
     }
   }
   if (lane == 0) {
@@ -254,47 +262,63 @@ __global__ __launch_bounds__(256) void coh_rescan_kernel(const uint32_t* __restr
 }
 
 // ---------------------------------------------------------------- C: apply the batch
-__device__ __forceinline__ uint32_t pad_idx(uint32_t x) { return x + (x >> 3); }  // +8 B / 64 B
+// Thread t of a block holds the block's events [8t, 8t+8) in registers (four 16-B loads);
+// the workgroup loops over blocks (grid-stride) and loads the next block's events while it
+// works on the current one.
+template <bool kVec>
+__device__ __forceinline__ void load_block_events(const uint64_t* __restrict__ ev, uint64_t n,
+                                                  uint64_t i0, uint64_t (&E)[kCohK]) {
+  if (kVec && i0 + kCohK <= n) {
+#pragma unroll
+    for (int q = 0; q < kCohK / 2; ++q) {
+      const uint4 v = ld_nt16(ev + i0 + 2 * q);
+      E[2 * q] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      E[2 * q + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < (int)kCohK; ++k) E[k] = (i0 + k < n) ? ev[i0 + k] : 0ull;
+  }
+}
 
-__global__ __launch_bounds__(256) void coh_apply_kernel(
-    uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
-    const uint32_t* __restrict__ carry, const uint32_t* __restrict__ last_head,
-    const uint64_t* __restrict__ head_pt, uint32_t* __restrict__ partial,
-    uint32_t* __restrict__ err) {
-  __shared__ uint64_t sev[kCohBlock + kCohBlock / 8];
-  __shared__ uint32_t wtot[4];
-  __shared__ uint32_t red[4][10];
+__device__ __forceinline__ uint64_t prev_lane64(uint64_t v) {
+  return (uint64_t)from_prev_lane((uint32_t)v) | ((uint64_t)from_prev_lane((uint32_t)(v >> 32)) << 32);
+}
+__device__ __forceinline__ uint64_t next_lane64(uint64_t v) {
+  return (uint64_t)from_next_lane((uint32_t)v) | ((uint64_t)from_next_lane((uint32_t)(v >> 32)) << 32);
+}
+
+// One block of pass C (kFull: all kCohBlock events present, no per-event bounds checks).
+template <bool kFull>
+__device__ __forceinline__ void coh_block(uint64_t* __restrict__ pt, uint64_t n_pages,
+                                          const uint64_t (&e)[kCohK], uint64_t b, uint64_t b0,
+                                          uint32_t cnt, uint64_t before, bool has_after,
+                                          uint64_t after, uint32_t lh, uint64_t lhp, uint32_t cin,
+                                          uint32_t* __restrict__ partial, uint32_t* wtot,
+                                          uint64_t* bnd, uint32_t (*red)[10], uint32_t& bad) {
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint64_t b = blockIdx.x;
-  const uint64_t b0 = b * kCohBlock;
-  const uint32_t cnt = (uint32_t)min((uint64_t)kCohBlock, n - b0);
-  for (uint32_t x = t; x < kCohBlock; x += 256) sev[pad_idx(x)] = (x < cnt) ? ev[b0 + x] : 0ull;
-  const uint64_t before = (b0 > 0) ? ev[b0 - 1] : 0ull;
-  const bool has_after = b0 + cnt < n;
-  const uint64_t after = has_after ? ev[b0 + cnt] : 0ull;
-  __syncthreads();
-
   const uint32_t first = t * kCohK;
-  const uint32_t lh = last_head[b];
-  const uint64_t lhp = head_pt[b];
   uint32_t* pst = reinterpret_cast<uint32_t*>(pt);  // state words at even indices
   uint32_t* pfl = pst + 1;                          // fault words at odd indices
+  // neighbours of this thread's 8 events: DPP inside the wave, LDS across waves
+  if (lane == 63) bnd[2 * wave] = e[kCohK - 1];
+  if (lane == 0) bnd[2 * wave + 1] = e[0];
+  __syncthreads();
+  uint64_t eprev = prev_lane64(e[kCohK - 1]);
+  uint64_t enext = next_lane64(e[0]);
+  if (lane == 0) eprev = wave ? bnd[2 * (wave - 1)] : before;
+  if (lane == 63) enext = (wave < 3) ? bnd[2 * (wave + 1) + 1] : after;
 
-  // ---- flags, sortedness, head words (every page-table read is before the first barrier
-  // below; every page-table write of this kernel is after it)
-  uint64_t e[kCohK];
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k) e[k] = sev[pad_idx(first + k)];
-  const uint64_t eprev = (first > 0) ? sev[pad_idx(first - 1)] : before;
-  const uint64_t enext = (first + kCohK < cnt) ? sev[pad_idx(first + kCohK)] : after;
-  uint32_t hmask = 0, emask = 0, bad = 0;
+  // ---- flags, sortedness, head words (every page-table read of this block happens before
+  // the barrier inside block_excl_compose; every write after it)
+  uint32_t hmask = 0, emask = 0;
   uint32_t hs[kCohK], hf[kCohK];
 #pragma unroll
   for (uint32_t k = 0; k < kCohK; ++k) {
     hs[k] = 0;
     hf[k] = 0;
     const uint32_t x = first + k;
-    if (x < cnt) {
+    if (kFull || x < cnt) {
       const uint64_t pg = ev_page(e[k]);
       const bool hp = (k == 0) ? (b0 + x > 0) : true;
       const uint64_t pp = ev_page(k == 0 ? eprev : e[k > 0 ? k - 1 : 0]);
@@ -320,42 +344,37 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
   uint32_t a = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kCohK; ++k) {
-    if (first + k < cnt) {
+    if (kFull || first + k < cnt) {
       const uint32_t te = ev_transform(e[k]);
       a = ((hmask >> k) & 1u) ? tcompose(kConst | hs[k], te) : tcompose(a, te);
     }
   }
-  uint32_t cur = block_excl_compose(a, carry[b], wtot);
+  uint32_t cur = block_excl_compose(a, cin, wtot);
 
-  // ---- walk: incoming state of every event -> faults / invalidations / transfers
-  uint64_t nf_lo = 0, nf_hi = 0;
-  uint32_t inv = 0, xfer = 0, fmask = 0;
-  uint32_t endst[kCohK];
+  // ---- walk: incoming state of every event -> faults / invalidations / transfers; the
+  // state word of a page is written at its segment's last event
+  uint32_t nf = 0, inv = 0, xfer = 0, fmask = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kCohK; ++k) {
-    endst[k] = 0;
-    if (first + k < cnt) {
+    if (kFull || first + k < cnt) {
       const uint32_t node = (uint32_t)(e[k] >> 1) & 7u;
       const bool wr = e[k] & 1u;
       const uint32_t S = ((hmask >> k) & 1u) ? (kConst | hs[k]) : cur;
       if (!(S & kConst)) bad = 1;
-      const uint32_t cs = S & 0xFFu, owner = (S >> 8) & 0xFFu, st = (S >> 16) & 3u;
+      const uint32_t cs = S & 0xFFu, owner = (S >> 8) & 0xFFu;
+      const bool excl = ((S >> 16) & 3u) == 2u;
       const uint32_t bit = 1u << node;
-      uint32_t fault;
-      if (!wr) {
-        fault = (cs & bit) ? 0u : 1u;
-      } else {
-        fault = (st == 2u && owner == node) ? 0u : 1u;
-        if (fault) {
-          inv += (uint32_t)__popc(cs & ~bit);
-          xfer += (owner != node) ? 1u : 0u;
-        }
-      }
-      const uint64_t inc1 = (uint64_t)fault << (16 * (node & 3u));
-      if (node < 4) nf_lo += inc1; else nf_hi += inc1;
+      const bool fw = !(excl && owner == node);          // write fault
+      const bool fr = (cs & bit) == 0u;                  // read fault
+      const uint32_t fault = (wr ? fw : fr) ? 1u : 0u;
+      const bool wf = wr && fw;
+      inv += wf ? (uint32_t)__popc(cs & ~bit) : 0u;
+      xfer += (wf && owner != node) ? 1u : 0u;
+      nf += fault << (4u * node);                        // 8 nibbles: <= 8 events/thread
       fmask |= fault << k;
       cur = tcompose(S, ev_transform(e[k]));
-      endst[k] = cur & ~kConst;
+      const uint64_t pg = ev_page(e[k]);
+      if (((emask >> k) & 1u) && pg < n_pages) pst[2 * pg] = cur & ~kConst;
     }
   }
 
@@ -363,7 +382,7 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
   uint32_t sv = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kCohK; ++k) {
-    if (first + k < cnt) {
+    if (kFull || first + k < cnt) {
       const uint32_t f = (fmask >> k) & 1u;
       sv = segsum(sv, ((hmask >> k) & 1u) ? (kConst | (hf[k] + f)) : f);
     }
@@ -381,7 +400,7 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
 #pragma unroll
   for (uint32_t k = 0; k < kCohK; ++k) {
     const uint32_t x = first + k;
-    if (x < cnt) {
+    if (kFull || x < cnt) {
       const uint32_t f = (fmask >> k) & 1u;
       if ((hmask >> k) & 1u) {
         running = hf[k] + f;
@@ -392,13 +411,11 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
       const uint64_t pg = ev_page(e[k]);
       if (pg < n_pages) {
         if ((emask >> k) & 1u) {
-          if (head_in_block) {
-            pt[pg] = (uint64_t)endst[k] | ((uint64_t)running << 32);  // closed here
-          } else {
-            pst[2 * pg] = endst[k];                                   // opened earlier
-            if (running) atomicAdd(&pfl[2 * pg], running);
-          }
-        } else if (x + 1 == cnt) {                                   // continues
+          if (head_in_block)
+            pfl[2 * pg] = running;                     // segment closed in this block
+          else if (running)
+            atomicAdd(&pfl[2 * pg], running);          // opened in an earlier block
+        } else if (x + 1 == cnt) {                     // continues into the next block
           const uint32_t add = head_in_block ? running - lh_old : running;
           if (add) atomicAdd(&pfl[2 * pg], add);
         }
@@ -406,10 +423,15 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
     }
   }
 
-  // ---- block partial row: inv, xfer, node faults 0..7
+  // ---- block partial row: inv, xfer, node faults 0..7 (nibbles -> 16-bit fields)
+  uint64_t nf_lo = 0, nf_hi = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    nf_lo |= (uint64_t)((nf >> (4 * q)) & 0xFu) << (16 * q);
+    nf_hi |= (uint64_t)((nf >> (4 * (q + 4))) & 0xFu) << (16 * q);
+  }
   const uint64_t slo = wave_sum64(nf_lo), shi = wave_sum64(nf_hi);
   const uint32_t sinv = (uint32_t)wave_sum64(inv), sxf = (uint32_t)wave_sum64(xfer);
-  const uint64_t anybad = __ballot(bad != 0);
   if (lane == 0) {
     red[wave][0] = sinv;
     red[wave][1] = sxf;
@@ -418,10 +440,49 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
       red[wave][2 + q] = (uint32_t)(slo >> (16 * q)) & 0xFFFFu;
       red[wave][6 + q] = (uint32_t)(shi >> (16 * q)) & 0xFFFFu;
     }
-    if (anybad) atomicOr(err, 2u);
   }
   __syncthreads();
   if (t < 10) partial[b * 10 + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(256) void coh_apply_kernel(
+    uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
+    uint64_t nb, const uint32_t* __restrict__ carry, const uint32_t* __restrict__ last_head,
+    const uint64_t* __restrict__ head_pt, uint32_t* __restrict__ partial,
+    uint32_t* __restrict__ err) {
+  __shared__ uint32_t wtot[4];
+  __shared__ uint64_t bnd[8];
+  __shared__ uint32_t red[4][10];
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  const uint32_t first = t * kCohK;
+  uint32_t bad = 0;
+  uint64_t e[kCohK];
+  uint64_t b = blockIdx.x;
+  if (b < nb) load_block_events<kVec>(ev, n, b * kCohBlock + first, e);
+  for (; b < nb; b += gridDim.x) {
+    const uint64_t b0 = b * kCohBlock;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kCohBlock, n - b0);
+    uint64_t en[kCohK];
+    const bool more = b + gridDim.x < nb;
+    if (more) load_block_events<kVec>(ev, n, (b + gridDim.x) * kCohBlock + first, en);
+    const uint64_t before = (b0 > 0) ? ev[b0 - 1] : 0ull;
+    const bool has_after = b0 + cnt < n;
+    const uint64_t after = has_after ? ev[b0 + cnt] : 0ull;
+    const uint32_t lh = last_head[b];
+    const uint64_t lhp = head_pt[b];
+    const uint32_t cin = carry[b];
+
+    if (cnt == kCohBlock)
+      coh_block<true>(pt, n_pages, e, b, b0, cnt, before, has_after, after, lh, lhp, cin,
+                      partial, wtot, bnd, red, bad);
+    else
+      coh_block<false>(pt, n_pages, e, b, b0, cnt, before, has_after, after, lh, lhp, cin,
+                       partial, wtot, bnd, red, bad);
+#pragma unroll
+    for (uint32_t k = 0; k < kCohK; ++k) e[k] = en[k];
+  }
+  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
 // ---------------------------------------------------------------- D: totals
@@ -516,8 +577,24 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* even
   }
   {
     ProfScope ps(prof, 7, s);
-    hipLaunchKernelGGL(coh_apply_kernel, dim3((unsigned)nb), dim3(256), 0, s, pt, n_pages,
-                       events, n_events, carry, lh, head_pt, partial, err);
+    // Persistent grid: every workgroup walks blocks b, b + grid, ... (no inter-workgroup
+    // waiting, so residency is only a speed question).
+    static int grid = 0;
+    if (!grid) {
+      int dev = 0, cus = 256, per = 4;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, coh_apply_kernel<true>, 256, 0);
+      grid = cus * (per > 0 ? per : 4);
+    }
+    const unsigned g2 = (unsigned)min((uint64_t)grid, nb);
+    const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
+    if (vec)
+      hipLaunchKernelGGL(coh_apply_kernel<true>, dim3(g2), dim3(256), 0, s, pt, n_pages, events,
+                         n_events, nb, carry, lh, head_pt, partial, err);
+    else
+      hipLaunchKernelGGL(coh_apply_kernel<false>, dim3(g2), dim3(256), 0, s, pt, n_pages, events,
+                         n_events, nb, carry, lh, head_pt, partial, err);
   }
   uint64_t g = (nb + 255) / 256;
   if (g > 1024) g = 1024;
