@@ -26,7 +26,7 @@ vp = C.c_void_p
 
 class GdsmRuns(C.Structure):
     _fields_ = [("n", C.c_uint64), ("rec_off", vp), ("data", vp), ("cap", C.c_uint64),
-                ("owned", C.c_uint32), ("_pad", C.c_uint32)]
+                ("n_cap", C.c_uint64), ("owned", C.c_uint32), ("_pad", C.c_uint32)]
 
 
 # name -> (restype, argtypes)
@@ -42,10 +42,12 @@ SIGNATURES = {
     "gdsm_sync": (C.c_int, [vp]),
     "gdsm_upload": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, vp]),
     "gdsm_download": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, vp]),
+    "gdsm_reserve": (C.c_int, [vp, C.c_uint64, C.c_uint64]),
     "gdsm_dev_alloc": (C.c_int, [vp, C.c_uint64, C.POINTER(vp)]),
     "gdsm_dev_free": (C.c_int, [vp, vp]),
     "gdsm_memcpy_h2d": (C.c_int, [vp, vp, vp, C.c_uint64]),
     "gdsm_memcpy_d2h": (C.c_int, [vp, vp, vp, C.c_uint64]),
+    "gdsm_memcpy_d2d": (C.c_int, [vp, vp, vp, C.c_uint64]),
     "gdsm_prof_enable": (C.c_int, [vp, C.c_int]),
     "gdsm_prof_read": (C.c_int, [vp, C.POINTER(C.c_double), u64p]),
     "gdsm_gen_pages": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,

@@ -197,6 +197,19 @@ int gdsm_download(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void* ho
   return page_copy(ctx, which, first, n, host, false);
 }
 
+int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events) {
+  if (!ctx) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  int rc = 0;
+  if (diff_pages) {
+    const uint64_t chunk = diff_pages < gdsm::kDiffChunk ? diff_pages : gdsm::kDiffChunk;
+    rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk));
+  }
+  if (!rc && coh_events)
+    rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(coh_events));
+  return rc;
+}
+
 int gdsm_dev_alloc(gdsm_ctx* ctx, uint64_t bytes, void** dev_ptr) {
   if (!ctx || !dev_ptr) return -EINVAL;
   DeviceGuard g(ctx->device);
@@ -257,6 +270,14 @@ int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches) {
   return 0;
 }
 
+int gdsm_memcpy_d2d(gdsm_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+  if (!ctx || (bytes && (!dst || !src))) return -EINVAL;
+  if (!bytes) return 0;
+  DeviceGuard g(ctx->device);
+  GDSM_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return 0;
+}
+
 int gdsm_gen_pages(gdsm_ctx* ctx, uint32_t arenas, uint64_t first_global, uint64_t stride,
                    uint64_t seed, int mode, uint32_t ppm) {
   if (!ctx) return -EINVAL;
@@ -309,6 +330,7 @@ int gdsm_runs_alloc(gdsm_ctx* ctx, uint64_t n, uint64_t cap, gdsm_runs* out) {
   ctx->allocs.insert(ro);
   ctx->allocs.insert(d);
   out->n = n;
+  out->n_cap = n;
   out->rec_off = static_cast<uint64_t*>(ro);
   out->data = static_cast<uint8_t*>(d);
   out->cap = cap;
@@ -331,7 +353,7 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
   if (!ctx || !out || !out->rec_off || (!out->data && out->cap)) return -EINVAL;
   if (!ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
   if (!ids && n > ctx->n_pages) return -EINVAL;
-  if (out->n < n && out->owned) return -EINVAL;
+  if (out->n_cap ? n > out->n_cap : (out->owned && n > out->n)) return -EINVAL;
   DeviceGuard g(ctx->device);
   const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
   int rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk ? chunk : 1));

@@ -71,10 +71,11 @@ typedef struct gdsm_ctx gdsm_ctx;
 
 /* A diff stream (SPEC §3). All pointers are device pointers. */
 typedef struct gdsm_runs {
-  uint64_t n;        /* records */
+  uint64_t n;        /* records in the stream (set by gdsm_diff) */
   uint64_t* rec_off; /* n + 1 */
   uint8_t* data;     /* cap bytes */
-  uint64_t cap;
+  uint64_t cap;      /* data capacity in bytes */
+  uint64_t n_cap;    /* record capacity: rec_off holds n_cap + 1 entries */
   uint32_t owned;    /* 1 if allocated by gdsm_runs_alloc */
   uint32_t _pad;
 } gdsm_runs;
@@ -93,11 +94,16 @@ int gdsm_sync(gdsm_ctx* ctx);
 /* Synchronous host <-> arena copies of pages [first, first+n). */
 int gdsm_upload(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, const void* host);
 int gdsm_download(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void* host);
+/* Pre-sizes the context's diff and coherence workspaces so later calls never reallocate (a
+ * reallocation synchronises the device). */
+int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events);
 /* Device scratch owned by the context (freed by gdsm_fini). */
 int gdsm_dev_alloc(gdsm_ctx* ctx, uint64_t bytes, void** dev_ptr);
 int gdsm_dev_free(gdsm_ctx* ctx, void* dev_ptr);
 int gdsm_memcpy_h2d(gdsm_ctx* ctx, void* dev, const void* host, uint64_t bytes);
 int gdsm_memcpy_d2h(gdsm_ctx* ctx, void* host, const void* dev, uint64_t bytes);
+/* Asynchronous device-to-device copy on the context stream. */
+int gdsm_memcpy_d2d(gdsm_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 
 /* Per-kernel timing: when enabled, every kernel the context launches is bracketed by HIP events
  * on its stream; gdsm_prof_read synchronises and returns the summed milliseconds and launch
@@ -121,8 +127,8 @@ int gdsm_twin(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n);
 /* Allocates a stream for n records with `cap` data bytes (cap 0: worst case n*10244). */
 int gdsm_runs_alloc(gdsm_ctx* ctx, uint64_t n, uint64_t cap, gdsm_runs* out);
 int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs);
-/* Diffs TWIN against CURRENT for the listed pages into `out` (out->n must be >= n; out->n is
- * set to n). Asynchronous; use gdsm_runs_total to learn the size. */
+/* Diffs TWIN against CURRENT for the listed pages into `out` (n <= out->n_cap; out->n is set
+ * to n). Asynchronous; use gdsm_runs_total to learn the size. */
 int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out);
 /* Synchronises, returns rec_off[n] in *total; -ENOSPC if it exceeded runs->cap. */
 int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total);
