@@ -65,6 +65,26 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_bcast(wav
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) { return dpp0<0x138>(v); }
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) { return dpp0<0x130>(v); }
 
+// ---- 16-lane DPP rows
+__device__ __forceinline__ uint32_t row_incl_sum(uint32_t x) {
+  x += dpp0<0x111>(x);
+  x += dpp0<0x112>(x);
+  x += dpp0<0x114>(x);
+  x += dpp0<0x118>(x);
+  return x;
+}
+__device__ __forceinline__ uint32_t row_incl_max(uint32_t x) {
+  x = max(x, dpp0<0x111>(x));
+  x = max(x, dpp0<0x112>(x));
+  x = max(x, dpp0<0x114>(x));
+  x = max(x, dpp0<0x118>(x));
+  return x;
+}
+// Lane 15 of the row, broadcast to the whole row (row_newbcast:15).
+__device__ __forceinline__ uint32_t row_last(uint32_t x) { return dpp0<0x15F>(x); }
+// Lane r-1 of the row (lane 0 of the row gets 0).
+__device__ __forceinline__ uint32_t row_prev(uint32_t x) { return dpp0<0x111>(x); }
+
 // Inclusive suffix minimum across lanes (lane l gets min over lanes >= l); bpermute based.
 __device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v) {
   const uint32_t lane = lane_id();

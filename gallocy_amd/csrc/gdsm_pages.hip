@@ -353,68 +353,65 @@ __device__ __forceinline__ void store_run_chunk(uint8_t* __restrict__ page, uint
   store_chunk(page + cs, mask, pay, pp + (lo - off));
 }
 
-// Applies one record (whole wave), one lane per run. Pass 1 validates every header (length,
-// bounds, sorted and non-overlapping, total size) so a malformed record writes nothing. Pass 2
-// stores: runs touching <= 2 chunks are stored by their own lane; otherwise the group's
-// (run, chunk) pairs are spread over the lanes (binary search over the runs' pair offsets in
-// LDS), so a 4096-byte run costs 4 wave iterations, not 256 lane iterations.
+// Applies up to four records at once, one per 16-lane DPP row (a lane per run). Pass 1 validates
+// every header of the row's record (length, bounds, sorted and non-overlapping, total size), so
+// a malformed record writes nothing. Pass 2 spreads the record's (run, 16-B chunk) pairs over
+// the row's lanes — a run is found by a 4-step binary search over the row's pair offsets — so
+// short and long runs cost the same per byte. `has` is false for rows without a record.
+// Returns false in the lanes of a row whose record is malformed.
 template <typename P32, typename P8>
-__device__ __forceinline__ bool apply_record(uint8_t* __restrict__ page, P32 rec32, P8 rec8,
-                                             uint32_t size, uint32_t* __restrict__ scratch) {
-  const uint32_t lane = lane_id();
-  const uint32_t nr = rec32[0];
-  if (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr) return false;
-  uint32_t pay_total = 0, prev_end = 0, bad = 0;
-  for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-    const uint32_t r = r0 + lane;
-    const uint32_t h = (r < nr) ? rec32[1 + r] : 0u;
-    const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
-    uint32_t pe = from_prev_lane(end);
-    if (lane == 0) pe = prev_end;
-    if (r < nr && (len == 0 || end > kPage || off < pe)) bad = 1;
-    pay_total += wave_sum(len);
-    prev_end = lane_bcast(end, 63);
+__device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32, P8 rec8,
+                                           uint32_t size, bool has) {
+  const uint32_t lane = lane_id(), lr = lane & 15, rb = lane & ~15u;
+  uint32_t nr = has ? rec32[0] : 0u;
+  bool bad = has && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr);
+  if (bad) nr = 0;
+  const uint32_t nit = lane_bcast(wave_incl_max((nr + 15u) >> 4), 63);
+  uint32_t pay = 0, prev_end = 0, lbad = 0;
+  for (uint32_t it = 0; it < nit; ++it) {
+    const uint32_t r = it * 16u + lr;
+    const bool v = r < nr;
+    const uint32_t h = v ? rec32[1 + r] : 0u;
+    const uint32_t off = h & 0xFFFFu, len = h >> 16, end = v ? off + len : 0u;
+    uint32_t pe = row_prev(end);
+    if (lr == 0) pe = prev_end;
+    if (v && (len == 0 || end > kPage || off < pe)) lbad = 1;
+    pay += row_last(row_incl_sum(v ? len : 0u));
+    prev_end = row_last(end);
   }
-  if (wave_sum(bad) || size != 4u + 4u * nr + ((pay_total + 3u) & ~3u)) return false;
-
-  const uint32_t pay0 = 4u + 4u * nr;  // payload start inside the record
+  if (row_last(row_incl_max(lbad))) bad = true;
+  if (has && !bad && size != 4u + 4u * nr + ((pay + 3u) & ~3u)) bad = true;
+  const uint32_t nrw = bad ? 0u : nr;  // runs this row writes
+  const uint32_t nit2 = lane_bcast(wave_incl_max((nrw + 15u) >> 4), 63);
   uint32_t pcarry = 0;
-  uint32_t* ci = scratch;        // [64] exclusive (run, chunk) pair offsets of the group
-  uint32_t* ppa = scratch + 64;  // [64] payload offsets of the group's runs
-  for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-    const uint32_t r = r0 + lane;
-    const uint32_t h = (r < nr) ? rec32[1 + r] : 0u;
-    const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
-    const uint32_t pinc = wave_incl_sum(len);
-    const uint32_t pp = pay0 + pcarry + pinc - len;  // payload of this run
-    pcarry += lane_bcast(pinc, 63);
+  for (uint32_t it = 0; it < nit2; ++it) {
+    const uint32_t r = it * 16u + lr;
+    const bool v = r < nrw;
+    const uint32_t h = v ? rec32[1 + r] : 0u;
+    const uint32_t off = h & 0xFFFFu, len = v ? h >> 16 : 0u, end = off + len;
+    const uint32_t pinc = row_incl_sum(len);
+    const uint32_t pp = 4u + 4u * nr + pcarry + pinc - len;  // payload of this run
+    pcarry += row_last(pinc);
     const uint32_t nch = len ? ((end - 1u) >> 4) - (off >> 4) + 1u : 0u;
-    const uint32_t cmax = lane_bcast(wave_incl_max(nch), 63);
-    if (cmax <= 2) {
-      for (uint32_t q = 0; q < nch; ++q)
-        store_run_chunk(page, ((off >> 4) + q) << 4, off, end, rec8, pp);
-      continue;
-    }
-    const uint32_t cinc = wave_incl_sum(nch);
-    const uint32_t T = lane_bcast(cinc, 63);
-    ci[lane] = cinc - nch;
-    ppa[lane] = pp;
-    wave_lds_sync();
-    for (uint32_t g = lane; g < T; g += 64) {
+    const uint32_t cinc = row_incl_sum(nch);
+    const uint32_t cex = cinc - nch;
+    const uint32_t T = row_last(cinc);
+    const uint32_t tmax = lane_bcast(wave_incl_max(T), 63);
+    for (uint32_t g = lr; g < ((tmax + 15u) & ~15u); g += 16) {
       uint32_t i = 0;
 #pragma unroll
-      for (uint32_t step = 32; step; step >>= 1)
-        if (i + step < 64 && ci[i + step] <= g) i += step;
-      // lane i's run: fetch its header and payload offset from the lane that owns it
-      const uint32_t hi = rec32[1 + r0 + i];
-      const uint32_t o = hi & 0xFFFFu, e = o + (hi >> 16);
-      const uint32_t ppi = ppa[i];
-      const uint32_t cs = ((o >> 4) + (g - ci[i])) << 4;
-      store_run_chunk(page, cs, o, e, rec8, ppi);
+      for (uint32_t step = 8; step; step >>= 1) {
+        const uint32_t c = (uint32_t)__shfl(cex, (int)(rb + i + step), 64);
+        if (c <= g) i += step;
+      }
+      const uint32_t oi = (uint32_t)__shfl(off, (int)(rb + i), 64);
+      const uint32_t ei = (uint32_t)__shfl(end, (int)(rb + i), 64);
+      const uint32_t pi = (uint32_t)__shfl(pp, (int)(rb + i), 64);
+      const uint32_t ci = (uint32_t)__shfl(cex, (int)(rb + i), 64);
+      if (g < T) store_run_chunk(page, ((oi >> 4) + (g - ci)) << 4, oi, ei, rec8, pi);
     }
-    wave_lds_sync();
   }
-  return true;
+  return !bad;
 }
 
 __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target,
@@ -423,10 +420,8 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
                                                     const uint8_t* __restrict__ data,
                                                     uint32_t* __restrict__ err) {
   __shared__ __attribute__((aligned(16))) uint32_t win_all[4][kApplyWin / 4];
-  __shared__ uint32_t bm_all[4][128];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, row = lane >> 4;
   uint32_t* win = win_all[wave];
-  uint32_t* bm = bm_all[wave];
   const uint64_t ntask = (n + 63) / 64;
   uint32_t bad = 0;
   for (uint64_t task = (uint64_t)blockIdx.x * 4 + wave; task < ntask;
@@ -443,15 +438,14 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
       const uint64_t fm = __ballot(fits);
       uint32_t k = fm ? 63u - (uint32_t)__clzll(fm) : j;  // highest lane whose offset fits
       if (cnt == 64 && (end_off - start) <= kApplyWin) k = 64;
-      if (k == j) {  // record j alone exceeds the window: straight from global
-        const uint64_t r0 = start, r1 = (j + 1 < 64) ? lane_bcast64(my_off, j + 1) : end_off;
-        if (r1 > r0) {
-          const uint64_t p = ids ? ids[a + j] : a + j;
-          const uint8_t* rec = data + r0;
-          if (!apply_record(target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec,
-                            (uint32_t)(r1 - r0), bm))
-            bad = 1;
-        }
+      if (k == j) {  // record j alone exceeds the window: straight from global, row 0 only
+        const uint64_t r1 = (j + 1 < 64) ? lane_bcast64(my_off, j + 1) : end_off;
+        const uint64_t p = ids ? ids[a + j] : a + j;
+        const uint8_t* rec = data + start;
+        const bool has = row == 0 && r1 > start;
+        if (!apply_rows(target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec,
+                        (uint32_t)(r1 - start), has))
+          bad = 1;
         ++j;
         continue;
       }
@@ -461,21 +455,27 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
       for (uint32_t q = lane; q < words; q += 64) win[q] = src[q];
       wave_lds_sync();
       const uint8_t* win8 = reinterpret_cast<const uint8_t*>(win);
-      for (uint32_t jj = j; jj < k; ++jj) {
-        const uint64_t r0 = lane_bcast64(my_off, jj);
-        const uint64_t r1 = (jj + 1 == k) ? stop : lane_bcast64(my_off, jj + 1);
-        if (r1 == r0) continue;
+      for (uint32_t jj = j; jj < k; jj += 4) {
+        const uint32_t mine = jj + row;  // this row's record
+        const bool in = mine < k;
+        const uint32_t ms = in ? mine : jj;
+        // both shuffles run in every lane: a bpermute from a lane that is switched off by a
+        // branch returns garbage, and `?:` would evaluate the second one in some rows only
+        const uint64_t r0 = __shfl(my_off, (int)ms, 64);
+        const uint64_t nx = __shfl(my_off, (int)min(ms + 1, 63u), 64);
+        const uint64_t r1 = (ms + 1 == k) ? stop : nx;
+        const bool has = in && r1 > r0;
         const uint32_t base = (uint32_t)(r0 - start);
-        const uint64_t p = ids ? ids[a + jj] : a + jj;
-        if (!apply_record(target + p * kPage, win + base / 4, win8 + base, (uint32_t)(r1 - r0),
-                          bm))
+        const uint64_t p = ids ? ids[a + ms] : a + ms;
+        if (!apply_rows(target + p * kPage, win + base / 4, win8 + base, (uint32_t)(r1 - r0),
+                        has))
           bad = 1;
       }
       wave_lds_sync();
       j = k;
     }
   }
-  if (bad && lane == 0) atomicOr(err, 1u);
+  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 1u);
 }
 
 // ------------------------------------------------------------------------- launchers
