@@ -4,6 +4,11 @@
 One step = diff of every page of the shard (TWIN vs CURRENT -> canonical run stream, SPEC §3)
 + apply of that stream to the REPLICA arena (SPEC §4); for N > 1 the records whose home shard
 is another rank are exchanged over RCCL (all-to-all) between the two (gallocy_amd/exchange.py).
+With --overlap on (the default for N > 1) steps are double-buffered: the exchange and apply of
+step k run on a second stream while step k+1 is diffed, hiding the RCCL all-to-all. On one GPU
+the default is serial (diff k+1 starts after apply k): the step is HBM-bound there and an
+overlapped apply only takes its bandwidth from the diff (measured within a few % either way).
+Every step is complete when the clock stops; the line reports the other mode's ms/step too.
 
 Workload (BASELINE.json configs[1]): 1M x 4 KiB pages per GPU, 1 % random 8-byte word writes,
 synthetic (SPEC §6), inputs resident in HBM before the timed region. Weak scaling: every rank
@@ -44,6 +49,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=2026)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="double-buffered steps (exchange/apply k overlaps diff k+1); auto = on "
+                         "for N > 1 (hides the RCCL exchange), off on one GPU (HBM-bound)")
     ap.add_argument("--workload", choices=["pages", "coherence", "mmult"], default="pages",
                     help="pages: BASELINE configs[1]/[2] (the headline); coherence: configs[3]; "
                          "mmult: configs[4] trace replay")
@@ -251,23 +259,38 @@ def main():
     ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n, stride=1,
                   arenas=("replica",))
     cap = n * (256 if mode == ga.GEN_UNIFORM else 1024)
-    runs = ga.Runs(ctx, n, cap=cap)
+    # Two diff streams: release k+1 is diffed while release k is exchanged / applied
+    # (gdsm_apply_async on one GPU, exchange.Shard's comm stream for N > 1).
+    runs = [ga.Runs(ctx, n, cap=cap) for _ in range(2)]
     shard = exchange.Shard(ctx, runs, rank, world, n) if world > 1 else None
     if shard is not None:
         shard.gen_args = (args.seed, mode, ppm)
 
-    def step():
-        ctx.diff(out=runs)
-        if shard is None:
-            ctx.apply(runs)
-        else:
-            shard.exchange_and_apply()
+    def steps(k: int, pipelined: bool):
+        if shard is not None:
+            if pipelined:
+                shard.run(k)
+            else:
+                for _ in range(k):
+                    ctx.diff(out=runs[0])
+                    shard.exchange_and_apply()
+                    shard.drain()
+            return
+        for i in range(k):
+            r = runs[i % 2] if pipelined else runs[0]
+            ctx.diff(out=r)
+            (ctx.apply_async if pipelined else ctx.apply)(r)
 
-    for _ in range(args.warmup):
-        step()
-    ctx.sync()
-    total = runs.total()  # raises ENOSPC if the capacity was too small
-    host = runs.to_host()
+    def drain():
+        if shard is not None:
+            shard.drain()
+        ctx.sync()
+
+    steps(args.warmup, True)
+    drain()
+    total = runs[0].total()  # raises ENOSPC if the capacity was too small
+    assert runs[1].total() == total or args.warmup < 2
+    host = runs[0].to_host()
     pay = payload_bytes(host.rec_off, host.data)
     del host
 
@@ -275,23 +298,32 @@ def main():
         if world > 1:
             dist.barrier()
 
-    barrier()
-    torch.cuda.synchronize()
-    ctx.prof_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    ctx.sync()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    prof = ctx.prof_read()
-    ctx.prof_enable(False)
-    dt = t1 - t0
-    if world > 1:
-        t = torch.tensor([dt], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    def timed(pipelined: bool, prof: bool):
+        barrier()
+        drain()
+        torch.cuda.synchronize()
+        if prof:
+            ctx.prof_enable(True)
+        t0 = time.perf_counter()
+        steps(args.steps, pipelined)
+        drain()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        p = ctx.prof_read() if prof else None
+        if prof:
+            ctx.prof_enable(False)
+        dt = t1 - t0
+        if world > 1:
+            t = torch.tensor([dt], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, p
+
+    # the other mode first, for reference, then the measured run; both over the same K steps
+    pipelined = args.overlap == "on" or (args.overlap == "auto" and world > 1)
+    dt_other, _ = timed(not pipelined, False)
+    dt, prof = timed(pipelined, True)
 
     # correctness of the measured work: REPLICA == CURRENT afterwards (diff of the two is empty)
     chk = ga.Runs(ctx, n, cap=1 << 20)
@@ -332,6 +364,9 @@ def main():
                        "pages_per_gpu": n, "seed": args.seed, "parallelism": f"page-shard x{world}",
                        "diff_bytes_per_step": int(total), "payload_bytes_per_step": int(pay)},
             "step_hbm_gbs": round(step_bytes * args.steps / dt / 1e9, 1),
+            "pipelined": pipelined,
+            ("serial_ms_per_step" if pipelined else "pipelined_ms_per_step"):
+                round(dt_other / args.steps * 1e3, 4),
             "roofline": {"bound": "hbm", "kernel": "diff_pages_kernel",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -339,6 +374,9 @@ def main():
                          "algorithmic_bytes_per_launch": int(diff_bytes),
                          "avg_launch_ms": round(avg_diff_ms, 4)},
             "stages": stages,
+            "exchange": None if shard is None else {
+                "sent_remote_bytes_per_step": shard.sent_remote,
+                "received_bytes_per_step": shard.received},
             "replica_equals_current": bool(replica_ok),
             "cpu_baseline": None,
         }

@@ -60,9 +60,10 @@ SIGNATURES = {
     "gdsm_diff": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns)]),
     "gdsm_runs_total": (C.c_int, [vp, C.POINTER(GdsmRuns), C.POINTER(C.c_uint64)]),
     "gdsm_apply": (C.c_int, [vp, C.c_int, vp, C.POINTER(GdsmRuns)]),
+    "gdsm_apply_async": (C.c_int, [vp, C.c_int, vp, C.POINTER(GdsmRuns)]),
     "gdsm_diff_workspace_bytes": (C.c_uint64, [C.c_uint64]),
     "gdsm_diff_raw": (C.c_int, [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, C.c_uint64, vp]),
-    "gdsm_apply_raw": (C.c_int, [vp, vp, C.c_uint64, vp, vp, vp]),
+    "gdsm_apply_raw": (C.c_int, [vp, vp, C.c_uint64, vp, vp, vp, vp]),
     "gdsm_twin_raw": (C.c_int, [vp, vp, vp, C.c_uint64, vp]),
     "gdsm_coh_init": (C.c_int, [vp, C.c_uint32]),
     "gdsm_coherence_batch": (C.c_int, [vp, vp, C.c_uint64, u64p]),

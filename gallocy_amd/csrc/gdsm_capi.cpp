@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <new>
 #include <set>
@@ -26,6 +27,14 @@ struct gdsm_ctx {
   uint64_t* coh_totals = nullptr;  // device 10 x u64
   uint32_t n_nodes = 0;
   std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks
+  // gdsm_apply_async: applies run on `aux`, ordered after everything enqueued on `stream` before
+  // them; every other operation joins `aux` first, except gdsm_diff, which only waits for the
+  // apply still reading its output stream (runs_busy) or writing an arena it reads.
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_main = nullptr, ev_aux = nullptr;
+  bool aux_pending = false;
+  uint32_t aux_targets = 0;                      // arenas written by pending async applies
+  std::map<const void*, hipEvent_t> runs_busy;   // rec_off -> last async apply reading it
   gdsm::Prof prof;
   gdsm::Prof* P() { return prof.on ? &prof : nullptr; }
 };
@@ -59,6 +68,22 @@ struct DeviceGuard {
     int cur = -1;
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
+};
+
+// Makes `stream` wait for every pending async apply.
+int join_aux(gdsm_ctx* ctx) {
+  if (!ctx->aux_pending) return 0;
+  GDSM_TRY(hipEventRecord(ctx->ev_aux, ctx->aux));
+  GDSM_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_aux, 0));
+  ctx->aux_pending = false;
+  ctx->aux_targets = 0;
+  return 0;
+}
+
+// Device guard for an operation on the context's stream: ordered after pending async applies.
+struct CtxGuard : DeviceGuard {
+  int rc;
+  explicit CtxGuard(gdsm_ctx* c) : DeviceGuard(c->device), rc(join_aux(c)) {}
 };
 
 int ensure(uint8_t** buf, uint64_t* have, uint64_t need) {
@@ -142,7 +167,8 @@ int gdsm_init(gdsm_ctx** out, int device, uint64_t n_pages, uint32_t flags) {
 
 int gdsm_fini(gdsm_ctx* ctx) {
   if (!ctx) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (auto& a : ctx->arena)
     if (a) (void)hipFree(a);
@@ -152,6 +178,10 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->coh_ws) (void)hipFree(ctx->coh_ws);
   if (ctx->coh_pt) (void)hipFree(ctx->coh_pt);
   if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
+  for (auto& kv : ctx->runs_busy) (void)hipEventDestroy(kv.second);
+  if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
+  if (ctx->ev_aux) (void)hipEventDestroy(ctx->ev_aux);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return 0;
@@ -165,11 +195,17 @@ int gdsm_arena(gdsm_ctx* ctx, int which, void** dev_ptr) {
 
 uint64_t gdsm_n_pages(const gdsm_ctx* ctx) { return ctx ? ctx->n_pages : 0; }
 
-void* gdsm_stream(gdsm_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+void* gdsm_stream(gdsm_ctx* ctx) {
+  if (!ctx) return nullptr;
+  DeviceGuard g(ctx->device);
+  (void)join_aux(ctx);  // the caller may enqueue anything on it
+  return reinterpret_cast<void*>(ctx->stream);
+}
 
 int gdsm_sync(gdsm_ctx* ctx) {
   if (!ctx) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   return check_and_clear_err(ctx);
 }
@@ -178,7 +214,8 @@ static int page_copy(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void*
   if (!ctx || which < 0 || which > 2 || !ctx->arena[which] || (!host && n)) return -EINVAL;
   if (first > ctx->n_pages || n > ctx->n_pages - first) return -EINVAL;
   if (n == 0) return 0;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   uint8_t* dev = ctx->arena[which] + first * GDSM_PAGE_SZ;
   const uint64_t bytes = n * GDSM_PAGE_SZ;
   if (up)
@@ -199,7 +236,8 @@ int gdsm_download(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void* ho
 
 int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events) {
   if (!ctx) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   int rc = 0;
   if (diff_pages) {
     const uint64_t chunk = diff_pages < gdsm::kDiffChunk ? diff_pages : gdsm::kDiffChunk;
@@ -212,7 +250,8 @@ int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events) {
 
 int gdsm_dev_alloc(gdsm_ctx* ctx, uint64_t bytes, void** dev_ptr) {
   if (!ctx || !dev_ptr) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   void* p = nullptr;
   GDSM_TRY(hipMalloc(&p, bytes ? bytes : 16));
   ctx->allocs.insert(p);
@@ -222,7 +261,8 @@ int gdsm_dev_alloc(gdsm_ctx* ctx, uint64_t bytes, void** dev_ptr) {
 
 int gdsm_dev_free(gdsm_ctx* ctx, void* dev_ptr) {
   if (!ctx || !dev_ptr || !ctx->allocs.count(dev_ptr)) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   (void)hipStreamSynchronize(ctx->stream);
   ctx->allocs.erase(dev_ptr);
   GDSM_TRY(hipFree(dev_ptr));
@@ -232,7 +272,8 @@ int gdsm_dev_free(gdsm_ctx* ctx, void* dev_ptr) {
 int gdsm_memcpy_h2d(gdsm_ctx* ctx, void* dev, const void* host, uint64_t bytes) {
   if (!ctx || (bytes && (!dev || !host))) return -EINVAL;
   if (!bytes) return 0;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
@@ -241,7 +282,8 @@ int gdsm_memcpy_h2d(gdsm_ctx* ctx, void* dev, const void* host, uint64_t bytes) 
 int gdsm_memcpy_d2h(gdsm_ctx* ctx, void* host, const void* dev, uint64_t bytes) {
   if (!ctx || (bytes && (!dev || !host))) return -EINVAL;
   if (!bytes) return 0;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
@@ -249,7 +291,8 @@ int gdsm_memcpy_d2h(gdsm_ctx* ctx, void* host, const void* dev, uint64_t bytes) 
 
 int gdsm_prof_enable(gdsm_ctx* ctx, int on) {
   if (!ctx) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   ctx->prof.resolve();
   ctx->prof.clear();
@@ -259,7 +302,8 @@ int gdsm_prof_enable(gdsm_ctx* ctx, int on) {
 
 int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches) {
   if (!ctx || !ms || !launches) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   ctx->prof.resolve();
   for (int i = 0; i < GDSM_PROF_STAGES; ++i) {
@@ -273,7 +317,8 @@ int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches) {
 int gdsm_memcpy_d2d(gdsm_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
   if (!ctx || (bytes && (!dst || !src))) return -EINVAL;
   if (!bytes) return 0;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
   return 0;
 }
@@ -287,7 +332,8 @@ int gdsm_gen_pages(gdsm_ctx* ctx, uint32_t arenas, uint64_t first_global, uint64
     if ((arenas & (1u << a)) && !ctx->arena[a]) return -EINVAL;
   if (mode != GDSM_GEN_UNIFORM && mode != GDSM_GEN_CLUSTERED) return -EINVAL;
   if (ppm > 1000000u) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   auto pick = [&](int a) { return (arenas & (1u << a)) ? ctx->arena[a] : nullptr; };
   GDSM_TRY(gdsm::launch_gen_pages(pick(GDSM_TWIN), pick(GDSM_CURRENT), pick(GDSM_REPLICA),
                                   ctx->n_pages, first_global, stride, seed, mode, ppm,
@@ -308,7 +354,8 @@ int gdsm_gen_pages_raw(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint64_t n
 int gdsm_twin(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n) {
   if (!ctx || !ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
   if (!ids && n > ctx->n_pages) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(gdsm::launch_twin(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              ctx->stream, ctx->P()));
   return 0;
@@ -318,7 +365,8 @@ int gdsm_runs_alloc(gdsm_ctx* ctx, uint64_t n, uint64_t cap, gdsm_runs* out) {
   if (!ctx || !out) return -EINVAL;
   if (cap == 0) cap = n * (uint64_t)GDSM_MAX_RECORD;
   cap = (cap + 15) & ~15ull;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   memset(out, 0, sizeof(*out));
   void* ro = nullptr;
   void* d = nullptr;
@@ -340,8 +388,14 @@ int gdsm_runs_alloc(gdsm_ctx* ctx, uint64_t n, uint64_t cap, gdsm_runs* out) {
 
 int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs) {
   if (!ctx || !runs || !runs->owned) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   (void)hipStreamSynchronize(ctx->stream);
+  auto it = ctx->runs_busy.find(runs->rec_off);
+  if (it != ctx->runs_busy.end()) {
+    (void)hipEventDestroy(it->second);
+    ctx->runs_busy.erase(it);
+  }
   for (void* p : {static_cast<void*>(runs->rec_off), static_cast<void*>(runs->data)}) {
     if (ctx->allocs.erase(p)) (void)hipFree(p);
   }
@@ -355,6 +409,12 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
   if (!ids && n > ctx->n_pages) return -EINVAL;
   if (out->n_cap ? n > out->n_cap : (out->owned && n > out->n)) return -EINVAL;
   DeviceGuard g(ctx->device);
+  if (ctx->aux_targets & ((1u << GDSM_TWIN) | (1u << GDSM_CURRENT))) {
+    int rc = join_aux(ctx);  // a pending apply writes an arena this diff reads
+    if (rc) return rc;
+  }
+  auto busy = ctx->runs_busy.find(out->rec_off);
+  if (busy != ctx->runs_busy.end()) GDSM_TRY(hipStreamWaitEvent(ctx->stream, busy->second, 0));
   const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
   int rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk ? chunk : 1));
   if (rc) return rc;
@@ -367,7 +427,8 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
 
 int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total) {
   if (!ctx || !runs || !total || !runs->rec_off) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   uint64_t t = 0;
   GDSM_TRY(hipMemcpyAsync(&t, runs->rec_off + runs->n, 8, hipMemcpyDeviceToHost, ctx->stream));
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
@@ -378,9 +439,31 @@ int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total) {
 int gdsm_apply(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_runs* in) {
   if (!ctx || !in || target < 0 || target > 2 || !ctx->arena[target]) return -EINVAL;
   if (!ids && in->n > ctx->n_pages) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(gdsm::launch_apply(ctx->arena[target], ids, in->n, in->rec_off, in->data, ctx->err,
                               ctx->stream, ctx->P()));
+  return 0;
+}
+
+int gdsm_apply_async(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_runs* in) {
+  if (!ctx || !in || target < 0 || target > 2 || !ctx->arena[target]) return -EINVAL;
+  if (!ids && in->n > ctx->n_pages) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  if (!ctx->aux) {
+    GDSM_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    GDSM_TRY(hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming));
+    GDSM_TRY(hipEventCreateWithFlags(&ctx->ev_aux, hipEventDisableTiming));
+  }
+  hipEvent_t& busy = ctx->runs_busy[in->rec_off];
+  if (!busy) GDSM_TRY(hipEventCreateWithFlags(&busy, hipEventDisableTiming));
+  GDSM_TRY(hipEventRecord(ctx->ev_main, ctx->stream));  // after the diff that produced `in`
+  GDSM_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_main, 0));
+  GDSM_TRY(gdsm::launch_apply(ctx->arena[target], ids, in->n, in->rec_off, in->data, ctx->err,
+                              ctx->aux, ctx->P()));
+  GDSM_TRY(hipEventRecord(busy, ctx->aux));
+  ctx->aux_pending = true;
+  ctx->aux_targets |= 1u << target;
   return 0;
 }
 
@@ -400,16 +483,16 @@ int gdsm_diff_raw(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, 
 }
 
 int gdsm_apply_raw(uint8_t* target, const uint32_t* ids, uint64_t n, const uint64_t* rec_off,
-                   const uint8_t* data, void* stream) {
+                   const uint8_t* data, uint32_t* err, void* stream) {
   if (!target || !rec_off || (!data && n)) return -EINVAL;
-  static uint32_t* err_word = nullptr;  // raw calls share one device error word per process
+  static uint32_t* sink = nullptr;  // unreported errors land here
   static std::mutex mu;
-  {
+  if (!err) {
     std::lock_guard<std::mutex> lk(mu);
-    if (!err_word) GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&err_word), 4));
-    GDSM_TRY(hipMemsetAsync(err_word, 0, 4, static_cast<hipStream_t>(stream)));
+    if (!sink) GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&sink), 4));
+    err = sink;
   }
-  GDSM_TRY(gdsm::launch_apply(target, ids, n, rec_off, data, err_word,
+  GDSM_TRY(gdsm::launch_apply(target, ids, n, rec_off, data, err,
                               static_cast<hipStream_t>(stream)));
   return 0;
 }
@@ -424,7 +507,8 @@ int gdsm_twin_raw(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64
 // ---- coherence -------------------------------------------------------------------------
 int gdsm_coh_init(gdsm_ctx* ctx, uint32_t n_nodes) {
   if (!ctx || n_nodes == 0 || n_nodes > GDSM_MAX_NODES) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   if (!ctx->coh_pt) {
     GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->coh_pt),
                        (ctx->n_pages ? ctx->n_pages : 1) * 8));
@@ -438,7 +522,8 @@ int gdsm_coh_init(gdsm_ctx* ctx, uint32_t n_nodes) {
 int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_events,
                                uint64_t* totals_dev) {
   if (!ctx || !ctx->coh_pt || !totals_dev || (!events && n_events)) return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   int rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
   if (rc) return rc;
   GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, events, n_events, totals_dev,
@@ -452,7 +537,8 @@ int gdsm_coherence_batch(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_event
   if (!ctx || !totals) return -EINVAL;
   int rc = gdsm_coherence_batch_async(ctx, events, n_events, ctx->coh_totals);
   if (rc) return rc;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(hipMemcpyAsync(totals, ctx->coh_totals, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost,
                           ctx->stream));
   return gdsm_sync(ctx);
@@ -463,7 +549,8 @@ int gdsm_coherence_batch(gdsm_ctx* ctx, const uint64_t* events, uint64_t n_event
 int gdsm_coh_download(gdsm_ctx* ctx, uint32_t* state, uint32_t* faults) {
   if (!ctx || !ctx->coh_pt) return -EINVAL;
   if (ctx->n_pages == 0) return 0;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   const uint32_t* base = reinterpret_cast<const uint32_t*>(ctx->coh_pt);
   if (state)
     GDSM_TRY(hipMemcpy2DAsync(state, 4, base, 8, 4, ctx->n_pages, hipMemcpyDeviceToHost,
@@ -478,7 +565,8 @@ int gdsm_coh_download(gdsm_ctx* ctx, uint32_t* state, uint32_t* faults) {
 int gdsm_coh_upload(gdsm_ctx* ctx, const uint32_t* state, const uint32_t* faults) {
   if (!ctx || !ctx->coh_pt) return -EINVAL;
   if (ctx->n_pages == 0) return 0;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   uint32_t* base = reinterpret_cast<uint32_t*>(ctx->coh_pt);
   if (state)
     GDSM_TRY(hipMemcpy2DAsync(base, 8, state, 4, 4, ctx->n_pages, hipMemcpyHostToDevice,
@@ -495,7 +583,8 @@ int gdsm_gen_events(gdsm_ctx* ctx, uint64_t* events, const uint64_t* offsets, ui
   if (!ctx || (n && (!events || !offsets)) || n_nodes == 0 || n_nodes > GDSM_MAX_NODES ||
       write_pct > 100)
     return -EINVAL;
-  DeviceGuard g(ctx->device);
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
   GDSM_TRY(gdsm::launch_gen_events(events, offsets, first_page, n, seed, n_nodes, write_pct,
                                    ctx->stream));
   return 0;

@@ -9,6 +9,7 @@ namespace gdsm {
 
 // Diff geometry: one 256-thread workgroup (4 waves) diffs kDiffPagesPerBlock pages.
 constexpr uint32_t kDiffPagesPerBlock = 64;
+constexpr uint32_t kDiffPagesPerWave = kDiffPagesPerBlock / 4;
 // Largest chunk of pages one diff pass handles with its workspace (the API loops over chunks).
 constexpr uint64_t kDiffChunk = 1ull << 20;
 

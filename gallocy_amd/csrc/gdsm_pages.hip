@@ -138,6 +138,7 @@ __device__ __forceinline__ void load_page(const uint8_t* __restrict__ twin,
 // order = (k, lane)); writes its record to `out` and returns the record size (wave-uniform).
 constexpr uint32_t kDiffStage = 2048;  // per-wave LDS record stage (bytes)
 
+template <bool kWrite>
 __device__ __forceinline__ uint32_t diff_one(const uint4 (&t)[4], const uint4 (&c)[4],
                                              uint32_t lane, uint8_t* __restrict__ out,
                                              uint32_t* __restrict__ stage) {
@@ -171,6 +172,12 @@ __device__ __forceinline__ uint32_t diff_one(const uint4 (&t)[4], const uint4 (&
   const uint32_t NR = carry & 0xFFFFu, NP = carry >> 16;
   if (NR == 0) return 0;
   const uint32_t size = 4u + 4u * NR + ((NP + 3u) & ~3u);
+  if (!kWrite) {  // measurement variant: keep the emit work's inputs alive, store nothing
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h ^= s[k] ^ e[k] ^ ps[k] ^ excl[k] ^ c[k].x;
+    return size + ((wave_sum(h) == 0x9E3779B9u) ? 4u : 0u);
+  }
   // Assemble the record in the wave's LDS stage when it fits, then write it with 16-B stores
   // (a handful of VMEM instructions instead of one per header and per payload byte).
   const bool staged = stage != nullptr && size <= kDiffStage;
@@ -195,32 +202,56 @@ __device__ __forceinline__ uint32_t diff_one(const uint4 (&t)[4], const uint4 (&
   return size;
 }
 
-// One workgroup = 4 waves = kDiffPagesPerBlock consecutive pages (wave w takes w, w+4, ...).
-// kPrefetch: the next page's 8 loads are issued before the current page is processed.
-template <bool kPrefetch, bool kStage>
-__global__ __launch_bounds__(256) void diff_pages_kernel(
+// One workgroup = 4 waves = kDiffPagesPerBlock consecutive pages; wave w takes the 16 pages
+// [16w, 16w + 16) of the block in order and appends their records, each rounded up to 16 B, to
+// its own region of the workspace (16 slots = the worst case): every wave writes one contiguous,
+// 16-B aligned stream, so partially written cache lines merge in L2 instead of going to HBM as
+// one partial line per record, and the pack kernel reads near-contiguous memory.
+// kVar (gdsm_tune "diff_variant"; in-process A/B, scripts/ab_diff.py):
+//   0  records assembled in the wave's LDS stage, written with 16-B stores (default)
+//   1  records written straight from the lanes (per-header / per-byte stores)
+//   2  as 0, and the next page's 8 loads issued before the current page is processed
+//   3  MEASUREMENT ONLY: full diff, records not written (sizes only) -- output is invalid
+//   4  MEASUREMENT ONLY: loads + a change count per page -- the read roofline of this kernel
+//   5  as 0, register budget capped at 64 VGPRs (8 waves/SIMD)
+template <int kVar>
+__device__ __forceinline__ void diff_pages_body(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
+  constexpr bool kPrefetch = kVar == 2;
+  constexpr bool kStage = kVar == 0 || kVar == 2 || kVar == 5;
   __shared__ uint32_t wsum[4];
-  __shared__ __attribute__((aligned(16))) uint32_t stage_all[kStage ? 4 : 1][kDiffStage / 4];
+  __shared__ __attribute__((aligned(16))) uint32_t stage_all[kStage ? 4 : 1][kStage ? kDiffStage / 4 : 1];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* stage = kStage ? stage_all[kStage ? wave : 0] : nullptr;
-  const uint64_t b0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock;
-  uint32_t acc = 0;
+  const uint64_t w0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock + wave * kDiffPagesPerWave;
+  uint8_t* region = ws + w0 * kRecSlot;
+  uint32_t acc = 0, acc16 = 0;
   uint4 t[4], c[4];
-  if (kPrefetch && b0 + wave < n)
-    load_page(twin, cur, ids ? ids[first + b0 + wave] : first + b0 + wave, lane, t, c);
-  for (uint32_t j = wave; j < kDiffPagesPerBlock; j += 4) {
-    const uint64_t i = b0 + j;  // index within chunk
+  if (kPrefetch && w0 < n) load_page(twin, cur, ids ? ids[first + w0] : first + w0, lane, t, c);
+  for (uint32_t j = 0; j < kDiffPagesPerWave; ++j) {
+    const uint64_t i = w0 + j;  // index within chunk
     if (i >= n) break;
     if (!kPrefetch) load_page(twin, cur, ids ? ids[first + i] : first + i, lane, t, c);
     uint4 tn[4], cn[4];
-    const bool nx = kPrefetch && j + 4 < kDiffPagesPerBlock && i + 4 < n;
-    if (nx) load_page(twin, cur, ids ? ids[first + i + 4] : first + i + 4, lane, tn, cn);
-    const uint32_t size = diff_one(t, c, lane, ws + i * kRecSlot, stage);
+    const bool nx = kPrefetch && j + 1 < kDiffPagesPerWave && i + 1 < n;
+    if (nx) load_page(twin, cur, ids ? ids[first + i + 1] : first + i + 1, lane, tn, cn);
+    uint32_t size;
+    if constexpr (kVar == 4) {
+      uint32_t d = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        d |= (t[k].x ^ c[k].x) | (t[k].y ^ c[k].y) | (t[k].z ^ c[k].z) | (t[k].w ^ c[k].w);
+      size = wave_sum(d ? 1u : 0u);
+    } else if constexpr (kVar == 3) {
+      size = diff_one<false>(t, c, lane, nullptr, nullptr);
+    } else {
+      size = diff_one<true>(t, c, lane, region + acc16, stage);
+    }
     if (lane == 0) sizes[i] = size;
     acc += size;
+    acc16 += (size + 15u) & ~15u;
     if (kPrefetch) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -232,6 +263,21 @@ __global__ __launch_bounds__(256) void diff_pages_kernel(
   if (lane == 0) wsum[wave] = acc;
   __syncthreads();
   if (threadIdx.x == 0) block_sum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+template <int kVar>
+__global__ __launch_bounds__(256) void diff_pages_kernel(
+    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
+  diff_pages_body<kVar>(twin, cur, ids, first, n, ws, sizes, block_sum);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void
+diff_pages_kernel_o8(const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+                     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n,
+                     uint8_t* __restrict__ ws, uint32_t* __restrict__ sizes,
+                     uint32_t* __restrict__ block_sum) {
+  diff_pages_body<5>(twin, cur, ids, first, n, ws, sizes, block_sum);
 }
 
 // One workgroup: block_off[b] = base + sum(block_sum[0..b)), base = rec_off[first].
@@ -262,7 +308,8 @@ __global__ __launch_bounds__(1024) void scan_blocks_kernel(const uint32_t* __res
 
 // Per workgroup (64 pages): page offsets inside the block -> rec_off; then every thread copies
 // output dwords of the block's packed range, finding each dword's record by binary search over
-// the 65 block-relative offsets in LDS (all loads independent, stores contiguous).
+// the 65 block-relative offsets in LDS (all loads independent, stores contiguous). A record's
+// source is its wave region (diff_pages_body) at the 16-B rounded prefix `src` of its row.
 __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ ws,
                                                    const uint32_t* __restrict__ sizes,
                                                    const uint64_t* __restrict__ block_off,
@@ -270,13 +317,17 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ w
                                                    uint64_t* __restrict__ rec_off,
                                                    uint8_t* __restrict__ data, uint64_t cap) {
   __shared__ uint32_t off[kDiffPagesPerBlock + 1];
+  __shared__ uint32_t src[kDiffPagesPerBlock];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t b0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock;
   const uint64_t base = block_off[blockIdx.x];
   if (wave == 0) {
+    static_assert(kDiffPagesPerWave == 16, "one DPP row per wave region");
     const uint64_t i = b0 + lane;
     const uint32_t sz = (i < n) ? sizes[i] : 0u;
     const uint32_t inc = wave_incl_sum(sz);
+    const uint32_t s16 = (sz + 15u) & ~15u;
+    src[lane] = row_incl_sum(s16) - s16;
     off[lane] = inc - sz;
     if (lane == 63) off[64] = inc;
     if (i < n) rec_off[first + i + 1] = base + inc;
@@ -297,9 +348,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ w
 #pragma unroll
     for (uint32_t step = 32; step; step >>= 1)
       if (off[r + step] <= byte) r += step;
-    const uint32_t* src =
-        reinterpret_cast<const uint32_t*>(ws + (b0 + r) * kRecSlot + (byte - off[r]));
-    dst[g] = *src;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(
+        ws + (b0 + (r & ~(kDiffPagesPerWave - 1))) * kRecSlot + src[r] + (byte - off[r]));
+    dst[g] = *p;
   }
 }
 
@@ -479,27 +530,20 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
 }
 
 // ------------------------------------------------------------------------- launchers
-// Diff kernel variant: without (default; 64 VGPRs, 8 waves/SIMD: 1.56 ms for config 2 on
-// MI355X) or with a next-page prefetch (105 VGPRs, 4 waves/SIMD: 1.62 ms). Set through gdsm_tune
-// ("diff_prefetch") or GDSM_DIFF_PREFETCH=0/1; used for in-process A/B measurements.
-static int g_diff_prefetch = -1;
-static bool diff_prefetch() {
-  if (g_diff_prefetch < 0) {
-    const char* e = getenv("GDSM_DIFF_PREFETCH");
-    g_diff_prefetch = (e && e[0] == '1') ? 1 : 0;
+// Diff kernel variant (see diff_pages_kernel); gdsm_tune("diff_variant", v) or
+// GDSM_DIFF_VARIANT=v; used for in-process A/B measurements.
+static int g_diff_variant = -1;
+static int diff_variant() {
+  if (g_diff_variant < 0) {
+    const char* e = getenv("GDSM_DIFF_VARIANT");
+    g_diff_variant = e ? atoi(e) : 0;
+    if (g_diff_variant < 0 || g_diff_variant > 5) g_diff_variant = 0;
   }
-  return g_diff_prefetch == 1;
+  return g_diff_variant;
 }
-// Record assembly in LDS + 16-B stores (default) or direct per-lane global stores.
-static int g_diff_stage = 1;
-static bool diff_stage() { return g_diff_stage == 1; }
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "diff_prefetch")) {
-    g_diff_prefetch = value ? 1 : 0;
-    return 0;
-  }
-  if (!strcmp(key, "diff_stage")) {
-    g_diff_stage = value ? 1 : 0;
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 5) {
+    g_diff_variant = (int)value;
     return 0;
   }
   return -1;
@@ -555,10 +599,11 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
     const uint64_t nb = (m + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
     {
       ProfScope ps(prof, 0, s);
-      auto kern = diff_prefetch() ? (diff_stage() ? diff_pages_kernel<true, true>
-                                                  : diff_pages_kernel<true, false>)
-                                  : (diff_stage() ? diff_pages_kernel<false, true>
-                                                  : diff_pages_kernel<false, false>);
+      static void (*const kVariants[])(const uint8_t*, const uint8_t*, const uint32_t*, uint64_t,
+                                       uint64_t, uint8_t*, uint32_t*, uint32_t*) = {
+          diff_pages_kernel<0>, diff_pages_kernel<1>, diff_pages_kernel<2>,
+          diff_pages_kernel<3>, diff_pages_kernel<4>, diff_pages_kernel_o8};
+      auto kern = kVariants[diff_variant()];
       hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids, first, m,
                          slots, sizes, block_sum);
     }

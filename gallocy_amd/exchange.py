@@ -71,35 +71,81 @@ def exchange_stream(rec_off: torch.Tensor, data: torch.Tensor, bounds: list[int]
 
 
 class Shard:
-    """Drives one rank's step: diff (already enqueued) -> exchange -> apply to REPLICA."""
+    """One rank's release pipeline: diff -> exchange -> apply to REPLICA.
+
+    The diff runs on the context's stream, the exchange (RCCL) and the apply of the received
+    records on a second stream, with the diff stream double-buffered: diff k+1 is enqueued
+    before exchange k, so the all-to-all and the home-side apply of step k overlap the diff of
+    step k+1 (the only host synchronisation, the byte counts of exchange k, then waits for
+    diff k alone). Buffer b is reused by diff k+2 only after exchange k has read it."""
 
     def __init__(self, ctx, runs, rank: int, world: int, n: int):
         from . import gdsm
         if n % world:
             raise ValueError("pages per rank must be a multiple of the rank count")
+        runs = list(runs) if isinstance(runs, (list, tuple)) else [runs]
         self.ctx, self.runs, self.rank, self.world, self.n = ctx, runs, rank, world, n
         self.lib = gdsm.lib()
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
+        self.stream = torch.cuda.ExternalStream(ctx.stream, device=dev)   # diff
+        self.comm = torch.cuda.Stream(device=dev)                          # exchange + apply
         self.bounds = dest_bounds(rank, world, n)
-        # Tensors aliasing the diff stream that libgdsm writes (device memory owned by ctx).
-        self.rec_off = _tensor_at(runs.s.rec_off, (n + 1,), torch.int64, dev)
-        self.data = _tensor_at(runs.s.data, (runs.cap,), torch.uint8, dev)
-        with torch.cuda.stream(self.stream):
+        # Tensors aliasing the diff streams that libgdsm writes (device memory owned by ctx).
+        self.views = [(_tensor_at(r.s.rec_off, (n + 1,), torch.int64, dev),
+                       _tensor_at(r.s.data, (r.cap,), torch.uint8, dev)) for r in runs]
+        self.ready = [torch.cuda.Event() for _ in runs]      # diff into buffer b done
+        self.consumed = [None for _ in runs]                  # exchange of buffer b done
+        with torch.cuda.stream(self.comm):
             self.recv_ids = torch.from_numpy(recv_ids(world, n)).to(dev)
+            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.sent_remote = 0
         self.received = 0
 
-    def exchange_and_apply(self):
-        with torch.cuda.stream(self.stream):
-            off, data, sent_remote, received = exchange_stream(self.rec_off, self.data, self.bounds,
-                                                              self.world)
+    def _diff(self, k: int):
+        b = k % len(self.runs)
+        if self.consumed[b] is not None:
+            self.stream.wait_event(self.consumed[b])
+        self.ctx.diff(out=self.runs[b])
+        self.ready[b].record(self.stream)
+
+    def _exchange_apply(self, k: int):
+        b = k % len(self.runs)
+        rec_off, data = self.views[b]
+        self.comm.wait_event(self.ready[b])
+        with torch.cuda.stream(self.comm):
+            off, rdata, sent_remote, received = exchange_stream(rec_off, data, self.bounds,
+                                                               self.world)
+            ev = torch.cuda.Event()
+            ev.record(self.comm)
+            self.consumed[b] = ev
             rc = self.lib.gdsm_apply_raw(self.ctx.arena_ptr("replica"), self.recv_ids.data_ptr(),
-                                         self.n, off.data_ptr(), data.data_ptr(), self.ctx.stream)
+                                         self.n, off.data_ptr(), rdata.data_ptr(),
+                                         self.err.data_ptr(), self.comm.cuda_stream)
             if rc:
                 raise RuntimeError(f"gdsm_apply_raw: {rc}")
-            self._keep = (off, data)  # alive until the stream has consumed them
         self.sent_remote, self.received = sent_remote, received
+
+    def run(self, steps: int):
+        """`steps` releases, pipelined as described above; returns with work still in flight."""
+        if steps <= 0:
+            return
+        self._diff(0)
+        for k in range(steps):
+            if k + 1 < steps:
+                self._diff(k + 1)
+            self._exchange_apply(k)
+
+    def exchange_and_apply(self):
+        """One unpipelined step (the diff already enqueued on the context stream)."""
+        self.ready[0].record(self.stream)
+        self._exchange_apply(0)
+
+    def drain(self):
+        """Waits for both streams; raises if an apply found a malformed record."""
+        self.comm.synchronize()
+        self.stream.synchronize()
+        if int(self.err.item()) != 0:
+            raise RuntimeError("apply: malformed record in the received stream")
 
     def verify(self) -> bool:
         """REPLICA (home block) == CURRENT content of those pages, generated independently."""

@@ -251,6 +251,11 @@ class Context:
     def apply(self, runs: Runs, target="replica", ids=None):
         check(lib().gdsm_apply(self.handle, _ARENA[target], self._ptr(ids), C.byref(runs.s)), "gdsm_apply")
 
+    def apply_async(self, runs: Runs, target="replica", ids=None):
+        """gdsm_apply_async: the apply overlaps the diffs enqueued after it (double buffering)."""
+        check(lib().gdsm_apply_async(self.handle, _ARENA[target], self._ptr(ids), C.byref(runs.s)),
+              "gdsm_apply_async")
+
     def _count(self, ids, n):
         if n is not None:
             return int(n)

@@ -134,14 +134,20 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out);
 int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total);
 /* Applies `in` to arena `target` (normally GDSM_REPLICA) for the listed pages (ids unique). */
 int gdsm_apply(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_runs* in);
+/* As gdsm_apply, on the context's second stream: it runs concurrently with the gdsm_diff calls
+ * that follow (double-buffered releases: diff k+1 overlaps apply k). A later gdsm_diff into the
+ * same `in` waits for this apply; every other call on the context is ordered after it.
+ * Malformed records are reported by the next gdsm_sync. */
+int gdsm_apply_async(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_runs* in);
 
 /* ---- raw entry points (caller-owned device memory, e.g. tensors; stream = hipStream_t) ---- */
 uint64_t gdsm_diff_workspace_bytes(uint64_t n);
 int gdsm_diff_raw(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                   uint64_t* rec_off, uint8_t* data, uint64_t cap, void* workspace,
                   uint64_t workspace_bytes, void* stream);
+/* err: caller-owned device word, OR-ed with 1 on a malformed record (NULL: not reported). */
 int gdsm_apply_raw(uint8_t* target, const uint32_t* ids, uint64_t n, const uint64_t* rec_off,
-                   const uint8_t* data, void* stream);
+                   const uint8_t* data, uint32_t* err, void* stream);
 int gdsm_twin_raw(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                   void* stream);
 
@@ -172,7 +178,7 @@ int gdsm_nw_diff(const char* mem1, size_t mem1_len, char** out1, const char* mem
 int gdsm_set_allocator(void* (*alloc_fn)(size_t), void (*free_fn)(void*));
 
 const char* gdsm_version(void);
-/* Process-wide kernel-variant knobs for measurement, e.g. ("diff_prefetch", 0|1). */
+/* Process-wide kernel-variant knobs for measurement, e.g. ("diff_variant", 0..4). */
 int gdsm_tune(const char* key, int64_t value);
 
 #ifdef __cplusplus

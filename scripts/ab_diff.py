@@ -1,5 +1,9 @@
 """In-process A/B of diff kernel variants (interleaved rounds, one device): per-launch time of
-diff_pages_kernel from HIP events, for BASELINE config 2 (1M pages, 1 % word writes)."""
+diff_pages_kernel from HIP events, for BASELINE config 2 (1M pages, 1 % word writes).
+
+    python scripts/ab_diff.py diff_variant 0,1,2,3,4
+
+Variants >= 3 are measurement-only kernels (no valid output); their totals are not checked."""
 import statistics
 import sys
 from pathlib import Path
@@ -8,7 +12,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 
-KEY = sys.argv[1] if len(sys.argv) > 1 else "diff_prefetch"
+KEY = sys.argv[1] if len(sys.argv) > 1 else "diff_variant"
 VALUES = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1"])]
 ROUNDS, REPS = 6, 10
 n = 1 << 20
@@ -28,10 +32,13 @@ for r in range(ROUNDS):
         p = ctx.prof_read()
         ctx.prof_enable(False)
         res[v].append(p["diff"][0] / p["diff"][1])
-        t = runs.total()
-        assert total is None or t == total
-        total = t
+        if KEY != "diff_variant" or v < 3:
+            t = runs.total()
+            assert total is None or t == total, (v, t, total)
+            total = t
+gdsm.lib().gdsm_tune(KEY.encode(), 0)
 for v in VALUES:
     ms = res[v]
-    gbs = (n * 8192 + total) / (statistics.median(ms) * 1e-3) / 1e9
-    print(f"{KEY}={v}: median {statistics.median(ms):.4f} ms  min {min(ms):.4f} ms  -> {gbs:.0f} GB/s")
+    gbs = (n * 8192 + (total or 0)) / (statistics.median(ms) * 1e-3) / 1e9
+    print(f"{KEY}={v}: median {statistics.median(ms):.4f} ms  min {min(ms):.4f} ms  -> {gbs:.0f} GB/s",
+          flush=True)

@@ -47,3 +47,28 @@ def test_shard_step_single_rank_rccl():
             assert shard.verify()
     finally:
         dist.destroy_process_group()
+
+
+def test_shard_pipelined_run_single_rank_rccl():
+    """Shard.run: diff k+1 on the context stream overlaps exchange + apply k on the comm
+    stream, two run buffers alternating; the replica must still end equal to CURRENT."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = 1 << 14
+        with ga.Context(n) as ctx:
+            ctx.gen_pages(seed=6, mode=ga.GEN_UNIFORM, ppm=10000, first_global=0, stride=1,
+                          arenas=("twin", "current"))
+            ctx.gen_pages(seed=6, mode=ga.GEN_UNIFORM, ppm=10000, first_global=0, stride=1,
+                          arenas=("replica",))
+            runs = [ga.Runs(ctx, n, cap=n * 256) for _ in range(2)]
+            shard = exchange.Shard(ctx, runs, 0, 1, n)
+            shard.gen_args = (6, ga.GEN_UNIFORM, 10000)
+            shard.run(5)
+            shard.drain()
+            ctx.sync()
+            assert shard.received == runs[0].total() == runs[1].total() > 0
+            assert shard.verify()
+    finally:
+        dist.destroy_process_group()

@@ -302,3 +302,51 @@ def test_apply_many_runs_and_long_runs():
         c.apply(Runs.from_host(c, HostRuns(ro, data)))
         c.sync()
         assert np.array_equal(c.download("replica"), cur)
+
+
+def test_apply_async_double_buffered_releases():
+    """gdsm_apply_async: diff k+1 overlaps apply k, two run buffers alternate. Step k releases
+    a distinct page subset; if diff k+2 overwrote buffer k%2 before apply k had read it, apply k
+    would write another subset's records onto these pages and the replica would differ."""
+    n, steps = 4096, 8
+    t, cur = oracle.gen_pages(n, seed=21, mode=1, ppm=200000)
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(n).astype(np.uint32)
+    subsets = np.array_split(perm, steps)
+    with ga.Context(n) as c:
+        c.upload("twin", t)
+        c.upload("current", cur)
+        c.upload("replica", t)
+        d_ids = [c.ids(s) for s in subsets]
+        runs = [Runs(c, n, cap=n * 2048) for _ in range(2)]
+        for k in range(steps):
+            r = runs[k % 2]
+            c.diff(d_ids[k], n=len(subsets[k]), out=r)
+            c.apply_async(r, "replica", d_ids[k])
+        c.sync()
+        assert np.array_equal(c.download("replica"), cur)
+        # a later synchronous call is ordered after the async applies (joins the second stream)
+        c.upload("replica", t)
+        for k in range(steps):
+            c.diff(d_ids[k], n=len(subsets[k]), out=runs[k % 2])
+            c.apply_async(runs[k % 2], "replica", d_ids[k])
+        c.twin()  # TWIN <- CURRENT, must run after every apply
+        c.sync()
+        assert np.array_equal(c.download("replica"), cur)
+        assert np.array_equal(c.download("twin"), cur)
+
+
+def test_apply_async_reports_malformed_stream():
+    n = 8
+    t, cur = oracle.gen_pages(n, seed=2, mode=0, ppm=50000)
+    ro, data = oracle.diff_pages(t, cur)
+    bad = data.copy()
+    i = int(np.flatnonzero(np.diff(ro))[0])
+    bad[int(ro[i]) + 4:int(ro[i]) + 8] = np.frombuffer(np.uint32(4090 | (100 << 16)).tobytes(),
+                                                      np.uint8)  # run past the page end
+    with ga.Context(n) as c:
+        c.upload("replica", t)
+        c.apply_async(Runs.from_host(c, HostRuns(ro, bad)))
+        with pytest.raises(GdsmError) as ei:
+            c.sync()
+        assert ei.value.errno == 22
