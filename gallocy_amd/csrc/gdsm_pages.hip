@@ -138,105 +138,218 @@ __device__ __forceinline__ void load_page(const uint8_t* __restrict__ twin,
 // order = (k, lane)); writes its record to `out` and returns the record size (wave-uniform).
 constexpr uint32_t kDiffStage = 2048;  // per-wave LDS record stage (bytes)
 
-template <bool kWrite>
-__device__ __forceinline__ uint32_t diff_one(const uint4 (&t)[4], const uint4 (&c)[4],
-                                             uint32_t lane, uint8_t* __restrict__ out,
-                                             uint32_t* __restrict__ stage) {
-  uint32_t m[4], s[4], e[4];
+// v_perm_b32 selectors compacting the bytes of a dword whose bit is set in a 4-bit mask to its
+// low bytes, in order; selector 0x0C yields a zero byte.
+__device__ __forceinline__ uint32_t compact_sel(uint32_t nib) {
+  uint32_t sel = 0x0C0C0C0Cu, sh = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) m[k] = diffmask16(t[k], c[k]);
+  for (uint32_t j = 0; j < 4; ++j)
+    if ((nib >> j) & 1u) {
+      sel = (sel & ~(0xFFu << sh)) | (j << sh);
+      sh += 8;
+    }
+  return sel;
+}
+
+// ORs the bytes of v (little-endian) into the 3-word window w at byte offset o (o + 8 <= 24).
+__device__ __forceinline__ void or_at(uint64_t v, uint32_t o, uint64_t& w0, uint64_t& w1,
+                                      uint64_t& w2) {
+  const uint32_t ob = (o & 7u) * 8u;
+  const uint64_t lo = v << ob;
+  const uint64_t hi = ob ? v >> (64u - ob) : 0ull;
+  const bool up = o >= 8u;
+  w0 |= up ? 0ull : lo;
+  w1 |= up ? lo : hi;
+  w2 |= up ? hi : 0ull;
+}
+
+// Emits the headers of the runs ending in one 16-B chunk and the chunk's changed bytes into the
+// wave's LDS record image (payload region pre-zeroed): the changed bytes are compacted in
+// registers (v_perm_b32 per dword), shifted to their byte position and OR-ed into <= 5 dwords,
+// so the cost does not grow with the number of changed bytes.
+__device__ __forceinline__ void emit_compact(uint32_t ch, uint32_t s, uint32_t e, uint32_t m,
+                                             uint32_t ps, uint32_t excl, const uint4 c,
+                                             uint32_t* __restrict__ img, uint32_t pay_base,
+                                             const uint32_t* __restrict__ sel_tab) {
+  const uint32_t pos = ch * 16u;
+  uint32_t r = excl & 0xFFFFu;
+  while (e) {
+    const uint32_t b = (uint32_t)__builtin_ctz(e);
+    e &= e - 1;
+    const uint32_t upto = s & ((2u << b) - 1u);
+    const uint32_t start = upto ? pos + 31u - (uint32_t)__builtin_clz(upto) : ps - 1u;
+    img[1 + r++] = start | ((pos + b - start + 1u) << 16);
+  }
+  const uint32_t n0 = m & 0xFu, n1 = (m >> 4) & 0xFu, n2 = (m >> 8) & 0xFu, n3 = m >> 12;
+  const uint32_t p0 = __builtin_amdgcn_perm(0u, c.x, sel_tab[n0]);
+  const uint32_t p1 = __builtin_amdgcn_perm(0u, c.y, sel_tab[n1]);
+  const uint32_t p2 = __builtin_amdgcn_perm(0u, c.z, sel_tab[n2]);
+  const uint32_t p3 = __builtin_amdgcn_perm(0u, c.w, sel_tab[n3]);
+  const uint32_t l0 = (uint32_t)__popc(n0), l1 = (uint32_t)__popc(n1);
+  const uint32_t l2 = (uint32_t)__popc(n2), l3 = (uint32_t)__popc(n3);
+  const uint64_t A = (uint64_t)p0 | ((uint64_t)p1 << (8u * l0));
+  const uint64_t B = (uint64_t)p2 | ((uint64_t)p3 << (8u * l2));
+  const uint32_t P = pay_base + (excl >> 16);  // byte address of the first payload byte
+  const uint32_t sh = P & 3u, len = l0 + l1 + l2 + l3;
+  uint64_t w0 = 0, w1 = 0, w2 = 0;
+  or_at(A, sh, w0, w1, w2);
+  or_at(B, sh + l0 + l1, w0, w1, w2);
+  const uint32_t nw = (sh + len + 3u) >> 2;  // dwords touched (<= 5)
+  uint32_t* d = img + (P >> 2);
+  if (nw > 0) atomicOr(d + 0, (uint32_t)w0);
+  if (nw > 1) atomicOr(d + 1, (uint32_t)(w0 >> 32));
+  if (nw > 2) atomicOr(d + 2, (uint32_t)w1);
+  if (nw > 3) atomicOr(d + 3, (uint32_t)(w1 >> 32));
+  if (nw > 4) atomicOr(d + 4, (uint32_t)w2);
+}
+
+// a[k] for k = 2*b1 + b0 as two levels of selects on the bits of k (a select chain on k == i
+// gets rewritten into an indexed private array, i.e. scratch memory).
+__device__ __forceinline__ uint32_t sel4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                         bool b0, bool b1) {
+  const uint32_t lo = b0 ? a1 : a0, hi = b0 ? a3 : a2;
+  return b1 ? hi : lo;
+}
+
+// Run structure of one page held in registers (chunk (k, lane) = bytes [(64k + lane) * 16, +16),
+// page order = (k, lane)): per chunk the byte-diff mask m, run-start bits s, run-end bits e, the
+// exclusive ranks excl (runs ending before the chunk in the low 16 bits, changed bytes before it
+// in the high 16) and ps (1 + the last run start before the chunk); NR / NP = the page's runs /
+// payload bytes (wave-uniform).
+struct PageRuns {
+  uint32_t m[4], s[4], e[4], excl[4], ps[4];
+  uint32_t NR, NP;
+};
+
+__device__ __forceinline__ void scan_page(const uint4 (&t)[4], const uint4 (&c)[4], uint32_t lane,
+                                          PageRuns& P) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) P.m[k] = diffmask16(t[k], c[k]);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     // neighbour chunks' edge bytes: lane-1 / lane+1 of the same k, wrapping across k
-    uint32_t up = from_prev_lane(m[k]);
-    uint32_t dn = from_next_lane(m[k]);
-    if (k > 0 && lane == 0) up = lane_bcast(m[k > 0 ? k - 1 : 0], 63);
-    if (k < 3 && lane == 63) dn = lane_bcast(m[k < 3 ? k + 1 : 3], 0);
-    s[k] = m[k] & ~((m[k] << 1) | ((up >> 15) & 1u)) & 0xFFFFu;   // first byte of a run
-    e[k] = m[k] & ~((m[k] >> 1) | ((dn & 1u) << 15)) & 0xFFFFu;   // last byte of a run
+    uint32_t up = from_prev_lane(P.m[k]);
+    uint32_t dn = from_next_lane(P.m[k]);
+    if (k > 0 && lane == 0) up = lane_bcast(P.m[k > 0 ? k - 1 : 0], 63);
+    if (k < 3 && lane == 63) dn = lane_bcast(P.m[k < 3 ? k + 1 : 3], 0);
+    P.s[k] = P.m[k] & ~((P.m[k] << 1) | ((up >> 15) & 1u)) & 0xFFFFu;   // first byte of a run
+    P.e[k] = P.m[k] & ~((P.m[k] >> 1) | ((dn & 1u) << 15)) & 0xFFFFu;   // last byte of a run
   }
   // Ranks: runs (counted at their ends) in the low 16 bits, payload bytes in the high 16.
-  uint32_t excl[4], ps[4], carry = 0, cmax = 0;
+  uint32_t carry = 0, cmax = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint32_t v = (uint32_t)__popc(e[k]) | ((uint32_t)__popc(m[k]) << 16);
+    const uint32_t v = (uint32_t)__popc(P.e[k]) | ((uint32_t)__popc(P.m[k]) << 16);
     const uint32_t inc = wave_incl_sum(v);
-    excl[k] = carry + inc - v;
+    P.excl[k] = carry + inc - v;
     carry += lane_bcast(inc, 63);
     const uint32_t pos = (uint32_t)(k * 64 + lane) * 16u;
-    const uint32_t ls = s[k] ? pos + 32u - (uint32_t)__builtin_clz(s[k]) : 0u;  // last start + 1
+    const uint32_t ls = P.s[k] ? pos + 32u - (uint32_t)__builtin_clz(P.s[k]) : 0u;  // last start + 1
     const uint32_t mx = wave_incl_max(ls);
-    ps[k] = max(cmax, from_prev_lane(mx));
+    P.ps[k] = max(cmax, from_prev_lane(mx));
     cmax = max(cmax, lane_bcast(mx, 63));
   }
-  const uint32_t NR = carry & 0xFFFFu, NP = carry >> 16;
-  if (NR == 0) return 0;
-  const uint32_t size = 4u + 4u * NR + ((NP + 3u) & ~3u);
-  if (!kWrite) {  // measurement variant: keep the emit work's inputs alive, store nothing
-    uint32_t h = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) h ^= s[k] ^ e[k] ^ ps[k] ^ excl[k] ^ c[k].x;
-    return size + ((wave_sum(h) == 0x9E3779B9u) ? 4u : 0u);
-  }
-  // Assemble the record in the wave's LDS stage when it fits, then write it with 16-B stores
-  // (a handful of VMEM instructions instead of one per header and per payload byte).
-  const bool staged = stage != nullptr && size <= kDiffStage;
-  uint8_t* rec = staged ? reinterpret_cast<uint8_t*>(stage) : out;
+  P.NR = carry & 0xFFFFu;
+  P.NP = carry >> 16;
+}
+
+__device__ __forceinline__ uint32_t record_size(const PageRuns& P) {
+  return P.NR ? 4u + 4u * P.NR + ((P.NP + 3u) & ~3u) : 0u;
+}
+
+// Byte-loop emission of a whole record (headers and payload bytes one store each) to `rec`
+// (LDS or global); lane 0 writes the run count and the zero padding.
+__device__ __forceinline__ void emit_bytes(const PageRuns& P, const uint4 (&c)[4], uint32_t lane,
+                                           uint8_t* __restrict__ rec) {
   uint32_t* hdr = reinterpret_cast<uint32_t*>(rec + 4);
-  uint8_t* pay = rec + 4 + 4 * NR;
+  uint8_t* pay = rec + 4 + 4 * P.NR;
   if (lane == 0) {
-    *reinterpret_cast<uint32_t*>(rec) = NR;
-    for (uint32_t q = NP; q & 3u; ++q) pay[q] = 0;  // zero padding
+    *reinterpret_cast<uint32_t*>(rec) = P.NR;
+    for (uint32_t q = P.NP; q & 3u; ++q) pay[q] = 0;
   }
-  emit_chunk(0 * 64 + lane, s[0], e[0], m[0], ps[0], excl[0], c[0], hdr, pay);
-  emit_chunk(1 * 64 + lane, s[1], e[1], m[1], ps[1], excl[1], c[1], hdr, pay);
-  emit_chunk(2 * 64 + lane, s[2], e[2], m[2], ps[2], excl[2], c[2], hdr, pay);
-  emit_chunk(3 * 64 + lane, s[3], e[3], m[3], ps[3], excl[3], c[3], hdr, pay);
-  if (staged) {
-    wave_lds_sync();
-    const uint4* src = reinterpret_cast<const uint4*>(stage);
-    uint4* dst = reinterpret_cast<uint4*>(out);
-    for (uint32_t q = lane; q < (size + 15u) / 16u; q += 64) dst[q] = src[q];
-    wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    emit_chunk(k * 64 + lane, P.s[k], P.e[k], P.m[k], P.ps[k], P.excl[k], c[k], hdr, pay);
+}
+
+// Compacted emission of a whole record into an LDS image of n16 16-B words: zero it, write the
+// run count, then every lane emits its dirty chunks (one loop trip per dirty chunk of the lane,
+// all four k at once). The caller orders the image before any read (wave_lds_sync).
+__device__ __forceinline__ void emit_image(const PageRuns& P, const uint4 (&c)[4], uint32_t lane,
+                                           uint32_t* __restrict__ img, uint32_t n16,
+                                           const uint32_t* __restrict__ sel_tab) {
+  uint4* z = reinterpret_cast<uint4*>(img);
+  for (uint32_t q = lane; q < n16; q += 64) z[q] = make_uint4(0, 0, 0, 0);
+  wave_lds_sync();
+  if (lane == 0) img[0] = P.NR;
+  const uint32_t pay_base = 4u + 4u * P.NR;
+  uint32_t dm = (P.m[0] ? 1u : 0u) | (P.m[1] ? 2u : 0u) | (P.m[2] ? 4u : 0u) | (P.m[3] ? 8u : 0u);
+  while (dm) {
+    const uint32_t k = (uint32_t)__builtin_ctz(dm);
+    dm &= dm - 1;
+    const bool b0 = k & 1u, b1 = k & 2u;
+#define GDSM_SEL4(a) sel4(a[0], a[1], a[2], a[3], b0, b1)
+    const uint4 cc = make_uint4(sel4(c[0].x, c[1].x, c[2].x, c[3].x, b0, b1),
+                                sel4(c[0].y, c[1].y, c[2].y, c[3].y, b0, b1),
+                                sel4(c[0].z, c[1].z, c[2].z, c[3].z, b0, b1),
+                                sel4(c[0].w, c[1].w, c[2].w, c[3].w, b0, b1));
+    emit_compact(k * 64u + lane, GDSM_SEL4(P.s), GDSM_SEL4(P.e), GDSM_SEL4(P.m),
+                 GDSM_SEL4(P.ps), GDSM_SEL4(P.excl), cc, img, pay_base, sel_tab);
+#undef GDSM_SEL4
   }
-  return size;
+}
+
+// Copies n16 16-B words from LDS to global memory (one wave, coalesced 16-B stores).
+__device__ __forceinline__ void flush_lds(const uint32_t* __restrict__ src, uint32_t n16,
+                                          uint8_t* __restrict__ dst, uint32_t lane) {
+  wave_lds_sync();
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  for (uint32_t q = lane; q < n16; q += 64) d[q] = s[q];
+  wave_lds_sync();
 }
 
 // One workgroup = 4 waves = kDiffPagesPerBlock consecutive pages; wave w takes the 16 pages
 // [16w, 16w + 16) of the block in order and appends their records, each rounded up to 16 B, to
-// its own region of the workspace (16 slots = the worst case): every wave writes one contiguous,
-// 16-B aligned stream, so partially written cache lines merge in L2 instead of going to HBM as
-// one partial line per record, and the pack kernel reads near-contiguous memory.
+// its own region of the workspace (16 slots = the worst case), which the pack kernel then reads
+// as near-contiguous memory.
 // kVar (gdsm_tune "diff_variant"; in-process A/B, scripts/ab_diff.py):
-//   0  records assembled in the wave's LDS stage, written with 16-B stores (default)
-//   1  records written straight from the lanes (per-header / per-byte stores)
-//   2  as 0, and the next page's 8 loads issued before the current page is processed
-//   3  MEASUREMENT ONLY: full diff, records not written (sizes only) -- output is invalid
+//   0  records compacted in registers, OR-ed into a per-wave LDS accumulation buffer of
+//      kDiffAcc bytes and written out only when it fills and after the wave's last page: the
+//      stores are whole, contiguous lines (default)
+//   1  as 0, but every record is written out as soon as it is built (one partial line or two
+//      per page: measured 0.10 ms slower per 1M pages than 0, the price of partial-line writes)
+//   2  byte-loop emission (emit_bytes) into the LDS stage, written out per record
+//   3  MEASUREMENT ONLY: full run scan, records not written (sizes only) -- output is invalid
 //   4  MEASUREMENT ONLY: loads + a change count per page -- the read roofline of this kernel
-//   5  as 0, register budget capped at 64 VGPRs (8 waves/SIMD)
+// Measured and dropped: next-page register prefetch, a 64-VGPR cap, records
+// stored straight from the lanes.
+constexpr uint32_t kDiffAcc = 4096;  // per-wave LDS accumulation buffer (bytes)
+
 template <int kVar>
 __device__ __forceinline__ void diff_pages_body(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
-  constexpr bool kPrefetch = kVar == 2;
-  constexpr bool kStage = kVar == 0 || kVar == 2 || kVar == 5;
+  constexpr uint32_t kBuf = (kVar == 0 || kVar == 5) ? kDiffAcc : kDiffStage;
   __shared__ uint32_t wsum[4];
-  __shared__ __attribute__((aligned(16))) uint32_t stage_all[kStage ? 4 : 1][kStage ? kDiffStage / 4 : 1];
+  __shared__ uint32_t sel_tab[16];
+  __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kBuf / 4];
+  if (threadIdx.x < 16) sel_tab[threadIdx.x] = compact_sel(threadIdx.x);
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* stage = kStage ? stage_all[kStage ? wave : 0] : nullptr;
+  uint32_t* buf = buf_all[wave];
   const uint64_t w0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock + wave * kDiffPagesPerWave;
-  uint8_t* region = ws + w0 * kRecSlot;
-  uint32_t acc = 0, acc16 = 0;
-  uint4 t[4], c[4];
-  if (kPrefetch && w0 < n) load_page(twin, cur, ids ? ids[first + w0] : first + w0, lane, t, c);
-  for (uint32_t j = 0; j < kDiffPagesPerWave; ++j) {
+  uint8_t* region = kVar == 5 ? ws + (w0 / kDiffPagesPerWave) * 4096 : ws + w0 * kRecSlot;
+  uint32_t acc = 0;      // record bytes of the wave's pages so far
+  uint32_t acc16 = 0;    // region bytes of the wave's pages so far (records rounded to 16 B)
+  uint32_t flushed = 0;  // region bytes already stored (variant 0); buffer = [flushed, acc16)
+  uint32_t my_size = 0;  // lane j: size of the wave's page j
+  const uint32_t cnt = (uint32_t)min((uint64_t)kDiffPagesPerWave, n > w0 ? n - w0 : 0);
+  for (uint32_t j = 0; j < cnt; ++j) {
     const uint64_t i = w0 + j;  // index within chunk
-    if (i >= n) break;
-    if (!kPrefetch) load_page(twin, cur, ids ? ids[first + i] : first + i, lane, t, c);
-    uint4 tn[4], cn[4];
-    const bool nx = kPrefetch && j + 1 < kDiffPagesPerWave && i + 1 < n;
-    if (nx) load_page(twin, cur, ids ? ids[first + i + 1] : first + i + 1, lane, tn, cn);
+    uint4 t[4], c[4];
+    load_page(twin, cur, ids ? ids[first + i] : first + i, lane, t, c);
     uint32_t size;
     if constexpr (kVar == 4) {
       uint32_t d = 0;
@@ -244,22 +357,47 @@ __device__ __forceinline__ void diff_pages_body(
       for (int k = 0; k < 4; ++k)
         d |= (t[k].x ^ c[k].x) | (t[k].y ^ c[k].y) | (t[k].z ^ c[k].z) | (t[k].w ^ c[k].w);
       size = wave_sum(d ? 1u : 0u);
-    } else if constexpr (kVar == 3) {
-      size = diff_one<false>(t, c, lane, nullptr, nullptr);
     } else {
-      size = diff_one<true>(t, c, lane, region + acc16, stage);
-    }
-    if (lane == 0) sizes[i] = size;
-    acc += size;
-    acc16 += (size + 15u) & ~15u;
-    if (kPrefetch) {
+      PageRuns P;
+      scan_page(t, c, lane, P);
+      size = record_size(P);
+      const uint32_t n16 = (size + 15u) >> 4;
+      if constexpr (kVar == 3) {  // keep the emission inputs alive, store nothing
+        uint32_t h = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        t[k] = tn[k];
-        c[k] = cn[k];
+        for (int k = 0; k < 4; ++k) h ^= P.s[k] ^ P.e[k] ^ P.ps[k] ^ P.excl[k] ^ c[k].x;
+        size += (wave_sum(h) == 0x9E3779B9u) ? 4u : 0u;
+      } else if (size != 0) {
+        if (16u * n16 > kBuf) {
+          // larger than the buffer: emitted straight to its place, byte by byte
+          if ((kVar == 0 || kVar == 5) && acc16 > flushed) {
+            flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
+            flushed = acc16;
+          }
+          emit_bytes(P, c, lane, region + acc16);
+          if (kVar == 0 || kVar == 5) flushed = acc16 + 16u * n16;
+        } else if constexpr (kVar == 0 || kVar == 5) {
+          if (acc16 - flushed + 16u * n16 > kBuf) {
+            flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
+            flushed = acc16;
+          }
+          emit_image(P, c, lane, buf + (acc16 - flushed) / 4, n16, sel_tab);
+        } else if constexpr (kVar == 1) {
+          emit_image(P, c, lane, buf, n16, sel_tab);
+          flush_lds(buf, n16, region + acc16, lane);
+        } else {
+          emit_bytes(P, c, lane, reinterpret_cast<uint8_t*>(buf));
+          flush_lds(buf, n16, region + acc16, lane);
+        }
       }
     }
+    if (lane == j) my_size = size;
+    acc += size;
+    acc16 += (size + 15u) & ~15u;
   }
+  if ((kVar == 0 || kVar == 5) && acc16 > flushed && (kVar == 0 || acc16 <= 4096))
+    flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
+  if (lane < cnt) sizes[w0 + lane] = my_size;
   if (lane == 0) wsum[wave] = acc;
   __syncthreads();
   if (threadIdx.x == 0) block_sum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
@@ -271,13 +409,6 @@ __global__ __launch_bounds__(256) void diff_pages_kernel(
     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
   diff_pages_body<kVar>(twin, cur, ids, first, n, ws, sizes, block_sum);
-}
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void
-diff_pages_kernel_o8(const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
-                     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n,
-                     uint8_t* __restrict__ ws, uint32_t* __restrict__ sizes,
-                     uint32_t* __restrict__ block_sum) {
-  diff_pages_body<5>(twin, cur, ids, first, n, ws, sizes, block_sum);
 }
 
 // One workgroup: block_off[b] = base + sum(block_sum[0..b)), base = rec_off[first].
@@ -365,7 +496,16 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ w
 constexpr uint32_t kApplyWin = 8192;  // bytes of records staged per wave
 
 // Stores the payload bytes selected by `mask` (16 bits, chunk of 16 B at dst) from pay[pp..].
-template <typename P8>
+// Replica store; kNT = nontemporal (streaming) cache policy.
+template <bool kNT, typename T>
+__device__ __forceinline__ void st(T* p, T v) {
+  if (kNT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+template <bool kNT, typename P8>
 __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint32_t mask, P8 pay,
                                             uint32_t pp) {
   if (mask == 0xFFFFu) {
@@ -374,7 +514,7 @@ __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint32_t 
     for (int d = 0; d < 4; ++d)
       w[d] = (uint32_t)pay[pp + 4 * d] | ((uint32_t)pay[pp + 4 * d + 1] << 8) |
              ((uint32_t)pay[pp + 4 * d + 2] << 16) | ((uint32_t)pay[pp + 4 * d + 3] << 24);
-    *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+    st<kNT>(reinterpret_cast<u32x4*>(dst), (u32x4){w[0], w[1], w[2], w[3]});
     return;
   }
 #pragma unroll
@@ -383,25 +523,25 @@ __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint32_t 
     if (nib == 0xFu) {
       const uint32_t v = (uint32_t)pay[pp] | ((uint32_t)pay[pp + 1] << 8) |
                          ((uint32_t)pay[pp + 2] << 16) | ((uint32_t)pay[pp + 3] << 24);
-      *reinterpret_cast<uint32_t*>(dst + 4 * d) = v;
+      st<kNT>(reinterpret_cast<uint32_t*>(dst + 4 * d), v);
       pp += 4;
     } else if (nib) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if ((nib >> k) & 1u) dst[4 * d + k] = pay[pp++];
+        if ((nib >> k) & 1u) st<kNT>(dst + 4 * d + k, (uint8_t)pay[pp++]);
     }
   }
 }
 
 // Stores the run bytes that fall into one 16-B destination chunk: chunk [cs, cs+16) of `page`,
 // run [off, end), payload of the run starting at pay[pp].
-template <typename P8>
+template <bool kNT, typename P8>
 __device__ __forceinline__ void store_run_chunk(uint8_t* __restrict__ page, uint32_t cs,
                                                 uint32_t off, uint32_t end, P8 pay, uint32_t pp) {
   const uint32_t lo = max(off, cs), hi = min(end, cs + 16u);
   const uint32_t mask = ((hi - cs >= 16u) ? 0xFFFFu : ((1u << (hi - cs)) - 1u)) &
                         ~((1u << (lo - cs)) - 1u);
-  store_chunk(page + cs, mask, pay, pp + (lo - off));
+  store_chunk<kNT>(page + cs, mask, pay, pp + (lo - off));
 }
 
 // Applies up to four records at once, one per 16-lane DPP row (a lane per run). Pass 1 validates
@@ -410,9 +550,10 @@ __device__ __forceinline__ void store_run_chunk(uint8_t* __restrict__ page, uint
 // the row's lanes — a run is found by a 4-step binary search over the row's pair offsets — so
 // short and long runs cost the same per byte. `has` is false for rows without a record.
 // Returns false in the lanes of a row whose record is malformed.
-template <typename P32, typename P8>
+// kMode: 0 = plain stores, 1 = MEASUREMENT ONLY (no replica stores), 2 = nontemporal stores.
+template <int kMode, typename P32, typename P8>
 __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32, P8 rec8,
-                                           uint32_t size, bool has) {
+                                           uint32_t size, bool has, uint32_t& sink) {
   const uint32_t lane = lane_id(), lr = lane & 15, rb = lane & ~15u;
   uint32_t nr = has ? rec32[0] : 0u;
   bool bad = has && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr);
@@ -459,12 +600,18 @@ __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32
       const uint32_t ei = (uint32_t)__shfl(end, (int)(rb + i), 64);
       const uint32_t pi = (uint32_t)__shfl(pp, (int)(rb + i), 64);
       const uint32_t ci = (uint32_t)__shfl(cex, (int)(rb + i), 64);
-      if (g < T) store_run_chunk(page, ((oi >> 4) + (g - ci)) << 4, oi, ei, rec8, pi);
+      if (g < T) {
+        if (kMode != 1)
+          store_run_chunk<kMode == 2>(page, ((oi >> 4) + (g - ci)) << 4, oi, ei, rec8, pi);
+        else  // measurement variant: everything but the replica stores
+          sink += oi ^ ei ^ (uint32_t)rec8[pi];
+      }
     }
   }
   return !bad;
 }
 
+template <int kMode>
 __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target,
                                                     const uint32_t* __restrict__ ids, uint64_t n,
                                                     const uint64_t* __restrict__ rec_off,
@@ -474,7 +621,7 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, row = lane >> 4;
   uint32_t* win = win_all[wave];
   const uint64_t ntask = (n + 63) / 64;
-  uint32_t bad = 0;
+  uint32_t bad = 0, sink = 0;
   for (uint64_t task = (uint64_t)blockIdx.x * 4 + wave; task < ntask;
        task += (uint64_t)gridDim.x * 4) {
     const uint64_t a = task * 64;
@@ -494,8 +641,8 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
         const uint64_t p = ids ? ids[a + j] : a + j;
         const uint8_t* rec = data + start;
         const bool has = row == 0 && r1 > start;
-        if (!apply_rows(target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec,
-                        (uint32_t)(r1 - start), has))
+        if (!apply_rows<kMode>(target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec,
+                                (uint32_t)(r1 - start), has, sink))
           bad = 1;
         ++j;
         continue;
@@ -518,8 +665,8 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
         const bool has = in && r1 > r0;
         const uint32_t base = (uint32_t)(r0 - start);
         const uint64_t p = ids ? ids[a + ms] : a + ms;
-        if (!apply_rows(target + p * kPage, win + base / 4, win8 + base, (uint32_t)(r1 - r0),
-                        has))
+        if (!apply_rows<kMode>(target + p * kPage, win + base / 4, win8 + base,
+                                (uint32_t)(r1 - r0), has, sink))
           bad = 1;
       }
       wave_lds_sync();
@@ -527,6 +674,7 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
     }
   }
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 1u);
+  if (kMode == 1 && sink == 0x9E3779B9u) atomicOr(err, 2u);
 }
 
 // ------------------------------------------------------------------------- launchers
@@ -541,7 +689,13 @@ static int diff_variant() {
   }
   return g_diff_variant;
 }
+// Apply kernel variant: 0 = normal; 1 = MEASUREMENT ONLY, no replica stores; 2 = nt stores.
+static int g_apply_variant = 0;
 int tune(const char* key, int64_t value) {
+  if (!strcmp(key, "apply_variant") && value >= 0 && value <= 2) {
+    g_apply_variant = (int)value;
+    return 0;
+  }
   if (!strcmp(key, "diff_variant") && value >= 0 && value <= 5) {
     g_diff_variant = (int)value;
     return 0;
@@ -602,7 +756,7 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
       static void (*const kVariants[])(const uint8_t*, const uint8_t*, const uint32_t*, uint64_t,
                                        uint64_t, uint8_t*, uint32_t*, uint32_t*) = {
           diff_pages_kernel<0>, diff_pages_kernel<1>, diff_pages_kernel<2>,
-          diff_pages_kernel<3>, diff_pages_kernel<4>, diff_pages_kernel_o8};
+          diff_pages_kernel<3>, diff_pages_kernel<4>, diff_pages_kernel<5>};
       auto kern = kVariants[diff_variant()];
       hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids, first, m,
                          slots, sizes, block_sum);
@@ -626,7 +780,9 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
   ProfScope ps(prof, 3, s);
-  hipLaunchKernelGGL(apply_kernel, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, target, ids, n,
+  auto kern = g_apply_variant == 1 ? apply_kernel<1> : g_apply_variant == 2 ? apply_kernel<2>
+                                                                              : apply_kernel<0>;
+  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, target, ids, n,
                      rec_off, data, err);
   return hipGetLastError();
 }

@@ -1,0 +1,53 @@
+"""Per-kernel times of the config-2 step in one process (HIP events from libgdsm's profiler):
+diff alone, apply alone (re-applying the same stream is idempotent), and the serial step
+diff -> scan -> pack -> apply, so that the cost one kernel leaves to the next shows up.
+
+    python scripts/ab_step.py [apply_variant values, e.g. 0,1]"""
+import statistics
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import gallocy_amd as ga  # noqa: E402
+from gallocy_amd import gdsm  # noqa: E402
+
+n = 1 << 20
+ctx = ga.Context(n)
+ctx.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+runs = ga.Runs(ctx, n, cap=n * 256)
+ctx.diff(out=runs)
+ctx.apply(runs)
+ctx.sync()
+REPS = 10
+AV = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0]
+
+
+def measure(fn):
+    fn()
+    ctx.sync()
+    ctx.prof_enable(True)
+    for _ in range(REPS):
+        fn()
+    ctx.sync()
+    p = ctx.prof_read()
+    ctx.prof_enable(False)
+    return {k: round(v[0] / v[1], 4) for k, v in p.items() if v[1]}
+
+
+def step():
+    ctx.diff(out=runs)
+    ctx.apply(runs)
+
+
+res = {}
+for r in range(3):
+    for name, fn in [("diff", lambda: ctx.diff(out=runs)), ("step", step)]:
+        res.setdefault(name, []).append(measure(fn))
+    for v in AV:
+        assert gdsm.lib().gdsm_tune(b"apply_variant", v) == 0
+        res.setdefault(f"apply{v}", []).append(measure(lambda: ctx.apply(runs)))
+        res.setdefault(f"step_apply{v}", []).append(measure(step))
+    gdsm.lib().gdsm_tune(b"apply_variant", 0)
+for name, lst in res.items():
+    keys = lst[0].keys()
+    print(name, {k: statistics.median(d[k] for d in lst) for k in keys}, flush=True)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 evidence for the bench workload: kernel trace + stats, then one PMC pass per counter
-# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: TCC slots).
+# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: TCC slots), summarised per kernel.
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
@@ -17,4 +17,7 @@ ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --no-cpu"}
 run kt 400 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 bench.py $ARGS
 run fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o fetch --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu
 run write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o write --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu
-find $OUT -name "*.csv" | head -50
+F=$(find $OUT/fetch -name "*counter_collection.csv" | head -1)
+W=$(find $OUT/write -name "*counter_collection.csv" | head -1)
+python3 scripts/pmc_summary.py "$F" "$W" $OUT/traffic.json > /dev/null && echo "traffic summary: $OUT/traffic.json"
+find $OUT -name "*stats.csv"

@@ -27,8 +27,8 @@ for k in sorted(set(fetch) | set(write)):
     f, w = fetch.get(k, 0.0), write.get(k, 0.0)
     out["kernels"][k] = {"fetch_kb_raw": f, "write_kb": w,
                          "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024)}
-d = out["kernels"].get("gdsm::diff_pages_kernel<false>")
-if d:
-    out["diff_pages_kernel_bytes_per_launch"] = d["hbm_bytes_per_launch"]
+for k, d in out["kernels"].items():
+    if k.startswith("gdsm::diff_pages_kernel"):
+        out["diff_pages_kernel_bytes_per_launch"] = d["hbm_bytes_per_launch"]
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(out, indent=1))

@@ -1,0 +1,158 @@
+// Read-roofline probe for the diff kernel's access pattern on gfx950: two 4 GiB arenas (TWIN and
+// CURRENT, 1M x 4 KiB pages) streamed once, one wave per page, XOR-OR reduced to one word per
+// page. Variants: pages per wave, pages in flight per wave, nt vs default loads, grid shape.
+// Not product code: it measures the ceiling the diff kernel is held against.
+//   hipcc --offload-arch=gfx950 -O3 scripts/read_probe.hip -o scripts/read_probe
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <vector>
+#include <algorithm>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
+// PPW pages per wave, processed INF at a time (INF pages' loads issued before any is reduced).
+template <int PPW, int INF, bool NT>
+__global__ __launch_bounds__(256) void rd_pages(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
+                                                uint32_t* __restrict__ out, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wave) * PPW;
+  for (int j = 0; j < PPW; j += INF) {
+    u32x4 t[INF][4], c[INF][4];
+#pragma unroll
+    for (int q = 0; q < INF; ++q) {
+      const uint64_t p = w0 + j + q;
+      if (p < n) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          t[q][k] = ld<NT>(a + p * 256 + k * 64 + lane);
+          c[q][k] = ld<NT>(b + p * 256 + k * 64 + lane);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < INF; ++q) {
+      const uint64_t p = w0 + j + q;
+      if (p >= n) break;
+      uint32_t d = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u32x4 x = t[q][k] ^ c[q][k];
+        d |= x.x | x.y | x.z | x.w;
+      }
+      const uint64_t m = __ballot(d != 0);
+      if (lane == 0) out[p] = (uint32_t)__popcll(m);
+    }
+  }
+}
+
+// Persistent grid-stride over pages, one page per wave iteration.
+template <bool NT>
+__global__ __launch_bounds__(256) void rd_persist(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
+                                                  uint32_t* __restrict__ out, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < n; p += nw) {
+    u32x4 t[4], c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      t[k] = ld<NT>(a + p * 256 + k * 64 + lane);
+      c[k] = ld<NT>(b + p * 256 + k * 64 + lane);
+    }
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32x4 x = t[k] ^ c[k];
+      d |= x.x | x.y | x.z | x.w;
+    }
+    const uint64_t m = __ballot(d != 0);
+    if (lane == 0) out[p] = (uint32_t)__popcll(m);
+  }
+}
+
+// Flat streaming: every thread reads consecutive 16-B chunks of both arenas (no page structure).
+template <bool NT>
+__global__ __launch_bounds__(256) void rd_flat(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
+                                               uint32_t* __restrict__ out, uint64_t nchunks) {
+  uint32_t d = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < nchunks; g += stride * 4) {
+    u32x4 x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t i = g + u * stride;
+      if (i < nchunks) { x[u] = ld<NT>(a + i); y[u] = ld<NT>(b + i); } else { x[u] = y[u] = (u32x4){0,0,0,0}; }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { const u32x4 z = x[u] ^ y[u]; d |= z.x | z.y | z.z | z.w; }
+  }
+  if (d == 0x12345678u) out[0] = d;
+}
+
+__global__ void fill(u32x4* p, uint64_t n, uint32_t s) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (u32x4){(uint32_t)i ^ s, (uint32_t)(i >> 7), s, (uint32_t)i * 2654435761u};
+}
+
+typedef void (*Kern)(const u32x4*, const u32x4*, uint32_t*, uint64_t);
+
+int main() {
+  const uint64_t n = 1 << 20, chunks = n * 256;
+  u32x4 *a, *b;
+  uint32_t* out;
+  CK(hipMalloc(&a, chunks * 16));
+  CK(hipMalloc(&b, chunks * 16));
+  CK(hipMalloc(&out, n * 4));
+  hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, a, chunks, 1u);
+  hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, b, chunks, 1u);
+  CK(hipDeviceSynchronize());
+  struct V { const char* name; Kern k; unsigned grid; uint64_t arg; };
+  std::vector<V> vs = {
+      {"pages ppw16 inf1 nt", rd_pages<16, 1, true>, (unsigned)(n / 64), n},
+      {"pages ppw16 inf1   ", rd_pages<16, 1, false>, (unsigned)(n / 64), n},
+      {"pages ppw16 inf2 nt", rd_pages<16, 2, true>, (unsigned)(n / 64), n},
+      {"pages ppw16 inf4 nt", rd_pages<16, 4, true>, (unsigned)(n / 64), n},
+      {"pages ppw4  inf1 nt", rd_pages<4, 1, true>, (unsigned)(n / 16), n},
+      {"pages ppw1  inf1 nt", rd_pages<1, 1, true>, (unsigned)(n / 4), n},
+      {"pages ppw64 inf2 nt", rd_pages<64, 2, true>, (unsigned)(n / 256), n},
+      {"persist 2048 nt    ", rd_persist<true>, 2048, n},
+      {"persist 4096 nt    ", rd_persist<true>, 4096, n},
+      {"persist 8192 nt    ", rd_persist<true>, 8192, n},
+      {"persist 2048       ", rd_persist<false>, 2048, n},
+      {"flat 4096 nt       ", rd_flat<true>, 4096, chunks},
+      {"flat 8192 nt       ", rd_flat<true>, 8192, chunks},
+      {"flat 8192          ", rd_flat<false>, 8192, chunks},
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int R = 5, K = 10;
+  std::vector<std::vector<float>> ms(vs.size());
+  for (int r = 0; r < R; ++r)
+    for (size_t v = 0; v < vs.size(); ++v) {
+      hipLaunchKernelGGL(vs[v].k, dim3(vs[v].grid), dim3(256), 0, 0, a, b, out, vs[v].arg);
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < K; ++i)
+        hipLaunchKernelGGL(vs[v].k, dim3(vs[v].grid), dim3(256), 0, 0, a, b, out, vs[v].arg);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float t;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ms[v].push_back(t / K);
+    }
+  for (size_t v = 0; v < vs.size(); ++v) {
+    std::sort(ms[v].begin(), ms[v].end());
+    const double med = ms[v][R / 2];
+    printf("%s  median %.4f ms  min %.4f ms  %.0f GB/s\n", vs[v].name, med, ms[v][0],
+           2.0 * chunks * 16 / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}

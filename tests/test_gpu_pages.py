@@ -350,3 +350,32 @@ def test_apply_async_reports_malformed_stream():
         with pytest.raises(GdsmError) as ei:
             c.sync()
         assert ei.value.errno == 22
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_diff_variants_bit_exact(variant, golden):
+    """Every output-producing diff kernel variant (gdsm_tune "diff_variant") is bit-exact on
+    edge pages, random byte densities (incl. records larger than the LDS stage) and clustered
+    writes."""
+    L = _lib.load()
+    assert L.gdsm_tune(b"diff_variant", variant) == 0
+    try:
+        g = golden["pages"]
+        cases = [(g["edge_twin"], g["edge_cur"])]
+        rng = np.random.default_rng(100 + variant)
+        for density in (0.002, 0.02, 0.2, 0.7):
+            tw = rng.integers(0, 256, (130, 4096), dtype=np.uint8)
+            cu = tw.copy()
+            mask = rng.random(tw.shape) < density
+            cu[mask] ^= rng.integers(1, 256, int(mask.sum()), dtype=np.uint8)
+            cases.append((tw, cu))
+        cases.append(oracle.gen_pages(200, seed=9, mode=1, ppm=100000))
+        cases.append(oracle.gen_pages(200, seed=9, mode=0, ppm=10000))
+        for tw, cu in cases:
+            with ga.Context(len(tw)) as c:
+                c.upload("twin", tw)
+                c.upload("current", cu)
+                ro, data = oracle.diff_pages(tw, cu)
+                _eq_runs(c.diff(cap=max(64, int(ro[-1]))).to_host(), ro, data)
+    finally:
+        L.gdsm_tune(b"diff_variant", 0)
