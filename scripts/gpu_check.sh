@@ -17,7 +17,7 @@ step() {  # name, timeout, cmd...
 }
 WHAT=${1:-all}
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
-  step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
+  step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
