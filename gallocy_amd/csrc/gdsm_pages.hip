@@ -5,11 +5,14 @@
 // gallocy/utils/diff.cpp:73-167, see legacy_diff.cpp.
 //
 // Diff pipeline (all HBM-bound, no MFMA):
-//   1. diff_pages_kernel   one wave per page: 4 x 16 B coalesced loads of twin and current per
-//                          lane, 16-bit byte-diff mask per 16-B chunk, run starts/ends from the
-//                          neighbour chunk's edge bit (shuffles), ranks by wave prefix sums;
-//                          the record goes to the page's fixed slot of the workspace, its size
-//                          to sizes[], the workgroup's sum to block_sum[].
+//   1. diff_compact_kernel one wave per page (16 pages per wave, the next page's loads in
+//                          flight): 4 x 16 B coalesced loads of twin and current per lane,
+//                          16-bit byte-diff mask per 16-B chunk, dirty chunks compacted by
+//                          ballot into LDS, run starts/ends from the neighbour entry's edge bit,
+//                          ranks by wave prefix sums over the compacted lanes; records are built
+//                          in LDS and stored (nontemporal) to the wave's region of the
+//                          workspace, sizes to sizes[], the workgroup's sum to block_sum[].
+//                          (diff_pages_kernel: the earlier whole-page-scan kernels, variants.)
 //   2. scan_blocks_kernel  one workgroup: exclusive scan of block_sum -> block_off.
 //   3. pack_kernel         per workgroup: page offsets inside the block -> rec_off, then
 //                          copies each record from its slot to its packed place.
@@ -299,13 +302,20 @@ __device__ __forceinline__ void emit_image(const PageRuns& P, const uint4 (&c)[4
   }
 }
 
-// Copies n16 16-B words from LDS to global memory (one wave, coalesced 16-B stores).
+// Copies n16 16-B words from LDS to global memory (one wave, coalesced 16-B stores;
+// kNT = nontemporal stores).
+template <bool kNT = false>
 __device__ __forceinline__ void flush_lds(const uint32_t* __restrict__ src, uint32_t n16,
                                           uint8_t* __restrict__ dst, uint32_t lane) {
   wave_lds_sync();
-  const uint4* s = reinterpret_cast<const uint4*>(src);
-  uint4* d = reinterpret_cast<uint4*>(dst);
-  for (uint32_t q = lane; q < n16; q += 64) d[q] = s[q];
+  const u32x4* s = reinterpret_cast<const u32x4*>(src);
+  u32x4* d = reinterpret_cast<u32x4*>(dst);
+  for (uint32_t q = lane; q < n16; q += 64) {
+    if (kNT)
+      __builtin_nontemporal_store(s[q], d + q);
+    else
+      d[q] = s[q];
+  }
   wave_lds_sync();
 }
 
@@ -313,17 +323,13 @@ __device__ __forceinline__ void flush_lds(const uint32_t* __restrict__ src, uint
 // [16w, 16w + 16) of the block in order and appends their records, each rounded up to 16 B, to
 // its own region of the workspace (16 slots = the worst case), which the pack kernel then reads
 // as near-contiguous memory.
-// kVar (gdsm_tune "diff_variant"; in-process A/B, scripts/ab_diff.py):
+// kVar (launcher variants 1-4):
 //   0  records compacted in registers, OR-ed into a per-wave LDS accumulation buffer of
 //      kDiffAcc bytes and written out only when it fills and after the wave's last page: the
-//      stores are whole, contiguous lines (default)
-//   1  as 0, but every record is written out as soon as it is built (one partial line or two
-//      per page: measured 0.10 ms slower per 1M pages than 0, the price of partial-line writes)
+//      stores are whole, contiguous lines
 //   2  byte-loop emission (emit_bytes) into the LDS stage, written out per record
 //   3  MEASUREMENT ONLY: full run scan, records not written (sizes only) -- output is invalid
 //   4  MEASUREMENT ONLY: loads + a change count per page -- the read roofline of this kernel
-// Measured and dropped: next-page register prefetch, a 64-VGPR cap, records
-// stored straight from the lanes.
 constexpr uint32_t kDiffAcc = 4096;  // per-wave LDS accumulation buffer (bytes)
 
 template <int kVar>
@@ -331,7 +337,8 @@ __device__ __forceinline__ void diff_pages_body(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
-  constexpr uint32_t kBuf = (kVar == 0 || kVar == 5) ? kDiffAcc : kDiffStage;
+  static_assert(kVar == 0 || kVar == 2 || kVar == 3 || kVar == 4, "diff variant");
+  constexpr uint32_t kBuf = kVar == 0 ? kDiffAcc : kDiffStage;
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t sel_tab[16];
   __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kBuf / 4];
@@ -340,7 +347,7 @@ __device__ __forceinline__ void diff_pages_body(
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* buf = buf_all[wave];
   const uint64_t w0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock + wave * kDiffPagesPerWave;
-  uint8_t* region = kVar == 5 ? ws + (w0 / kDiffPagesPerWave) * 4096 : ws + w0 * kRecSlot;
+  uint8_t* region = ws + w0 * kRecSlot;
   uint32_t acc = 0;      // record bytes of the wave's pages so far
   uint32_t acc16 = 0;    // region bytes of the wave's pages so far (records rounded to 16 B)
   uint32_t flushed = 0;  // region bytes already stored (variant 0); buffer = [flushed, acc16)
@@ -370,21 +377,18 @@ __device__ __forceinline__ void diff_pages_body(
       } else if (size != 0) {
         if (16u * n16 > kBuf) {
           // larger than the buffer: emitted straight to its place, byte by byte
-          if ((kVar == 0 || kVar == 5) && acc16 > flushed) {
+          if (kVar == 0 && acc16 > flushed) {
             flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
             flushed = acc16;
           }
           emit_bytes(P, c, lane, region + acc16);
-          if (kVar == 0 || kVar == 5) flushed = acc16 + 16u * n16;
-        } else if constexpr (kVar == 0 || kVar == 5) {
+          if (kVar == 0) flushed = acc16 + 16u * n16;
+        } else if constexpr (kVar == 0) {
           if (acc16 - flushed + 16u * n16 > kBuf) {
             flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
             flushed = acc16;
           }
           emit_image(P, c, lane, buf + (acc16 - flushed) / 4, n16, sel_tab);
-        } else if constexpr (kVar == 1) {
-          emit_image(P, c, lane, buf, n16, sel_tab);
-          flush_lds(buf, n16, region + acc16, lane);
         } else {
           emit_bytes(P, c, lane, reinterpret_cast<uint8_t*>(buf));
           flush_lds(buf, n16, region + acc16, lane);
@@ -395,8 +399,7 @@ __device__ __forceinline__ void diff_pages_body(
     acc += size;
     acc16 += (size + 15u) & ~15u;
   }
-  if ((kVar == 0 || kVar == 5) && acc16 > flushed && (kVar == 0 || acc16 <= 4096))
-    flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
+  if (kVar == 0 && acc16 > flushed) flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
   if (lane < cnt) sizes[w0 + lane] = my_size;
   if (lane == 0) wsum[wave] = acc;
   __syncthreads();
@@ -409,6 +412,139 @@ __global__ __launch_bounds__(256) void diff_pages_kernel(
     const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
   diff_pages_body<kVar>(twin, cur, ids, first, n, ws, sizes, block_sum);
+}
+
+// ---- compacted diff (launcher variants 0, 5, 6): work only on the page's dirty 16-B chunks.
+// After the byte-diff masks are built, a ballot per k ranks the dirty chunks in page order and
+// each dirty lane parks (chunk << 16 | mask) and its current bytes in the wave's LDS list. Run
+// starts/ends, ranks and emission then run over the compacted lanes, so a sparse page costs one
+// pair of wave scans instead of four, and the page's registers die right after the masks (the
+// next page's loads are in flight meanwhile: kPrefetch). Records go out with nontemporal stores
+// (kStore 2): measured 0.05 ms per 1M pages faster than plain stores, and the following pack
+// and the previous step's apply write-back no longer slow the diff (scripts/ab_step.py).
+// A page with more than 64 dirty chunks (over a quarter of the page changed) is only sized here
+// (its size is flagged with kSlowPage in sizes[] and it takes no room in the wave's region); the
+// pack kernel, which knows its final offset, emits it straight from the arenas (emit_bytes).
+constexpr uint32_t kSlowPage = 0x80000000u;
+// Per-wave LDS record buffer (bytes): holds the largest record of a page with <= 64 dirty chunks
+// (4 + 4 * 512 runs + 1024 payload bytes = 3076, rounded to 16 B).
+constexpr uint32_t kCAcc = 3088;
+
+// Size of the record of a page whose byte-diff masks m[k] (chunk (k, lane)) are in registers
+// (the run ends need the next chunk's first bit: DPP from lane + 1, wrapping across k).
+__device__ __forceinline__ uint32_t record_size_masks(const uint32_t (&m)[4], uint32_t lane) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t dn = from_next_lane(m[k]);
+    if (k < 3 && lane == 63) dn = lane_bcast(m[k < 3 ? k + 1 : 3], 0);
+    const uint32_t e = m[k] & ~((m[k] >> 1) | ((dn & 1u) << 15)) & 0xFFFFu;
+    v += (uint32_t)__popc(e) | ((uint32_t)__popc(m[k]) << 16);
+  }
+  const uint32_t tot = wave_sum(v);
+  const uint32_t NR = tot & 0xFFFFu, NP = tot >> 16;
+  return NR ? 4u + 4u * NR + ((NP + 3u) & ~3u) : 0u;
+}
+
+template <bool kPrefetch, int kStore>
+__device__ __forceinline__ void diff_compact_body(
+    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t sel_tab[16];
+  __shared__ uint32_t ent_all[4][64];
+  __shared__ uint4 dat_all[4][64];
+  __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kCAcc / 4];
+  if (threadIdx.x < 16) sel_tab[threadIdx.x] = compact_sel(threadIdx.x);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* ent = ent_all[wave];
+  uint4* dat = dat_all[wave];
+  uint32_t* buf = buf_all[wave];
+  const uint64_t w0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock + wave * kDiffPagesPerWave;
+  uint8_t* region = ws + w0 * kRecSlot;
+  uint32_t acc = 0;      // record bytes of the wave's pages so far
+  uint32_t acc16 = 0;    // region bytes used so far (records rounded to 16 B; slow pages: none)
+  uint32_t flushed = 0;  // region bytes already stored; the LDS buffer holds [flushed, acc16)
+  uint32_t my_size = 0;  // lane j: size (| kSlowPage) of the wave's page j
+  const uint32_t cnt = (uint32_t)min((uint64_t)kDiffPagesPerWave, n > w0 ? n - w0 : 0);
+  uint4 t[4], c[4];
+  if (kPrefetch && cnt) load_page(twin, cur, ids ? ids[first + w0] : first + w0, lane, t, c);
+  for (uint32_t j = 0; j < cnt; ++j) {
+    if (!kPrefetch) load_page(twin, cur, ids ? ids[first + w0 + j] : first + w0 + j, lane, t, c);
+    uint32_t m[4], D = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m[k] = diffmask16(t[k], c[k]);
+      const uint64_t B = __ballot(m[k] != 0u);
+      const uint32_t rank = D + __builtin_amdgcn_mbcnt_hi(
+                                    (uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+      if (m[k] && rank < 64u) {
+        ent[rank] = ((uint32_t)(k * 64 + lane) << 16) | m[k];
+        dat[rank] = c[k];
+      }
+      D += (uint32_t)__popcll(B);
+    }
+    if (kPrefetch && j + 1 < cnt)
+      load_page(twin, cur, ids ? ids[first + w0 + j + 1] : first + w0 + j + 1, lane, t, c);
+    uint32_t size = 0, flag = 0;
+    if (D > 64u) {
+      size = record_size_masks(m, lane);
+      flag = kSlowPage;
+    } else if (D) {
+      wave_lds_sync();
+      const bool valid = lane < D;
+      const uint32_t E = valid ? ent[lane] : 0u;
+      const uint32_t Ep = from_prev_lane(E), En = from_next_lane(E);
+      const uint32_t g = E >> 16, mm = E & 0xFFFFu;
+      const uint32_t up = (Ep != 0u && (Ep >> 16) + 1u == g) ? (Ep >> 15) & 1u : 0u;
+      const uint32_t dn = (En != 0u && (En >> 16) == g + 1u) ? En & 1u : 0u;
+      const uint32_t s = mm & ~((mm << 1) | up) & 0xFFFFu;
+      const uint32_t e = mm & ~((mm >> 1) | (dn << 15)) & 0xFFFFu;
+      const uint32_t v = (uint32_t)__popc(e) | ((uint32_t)__popc(mm) << 16);
+      const uint32_t inc = wave_incl_sum(v);
+      const uint32_t tot = lane_bcast(inc, 63);
+      const uint32_t ls = s ? g * 16u + 32u - (uint32_t)__builtin_clz(s) : 0u;
+      const uint32_t ps = from_prev_lane(wave_incl_max(ls));
+      const uint32_t NR = tot & 0xFFFFu, NP = tot >> 16;
+      size = 4u + 4u * NR + ((NP + 3u) & ~3u);
+      const uint32_t rec16 = (size + 15u) & ~15u;
+      if (acc16 - flushed + rec16 > kCAcc) {
+        if (kStore != 1) flush_lds<kStore == 2>(buf, (acc16 - flushed) >> 4, region + flushed, lane);
+        flushed = acc16;
+      }
+      uint32_t* img = buf + (acc16 - flushed) / 4u;
+      uint4* z = reinterpret_cast<uint4*>(img);
+      for (uint32_t q = lane; q < rec16 >> 4; q += 64) z[q] = make_uint4(0, 0, 0, 0);
+      const uint4 cc = valid ? dat[lane] : make_uint4(0, 0, 0, 0);
+      wave_lds_sync();
+      if (lane == 0) img[0] = NR;
+      if (valid) emit_compact(g, s, e, mm, ps, inc - v, cc, img, 4u + 4u * NR, sel_tab);
+      wave_lds_sync();
+      acc16 += rec16;
+    }
+    if (lane == j) my_size = size | flag;
+    acc += size;
+  }
+  if (acc16 > flushed) {
+    if (kStore != 1) flush_lds<kStore == 2>(buf, (acc16 - flushed) >> 4, region + flushed, lane);
+    else if (wave_sum(buf[lane]) == 0x9E3779B9u) sizes[0] = 0;  // keep the LDS work alive
+  }
+  if (lane < cnt) sizes[w0 + lane] = my_size;
+  if (lane == 0) wsum[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// kStore: 0 = plain record stores, 1 = MEASUREMENT ONLY: no record stores, 2 = nontemporal.
+// kWaves: occupancy target handed to the register allocator (waves per SIMD).
+template <bool kPrefetch, int kStore, int kWaves = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_compact_kernel(
+    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
+  diff_compact_body<kPrefetch, kStore>(twin, cur, ids, first, n, ws, sizes, block_sum);
 }
 
 // One workgroup: block_off[b] = base + sum(block_sum[0..b)), base = rec_off[first].
@@ -440,31 +576,42 @@ __global__ __launch_bounds__(1024) void scan_blocks_kernel(const uint32_t* __res
 // Per workgroup (64 pages): page offsets inside the block -> rec_off; then every thread copies
 // output dwords of the block's packed range, finding each dword's record by binary search over
 // the 65 block-relative offsets in LDS (all loads independent, stores contiguous). A record's
-// source is its wave region (diff_pages_body) at the 16-B rounded prefix `src` of its row.
+// source is its wave region (diff kernels) at the 16-B rounded prefix `src` of its row. Pages
+// flagged kSlowPage (compacted diff: > 64 dirty chunks) have no region copy: one wave re-reads
+// the page and emits its record straight into the packed stream.
 __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ ws,
                                                    const uint32_t* __restrict__ sizes,
                                                    const uint64_t* __restrict__ block_off,
                                                    uint64_t first, uint64_t n,
                                                    uint64_t* __restrict__ rec_off,
-                                                   uint8_t* __restrict__ data, uint64_t cap) {
+                                                   uint8_t* __restrict__ data, uint64_t cap,
+                                                   const uint8_t* __restrict__ twin,
+                                                   const uint8_t* __restrict__ cur,
+                                                   const uint32_t* __restrict__ ids) {
   __shared__ uint32_t off[kDiffPagesPerBlock + 1];
   __shared__ uint32_t src[kDiffPagesPerBlock];
+  __shared__ uint64_t slow_mask;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t b0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock;
   const uint64_t base = block_off[blockIdx.x];
   if (wave == 0) {
     static_assert(kDiffPagesPerWave == 16, "one DPP row per wave region");
     const uint64_t i = b0 + lane;
-    const uint32_t sz = (i < n) ? sizes[i] : 0u;
+    const uint32_t raw = (i < n) ? sizes[i] : 0u;
+    const bool slow = (raw & kSlowPage) != 0u;
+    const uint32_t sz = raw & ~kSlowPage;
     const uint32_t inc = wave_incl_sum(sz);
-    const uint32_t s16 = (sz + 15u) & ~15u;
+    const uint32_t s16 = slow ? 0u : (sz + 15u) & ~15u;
     src[lane] = row_incl_sum(s16) - s16;
     off[lane] = inc - sz;
     if (lane == 63) off[64] = inc;
+    const uint64_t sm = __ballot(slow);
+    if (lane == 0) slow_mask = sm;
     if (i < n) rec_off[first + i + 1] = base + inc;
     if (first == 0 && blockIdx.x == 0 && lane == 0) rec_off[0] = 0;
   }
   __syncthreads();
+  const uint64_t sm = slow_mask;
   // Only records that end inside the capacity are copied.
   uint32_t limit = off[64];
   if (base + limit > cap) {
@@ -479,9 +626,21 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ w
 #pragma unroll
     for (uint32_t step = 32; step; step >>= 1)
       if (off[r + step] <= byte) r += step;
+    if ((sm >> r) & 1u) continue;
     const uint32_t* p = reinterpret_cast<const uint32_t*>(
         ws + (b0 + (r & ~(kDiffPagesPerWave - 1))) * kRecSlot + src[r] + (byte - off[r]));
     dst[g] = *p;
+  }
+  for (uint64_t rem = sm; rem;) {  // wave-uniform
+    const uint32_t r = (uint32_t)__builtin_ctzll(rem);
+    rem &= rem - 1;
+    if ((r & 3u) != wave || base + off[r + 1] > cap) continue;
+    const uint64_t i = first + b0 + r;
+    uint4 t[4], c[4];
+    load_page(twin, cur, ids ? ids[i] : i, lane, t, c);
+    PageRuns P;
+    scan_page(t, c, lane, P);
+    emit_bytes(P, c, lane, data + base + off[r]);
   }
 }
 
@@ -678,14 +837,21 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
 }
 
 // ------------------------------------------------------------------------- launchers
-// Diff kernel variant (see diff_pages_kernel); gdsm_tune("diff_variant", v) or
-// GDSM_DIFF_VARIANT=v; used for in-process A/B measurements.
+// Diff kernel variant, gdsm_tune("diff_variant", v) or GDSM_DIFF_VARIANT=v (in-process A/B,
+// scripts/ab_diff.py):
+//   0  compacted, next page's loads in flight, nontemporal record stores, 5 waves/SIMD (default)
+//   1  per-chunk scans over the whole page, records OR-ed into a per-wave LDS buffer
+//   2  as 1 with byte-loop emission
+//   3  MEASUREMENT ONLY: variant 1's full run scan, records not written (output invalid)
+//   4  MEASUREMENT ONLY: loads + a change count per page (the read roofline of this kernel)
+//   5  compacted, one page at a time, plain stores, 8 waves/SIMD
+//   6  MEASUREMENT ONLY: variant 0 without the record stores
 static int g_diff_variant = -1;
 static int diff_variant() {
   if (g_diff_variant < 0) {
     const char* e = getenv("GDSM_DIFF_VARIANT");
     g_diff_variant = e ? atoi(e) : 0;
-    if (g_diff_variant < 0 || g_diff_variant > 5) g_diff_variant = 0;
+    if (g_diff_variant < 0 || g_diff_variant > 6) g_diff_variant = 0;
   }
   return g_diff_variant;
 }
@@ -696,7 +862,7 @@ int tune(const char* key, int64_t value) {
     g_apply_variant = (int)value;
     return 0;
   }
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 5) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 6) {
     g_diff_variant = (int)value;
     return 0;
   }
@@ -753,10 +919,13 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
     const uint64_t nb = (m + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
     {
       ProfScope ps(prof, 0, s);
+      // gdsm_tune("diff_variant", v): see diff_variant() above
       static void (*const kVariants[])(const uint8_t*, const uint8_t*, const uint32_t*, uint64_t,
                                        uint64_t, uint8_t*, uint32_t*, uint32_t*) = {
-          diff_pages_kernel<0>, diff_pages_kernel<1>, diff_pages_kernel<2>,
-          diff_pages_kernel<3>, diff_pages_kernel<4>, diff_pages_kernel<5>};
+          diff_compact_kernel<true, 2, 5>, diff_pages_kernel<0>,
+          diff_pages_kernel<2>,            diff_pages_kernel<3>,
+          diff_pages_kernel<4>,            diff_compact_kernel<false, 0, 4>,
+          diff_compact_kernel<true, 1, 5>};
       auto kern = kVariants[diff_variant()];
       hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids, first, m,
                          slots, sizes, block_sum);
@@ -769,7 +938,7 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
     {
       ProfScope ps(prof, 2, s);
       hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nb), dim3(256), 0, s, slots, sizes,
-                         block_off, first, m, rec_off, data, cap);
+                         block_off, first, m, rec_off, data, cap, twin, cur, ids);
     }
   }
   return hipGetLastError();

@@ -1,9 +1,9 @@
 """In-process A/B of diff kernel variants (interleaved rounds, one device): per-launch time of
 diff_pages_kernel from HIP events, for BASELINE config 2 (1M pages, 1 % word writes).
 
-    python scripts/ab_diff.py diff_variant 0,1,2,3,4
+    python scripts/ab_diff.py diff_variant 0,1,5,6,3,4
 
-Variants 3 and 4 are measurement-only kernels (no valid output); their totals are not checked."""
+Variants 3, 4 and 6 are measurement-only kernels (no valid output); their totals are not checked."""
 import statistics
 import sys
 from pathlib import Path
@@ -32,7 +32,7 @@ for r in range(ROUNDS):
         p = ctx.prof_read()
         ctx.prof_enable(False)
         res[v].append(p["diff"][0] / p["diff"][1])
-        if KEY != "diff_variant" or v in (0, 1, 2):
+        if KEY != "diff_variant" or v in (0, 1, 2, 5):
             t = runs.total()
             assert total is None or t == total, (v, t, total)
             total = t

@@ -152,6 +152,11 @@ def test_capacity_overflow_reports_enospc():
         L = _lib.load()
         assert L.gdsm_memcpy_d2h(c.handle, got.ctypes.data, runs.s.rec_off, got.nbytes) == 0
         assert np.array_equal(got, ro)  # rec_off is complete even when data overflowed
+        # every record that ends inside the capacity was written (fast and re-read pages alike)
+        fit = int(ro[ro <= cap].max())
+        part = np.empty(fit, np.uint8)
+        assert L.gdsm_memcpy_d2h(c.handle, part.ctypes.data, runs.s.data, fit) == 0
+        assert np.array_equal(part, data[:fit])
 
 
 def test_apply_rejects_malformed_stream():
@@ -352,7 +357,31 @@ def test_apply_async_reports_malformed_stream():
         assert ei.value.errno == 22
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+def _mixed_density_pages(rng, n):
+    """Pages whose dirty-chunk counts straddle the compacted kernel's 64-chunk fast path: clean,
+    sparse, exactly 64 / 65 dirty 16-B chunks, dense, fully changed, in random order."""
+    tw = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    cu = tw.copy()
+    for i in range(n):
+        kind = rng.integers(0, 6)
+        if kind == 1:
+            m = rng.random(4096) < 0.003
+        elif kind in (2, 3):
+            m = np.zeros(4096, bool)
+            chunks = rng.choice(256, 64 if kind == 2 else 65, replace=False)
+            for ch in chunks:
+                m[ch * 16 + rng.integers(0, 16, rng.integers(1, 17))] = True
+        elif kind == 4:
+            m = rng.random(4096) < 0.4
+        elif kind == 5:
+            m = np.ones(4096, bool)
+        else:
+            continue
+        cu[i, m] ^= rng.integers(1, 256, int(m.sum()), dtype=np.uint8)
+    return tw, cu
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 5])
 def test_diff_variants_bit_exact(variant, golden):
     """Every output-producing diff kernel variant (gdsm_tune "diff_variant") is bit-exact on
     edge pages, random byte densities (incl. records larger than the LDS stage) and clustered
@@ -371,6 +400,7 @@ def test_diff_variants_bit_exact(variant, golden):
             cases.append((tw, cu))
         cases.append(oracle.gen_pages(200, seed=9, mode=1, ppm=100000))
         cases.append(oracle.gen_pages(200, seed=9, mode=0, ppm=10000))
+        cases.append(_mixed_density_pages(rng, 300))
         for tw, cu in cases:
             with ga.Context(len(tw)) as c:
                 c.upload("twin", tw)
