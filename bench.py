@@ -123,15 +123,18 @@ def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
 DIFF_KERNEL = "gdsm::diff_compact_kernel"
 
 
-def read_traffic():
+def read_traffic(pages: int, mode: str, ppm: int):
     """Per-launch HBM bytes of the diff kernel from the newest committed PMC summary that
-    measured that kernel (profiles/*traffic*.json, scripts/gpu_prof.sh), else None."""
+    measured that kernel on this workload (profiles/*traffic*.json, scripts/gpu_prof.sh), else
+    None. Summaries without a workload tag are for the default config-2 workload."""
+    default = {"pages": 1 << 20, "mode": "uniform", "ppm": 10000}
     for p in sorted((ROOT / "profiles").glob("*traffic*.json"), reverse=True):
         try:
             j = json.loads(p.read_text())
         except Exception:  # noqa: BLE001
             continue
-        if str(j.get("diff_kernel", "")).startswith(DIFF_KERNEL):
+        if (str(j.get("diff_kernel", "")).startswith(DIFF_KERNEL)
+                and j.get("workload", default) == {"pages": pages, "mode": mode, "ppm": ppm}):
             return j.get("diff_kernel_bytes_per_launch"), p.name
     return None, None
 
@@ -343,14 +346,17 @@ def main():
                                      ctx.stream)
     replica_ok = rc == 0 and chk.total() == 0 if shard is None else shard.verify()
 
+    # The diff runs as ceil(n / 1M) chunk launches per step (kDiffChunk): bytes per launch and
+    # time per launch are both taken over one chunk launch on average.
     diff_ms, diff_launches = prof["diff"]
     avg_diff_ms = diff_ms / max(1, diff_launches)
-    diff_bytes = n * 8192 + total  # algorithmic: twin + current read, records written
+    per_step = max(1, diff_launches // args.steps)
+    diff_bytes = (n * 8192 + total) / per_step  # algorithmic per launch: twin + current, records
     achieved = diff_bytes / (avg_diff_ms * 1e-3) / 1e9
     step_bytes = n * 8192 + 2 * total + pay  # B_page summed
     ms_step = dt / args.steps * 1e3
     value = world * n * args.steps / dt
-    traffic, traffic_src = read_traffic()
+    traffic, traffic_src = read_traffic(n, args.mode, ppm)
 
     if rank == 0:
         stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
