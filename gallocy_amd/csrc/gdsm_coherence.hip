@@ -21,14 +21,18 @@
 //                       coalesced 64-event steps. Records the last head's page-table word so
 //                       pass C never reads a word another block writes.
 //   B coh_group/_top/_rescan  exclusive scan of the block aggregates (groups of 1024 blocks).
-//   C coh_apply_kernel  persistent workgroups, 8 consecutive events per thread in registers
-//                       (next block prefetched), block scan with the carry-in, per-event
-//                       faults, segmented fault sums, final words written at segment ends
-//                       (atomics only for segments split across blocks), one partial row of
-//                       totals per block.
+//   C coh_apply_block_kernel  one block per workgroup, 8 consecutive events per thread, each
+//                       wave on its own 512 events (coh_wave): DPP scans, one barrier for the
+//                       wave aggregates, per-event faults from a (last CONST, reads since)
+//                       state, page-table words loaded / stored through a per-wave LDS head
+//                       list by consecutive lanes, one partial row of totals per block.
+//                       (coh_apply_kernel: the round-1 persistent block-scan kernel, variant 1.)
 //   D coh_reduce_kernel partial rows -> the 10 batch totals.
 #include "gdsm_common.h"
 #include "gdsm_launch.h"
+
+#include <stdlib.h>
+#include <string.h>
 
 namespace gdsm {
 
@@ -87,6 +91,27 @@ __device__ __forceinline__ uint32_t wave_incl_segsum(uint32_t v) {
     const uint32_t t = __shfl_up(v, d, 64);
     if (lane >= (uint32_t)d) v = segsum(t, v);
   }
+  return v;
+}
+
+// The same two scans on DPP (no LDS traffic): 0 is the identity of tcompose and of segsum,
+// and it is what an out-of-range or masked-off DPP source reads.
+__device__ __forceinline__ uint32_t wave_incl_compose_dpp(uint32_t v) {
+  v = tcompose(dpp0<0x111>(v), v);
+  v = tcompose(dpp0<0x112>(v), v);
+  v = tcompose(dpp0<0x114>(v), v);
+  v = tcompose(dpp0<0x118>(v), v);
+  v = tcompose(dpp0<0x142, 0xA>(v), v);
+  v = tcompose(dpp0<0x143, 0xC>(v), v);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_segsum_dpp(uint32_t v) {
+  v = segsum(dpp0<0x111>(v), v);
+  v = segsum(dpp0<0x112>(v), v);
+  v = segsum(dpp0<0x114>(v), v);
+  v = segsum(dpp0<0x118>(v), v);
+  v = segsum(dpp0<0x142, 0xA>(v), v);
+  v = segsum(dpp0<0x143, 0xC>(v), v);
   return v;
 }
 
@@ -485,6 +510,267 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
+// ---------------------------------------------------------------- C': wave-sliced pass C
+// Same block / carry inputs as coh_apply_kernel, restated for a low instruction count per event:
+//  * every wave works on its own 512 events (8 consecutive per lane); neighbours by DPP, the
+//    wave edges read from memory; ONE barrier per block hands the four wave aggregates across
+//    (double-buffered slots);
+//  * pages are compared as 32-bit ids (SPEC §1: page ids are u32; any higher page bit marks the
+//    batch invalid);
+//  * inside a lane the state is kept as (C, R) = the last CONST word and the OR of the reads
+//    since, so an event costs a few selects instead of a transform composition: a read by n
+//    faults iff n is outside C.copyset | R; a write by n faults unless C is EXCLUSIVE, owned by
+//    n and no read since brought in a node outside C.copyset; the lane aggregate for the scan
+//    is CONST(C) then READ(R), or READ(R) when the lane saw no CONST;
+//  * fault counts are segmented per wave (a segment that leaves the wave adds its count
+//    atomically; its head's old count stays in memory); page-table words move through the wave's
+//    LDS head list (below), so loads and stores are coalesced 8-B accesses.
+struct CohAcc {
+  uint32_t inv, xfer;
+  uint64_t nf8;  // per-node faults of the block, one byte per node (<= 8 per thread)
+};
+
+__device__ __forceinline__ uint32_t page32(uint64_t e) { return (uint32_t)(e >> 4); }
+
+// Page-table traffic of one wave goes through its LDS head list (wd / hpg, kCohHeads entries):
+// the heads of the wave are ranked in event order; their page-table words are loaded by
+// consecutive lanes (coalesced), and every segment that starts AND ends inside the wave leaves
+// its final (state | faults << 32) word in its head's slot, stored by consecutive lanes as one
+// 8-B write per page. Only the wave's first segment (opened before it) and its last (continued
+// after it) touch the page table from the event's lane: one state store / fault atomic each.
+constexpr uint32_t kCohHeads = 64 * kCohK;  // heads per wave, at most one per event
+constexpr uint32_t kSent = 0xFFFFFFFFu;
+
+// kMeasure (MEASUREMENT ONLY, output invalid): 1 = no page-table stores, 2 = no page-table
+// loads or stores either.
+template <bool kFull, int kMeasure = 0>
+__device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
+                                         const uint64_t* __restrict__ ev, uint64_t n,
+                                         const uint64_t (&e)[kCohK], uint64_t b0, uint32_t cnt,
+                                         uint32_t lh, uint64_t lhp, uint32_t cin,
+                                         uint32_t* __restrict__ slot, uint64_t* __restrict__ wd,
+                                         uint32_t* __restrict__ hpg, CohAcc& A, uint32_t& bad) {
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t first = t * kCohK;  // block-relative index of e[0]
+  uint32_t* pst = reinterpret_cast<uint32_t*>(pt);
+  uint32_t* pfl = pst + 1;
+  const uint64_t wfirst = b0 + (uint64_t)wave * 64 * kCohK;
+  const uint32_t nvalid =
+      kFull ? kCohK
+            : (uint32_t)min((int64_t)kCohK, max((int64_t)0, (int64_t)cnt - (int64_t)first));
+  uint32_t hib = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCohK; ++k)
+    if (kFull || k < nvalid) hib |= (uint32_t)(e[k] >> 36);
+  if (hib) bad = 1;
+  uint32_t pprev = from_prev_lane(page32(e[kCohK - 1]));
+  uint32_t pnext = from_next_lane(page32(e[0]));
+  if (lane == 0 && wfirst > 0 && wfirst <= n) pprev = page32(ev[wfirst - 1]);
+  if (lane == 63 && wfirst + 64 * kCohK < n) pnext = page32(ev[wfirst + 64 * kCohK]);
+  const uint64_t g0 = b0 + first;  // global index of e[0]
+
+  // ---- heads and segment ends
+  uint32_t hmask = 0, emask = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCohK; ++k) {
+    if (kFull || k < nvalid) {
+      const uint32_t pk = page32(e[k]);
+      const uint32_t pp = k ? page32(e[k > 0 ? k - 1 : 0]) : pprev;
+      if ((k == 0 && g0 == 0) || pk != pp) {
+        hmask |= 1u << k;
+        if ((k > 0 || g0 > 0) && pk < pp) bad = 1;
+        if (pk >= n_pages) bad = 1;
+      }
+      const uint32_t pn = (k + 1 < kCohK) ? page32(e[k + 1 < kCohK ? k + 1 : k]) : pnext;
+      if (g0 + k + 1 >= n || pn != pk) emask |= 1u << k;
+    }
+  }
+  const uint32_t hc = (uint32_t)__popc(hmask);
+  const uint32_t hinc = wave_incl_sum(hc);
+  const uint32_t hb0 = hinc - hc, nh = lane_bcast(hinc, 63);
+
+  // ---- head list: pages, then the page-table words by consecutive lanes (before the barrier)
+  uint32_t hr = hb0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCohK; ++k)
+    if ((hmask >> k) & 1u) {
+      const uint32_t pk = page32(e[k]);
+      if (first + k == lh) {  // the block's last head: pass A's snapshot
+        hpg[hr] = kSent;
+        wd[hr] = lhp;
+      } else {
+        hpg[hr] = pk < n_pages ? pk : kSent;
+        wd[hr] = 0;
+      }
+      ++hr;
+    }
+  wave_lds_sync();
+  for (uint32_t j = lane; j < nh; j += 64) {
+    const uint32_t pg = hpg[j];
+    if (pg != kSent) wd[j] = (kMeasure < 2) ? pt[pg] : (uint64_t)pg * 0x9E3779B9u;
+    hpg[j] = kSent;
+  }
+  wave_lds_sync();
+
+  // ---- lane aggregate: CONST(last CONST word) then READ(reads since), or READ(all reads)
+  uint32_t lc = 0, ra = 0, hasc = hmask;
+  hr = hb0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCohK; ++k)
+    if (kFull || k < nvalid) {
+      const uint32_t x = (uint32_t)e[k], node = (x >> 1) & 7u, bit = 1u << node;
+      if ((hmask >> k) & 1u) {
+        lc = (uint32_t)wd[hr++];
+        ra = 0;
+      }
+      hasc |= x & 1u;
+      if (x & 1u) {
+        lc = (node << 8) | bit | 0x60000u;
+        ra = 0;
+      } else {
+        ra |= bit;
+      }
+    }
+  const uint32_t a = hasc ? tcompose(kConst | lc, ra) : ra;
+  const uint32_t inc = wave_incl_compose_dpp(a);
+  if (lane == 63) slot[wave] = inc;
+  __syncthreads();
+  uint32_t carry = cin;
+  for (uint32_t w = 0; w < wave; ++w) carry = tcompose(carry, slot[w]);
+  const uint32_t cur = tcompose(carry, from_prev_lane(inc));
+  if (!(cur & kConst) && (hmask & 1u) == 0u && (kFull || nvalid > 0)) bad = 1;
+
+  // ---- walk: faults, invalidations, transfers; final state of each segment end
+  uint32_t C = cur & ~kConst, R = 0, fmask = 0, run = 0;
+  hr = hb0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCohK; ++k) {
+    if (kFull || k < nvalid) {
+      const uint32_t x = (uint32_t)e[k], node = (x >> 1) & 7u, bit = 1u << node;
+      const uint32_t wr = x & 1u;
+      if ((hmask >> k) & 1u) {
+        C = (uint32_t)wd[hr++];
+        R = 0;
+        run = 0;
+      }
+      const uint32_t csr = (C | R) & 0xFFu;
+      const uint32_t own = (((C >> 8) & 0xFFu) == node) ? 1u : 0u;
+      const uint32_t excl = (((C >> 16) & 3u) == 2u && (R & ~C) == 0u) ? 1u : 0u;
+      const uint32_t wf = wr & ~(excl & own);
+      const uint32_t rf = ((csr >> node) & 1u) ^ 1u;
+      const uint32_t f = wr ? wf : rf;
+      A.inv += wf ? (uint32_t)__popc(csr & ~bit) : 0u;
+      A.xfer += wf & (own ^ 1u);
+      A.nf8 += (uint64_t)f << (8u * node);
+      fmask |= f << k;
+      run += f;
+      if (wr) {
+        C = (node << 8) | bit | 0x60000u;
+        R = 0;
+      } else {
+        R |= bit;
+      }
+      if ((emask >> k) & 1u) {
+        const uint32_t pk = page32(e[k]);
+        const uint32_t flip = (((C >> 16) & 3u) == 2u && (R & ~C) != 0u) ? 0x30000u : 0u;
+        const uint32_t st = (C | R) ^ flip;
+        if (hr > 0)
+          hpg[hr - 1] = st;  // segment inside the wave: parked in its head's slot
+        else if (pk < n_pages && kMeasure == 0)
+          pst[2 * (uint64_t)pk] = st;  // the wave's first segment, opened before it
+        if (kMeasure && pk == kSent) bad |= st;
+      }
+    }
+  }
+  wave_lds_sync();
+
+  // ---- fault counts since each head (segmented over the wave); the head's old count is added
+  // for segments that end in the wave, and stays in memory for the two edge segments
+  const uint32_t sex = from_prev_lane(wave_incl_segsum_dpp((hmask ? kConst : 0u) | run));
+  uint32_t running = sex & ~kConst;
+  hr = hb0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCohK; ++k) {
+    if (kFull || k < nvalid) {
+      const uint32_t f = (fmask >> k) & 1u;
+      if ((hmask >> k) & 1u) {
+        running = f;
+        ++hr;
+      } else {
+        running += f;
+      }
+      const uint32_t pk = page32(e[k]);
+      if ((emask >> k) & 1u) {
+        if (hr > 0) {
+          if (pk < n_pages) {
+            const uint32_t st = hpg[hr - 1];
+            const uint32_t fl = (uint32_t)(wd[hr - 1] >> 32) + running;
+            wd[hr - 1] = (uint64_t)st | ((uint64_t)fl << 32);
+            hpg[hr - 1] = pk;
+          }
+        } else if (running && pk < n_pages && kMeasure == 0) {
+          atomicAdd(&pfl[2 * (uint64_t)pk], running);
+        }
+      } else if (k == kCohK - 1 && lane == 63 && running && pk < n_pages && kMeasure == 0) {
+        atomicAdd(&pfl[2 * (uint64_t)pk], running);  // continues past this wave
+      }
+      if (kMeasure && pk == kSent) bad |= running;
+    }
+  }
+  wave_lds_sync();
+  // ---- segments closed inside the wave: one 8-B page-table word each, consecutive lanes
+  for (uint32_t j = lane; j < nh; j += 64) {
+    const uint32_t pg = hpg[j];
+    if (pg != kSent && kMeasure == 0) pt[pg] = wd[j];
+  }
+  wave_lds_sync();
+}
+
+// C' kernel: one 2048-event block per workgroup, four coh_wave bodies (no persistent loop and
+// no prefetch: at 82 VGPRs five workgroups per CU hide the latency; a persistent version with
+// the next block in flight ran at 3 waves/SIMD and was 1.3x slower), totals reduced per block
+// into a partial row.
+template <int kMeasure>
+__global__ __launch_bounds__(256) void coh_apply_block_kernel(
+    uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
+    uint64_t nb, const uint32_t* __restrict__ carry, const uint32_t* __restrict__ last_head,
+    const uint64_t* __restrict__ head_pt, uint32_t* __restrict__ partial,
+    uint32_t* __restrict__ err) {
+  __shared__ uint32_t slots[4];
+  __shared__ uint32_t red[4][10];
+  __shared__ uint64_t wd[4][kCohHeads];
+  __shared__ uint32_t hpg[4][kCohHeads];
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint64_t b = blockIdx.x;
+  uint32_t bad = 0;
+  CohAcc A;
+  A.inv = A.xfer = 0;
+  A.nf8 = 0;
+  const uint64_t b0 = b * kCohBlock;
+  const uint32_t cnt = (uint32_t)min((uint64_t)kCohBlock, n - b0);
+  uint64_t e[kCohK];
+  load_block_events<true>(ev, n, b0 + t * kCohK, e);
+  if (cnt == kCohBlock)
+    coh_wave<true, kMeasure>(pt, n_pages, ev, n, e, b0, cnt, last_head[b], head_pt[b], carry[b],
+                             slots, wd[wave], hpg[wave], A, bad);
+  else
+    coh_wave<false, kMeasure>(pt, n_pages, ev, n, e, b0, cnt, last_head[b], head_pt[b], carry[b],
+                              slots, wd[wave], hpg[wave], A, bad);
+  const uint32_t v[10] = {A.inv, A.xfer,
+                          (uint32_t)(A.nf8 >> 0) & 0xFFu, (uint32_t)(A.nf8 >> 8) & 0xFFu,
+                          (uint32_t)(A.nf8 >> 16) & 0xFFu, (uint32_t)(A.nf8 >> 24) & 0xFFu,
+                          (uint32_t)(A.nf8 >> 32) & 0xFFu, (uint32_t)(A.nf8 >> 40) & 0xFFu,
+                          (uint32_t)(A.nf8 >> 48) & 0xFFu, (uint32_t)(A.nf8 >> 56) & 0xFFu};
+#pragma unroll
+  for (int q = 0; q < 10; ++q) {
+    const uint32_t s = wave_sum(v[q]);
+    if (lane == 0) red[wave][q] = s;
+  }
+  __syncthreads();
+  if (t < 10) partial[b * 10 + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
+}
+
 // ---------------------------------------------------------------- D: totals
 __global__ __launch_bounds__(256) void coh_reduce_kernel(const uint32_t* __restrict__ partial,
                                                          uint64_t nb,
@@ -532,6 +818,19 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------- launchers
+// Pass C variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = coh_apply_block_kernel
+// (default), 1 = coh_apply_kernel (block-wide scans, per-event page-table accesses; the round-1
+// kernel), 2 / 3 = MEASUREMENT ONLY: variant 0 without page-table stores / without any
+// page-table traffic (output invalid). Variant 0 needs 16-B aligned events, else 1 runs.
+static int g_coh_variant = getenv("GDSM_COH_VARIANT") ? atoi(getenv("GDSM_COH_VARIANT")) : 0;
+int coh_tune(const char* key, int64_t value) {
+  if (!strcmp(key, "coh_variant") && value >= 0 && value <= 3) {
+    g_coh_variant = (int)value;
+    return 0;
+  }
+  return -1;
+}
+
 static inline uint64_t coh_blocks(uint64_t n) { return (n + kCohBlock - 1) / kCohBlock; }
 static inline uint64_t coh_groups(uint64_t nb) { return (nb + kCohGroup - 1) / kCohGroup; }
 
@@ -563,6 +862,7 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* even
   uint32_t* carry = lh + nb;
   uint32_t* partial = carry + nb;
   uint32_t* groups = partial + nb * 10;
+  const uint64_t rows = nb;  // one partial row of totals per block
   {
     ProfScope ps(prof, 5, s);
     hipLaunchKernelGGL(coh_tail_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, pt,
@@ -589,18 +889,23 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* even
     }
     const unsigned g2 = (unsigned)min((uint64_t)grid, nb);
     const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
-    if (vec)
+    if (g_coh_variant != 1 && vec) {
+      auto kern = g_coh_variant == 0 ? coh_apply_block_kernel<0>
+                : g_coh_variant == 2 ? coh_apply_block_kernel<1> : coh_apply_block_kernel<2>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, pt, n_pages,
+                         events, n_events, nb, carry, lh, head_pt, partial, err);
+    } else if (vec)
       hipLaunchKernelGGL(coh_apply_kernel<true>, dim3(g2), dim3(256), 0, s, pt, n_pages, events,
                          n_events, nb, carry, lh, head_pt, partial, err);
     else
       hipLaunchKernelGGL(coh_apply_kernel<false>, dim3(g2), dim3(256), 0, s, pt, n_pages, events,
                          n_events, nb, carry, lh, head_pt, partial, err);
   }
-  uint64_t g = (nb + 255) / 256;
+  uint64_t g = (rows + 255) / 256;
   if (g > 1024) g = 1024;
   {
     ProfScope ps(prof, 8, s);
-    hipLaunchKernelGGL(coh_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, partial, nb,
+    hipLaunchKernelGGL(coh_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, partial, rows,
                        reinterpret_cast<unsigned long long*>(totals));
   }
   return hipGetLastError();

@@ -16,6 +16,7 @@ constexpr uint64_t kDiffChunk = 1ull << 20;
 uint64_t diff_workspace_bytes(uint64_t n_chunk);
 // Kernel variant knobs (see gdsm_tune); returns -1 for an unknown key.
 int tune(const char* key, int64_t value);
+int coh_tune(const char* key, int64_t value);
 
 hipError_t launch_gen_pages(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint64_t n,
                             uint64_t first_global, uint64_t stride, uint64_t seed, int mode,

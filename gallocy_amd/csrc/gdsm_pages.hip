@@ -866,7 +866,7 @@ int tune(const char* key, int64_t value) {
     g_diff_variant = (int)value;
     return 0;
   }
-  return -1;
+  return coh_tune(key, value);
 }
 
 uint64_t diff_workspace_bytes(uint64_t n_chunk) {
