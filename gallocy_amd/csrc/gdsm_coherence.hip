@@ -41,6 +41,7 @@ constexpr uint32_t kCohK = 8;                   // events per thread
 constexpr uint32_t kCohBlock = 256 * kCohK;     // events per block
 constexpr uint32_t kCohGroup = 1024;            // blocks per scan group
 constexpr uint32_t kNoHead = 0xFFFFFFFFu;
+constexpr uint64_t kNoHead64 = ~0ull;
 
 // a, then b. Branch-free: for a READ b the copyset gains R, and a CONST(EXCLUSIVE) a turns
 // SHARED (state bits 10 -> 01) when R holds a node outside its copyset.
@@ -178,9 +179,39 @@ __global__ __launch_bounds__(256) void coh_tail_kernel(const uint64_t* __restric
     acc = wave_reduce_compose(te);
     lh = (uint32_t)(wlo + hl - lo);
     hp = lane_bcast64(hp, (int)hl);
+  } else if (const uint64_t wm = __ballot(valid && (e & 1u))) {
+    // 2) no head in the tail but a write in it: the aggregate only depends on the events from
+    //    the tail's last write on. The block's last head (if any) is the first event of the
+    //    tail's page: found by sampling every 32nd event, then the 32 events before the hit.
+    const uint32_t lw = 63u - (uint32_t)__clzll(wm);
+    acc = wave_reduce_compose((valid && lane >= lw) ? ev_transform(e) : 0u);
+    const uint64_t P = ev_page(lane_bcast64(e, 63));
+    uint64_t h = kNoHead64;  // global index of the last head
+    if (hi - lo <= 64) {
+      // the whole block is the tail and holds no head
+    } else {
+      const uint64_t sidx = lo + (uint64_t)lane * 32;
+      const bool in = sidx < wlo;
+      const uint64_t sm = __ballot(in && ev_page(ev[sidx]) == P);
+      const uint32_t j0 = sm ? (uint32_t)__builtin_ctzll(sm) : (uint32_t)((wlo - lo + 31) / 32);
+      if (j0 == 0) {  // the block starts inside P's segment
+        if (lo == 0 || ev_page(ev[lo - 1]) != P) h = lo;
+      } else {
+        const uint64_t w0 = lo + (uint64_t)(j0 - 1) * 32 + 1;  // after the last sample below P
+        const uint64_t ix = w0 + lane;
+        const uint64_t hm2 = __ballot(lane < 32 && ix <= wlo && ev_page(ev[ix]) == P);
+        h = w0 + (uint64_t)__builtin_ctzll(hm2);  // hm2 != 0: ev[wlo] has page P
+      }
+    }
+    if (h != kNoHead64) {
+      lh = (uint32_t)(h - lo);
+      hp = (P < n_pages) ? pt[P] : 0ull;
+      // a head inside the block seeds the fold: CONST(page-table state) before the last write
+      // changes nothing (the write replaces it), so acc stands
+    }
   } else {
-    // 2) no head in the tail: the block is (mostly) one hot page. Fold it in 64-event steps of
-    //    coalesced loads (8 steps in flight at a time), one ordered wave reduction per step.
+    // 3) no head and no write in the tail: fold the whole block in 64-event steps of coalesced
+    //    loads (8 steps in flight at a time), one ordered wave reduction per step.
     acc = 0;
     uint64_t carry_ev = (lo > 0) ? ev[lo - 1] : 0;  // event before the current step's lane 0
     for (uint64_t j0 = lo; j0 < hi; j0 += 512) {

@@ -62,6 +62,22 @@ def test_block_boundary_alignment_and_write_mix():
             _run_both(n, [ev])
 
 
+@pytest.mark.parametrize("write_pct", [0, 3, 20, 100])
+def test_hot_page_heads_at_every_sampling_offset(write_pct):
+    """A page whose segment starts at many offsets inside a 2048-event block and runs past its
+    end: pass A finds such a block's last head by sampling every 32nd event, then the 32 before
+    the hit (tail without a head but with a write), or folds the block (no write in the tail)."""
+    offsets = [0, 1, 2, 31, 32, 33, 63, 64, 65, 1000, 1951, 1952, 1983, 1984, 1985, 2047]
+    counts = []
+    for o in offsets:
+        counts += [o, 2048 * 2 + 17, 1, 0, 2048 - (o % 7) - 1, 3]
+    n = len(counts) + 8
+    cts = np.zeros(n, np.uint64)
+    cts[:len(counts)] = counts
+    ev = oracle.gen_events(cts, seed=71 + write_pct, write_pct=write_pct)
+    _run_both(n, [ev, ev])
+
+
 def test_multi_batch_persistence_and_fewer_nodes():
     n = 3000
     rng = np.random.default_rng(8)
