@@ -548,28 +548,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
 }
 
 // One workgroup: block_off[b] = base + sum(block_sum[0..b)), base = rec_off[first].
+// Thread t owns blocks [16t, 16t + 16) (four 16-B loads), sums them, the 1024 thread sums are
+// scanned by DPP inside each wave and through LDS across the 16 waves, then every thread writes
+// its 16 offsets. Block sums are < 2^32 each, offsets are u64. nb <= 16384 (kDiffChunk / 64).
 __global__ __launch_bounds__(1024) void scan_blocks_kernel(const uint32_t* __restrict__ block_sum,
                                                            uint64_t nb,
                                                            const uint64_t* __restrict__ base_ptr,
                                                            uint64_t* __restrict__ block_off) {
-  __shared__ uint64_t part[1024];
-  const uint32_t t = threadIdx.x;
-  const uint64_t per = (nb + 1023) / 1024;
-  const uint64_t lo = min(nb, (uint64_t)t * per), hi = min(nb, lo + per);
-  uint64_t s = 0;
-  for (uint64_t b = lo; b < hi; ++b) s += block_sum[b];
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-    const uint64_t v = (t >= d) ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  __shared__ uint64_t wtot[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint64_t b0 = (uint64_t)t * 16;
+  uint32_t v[16];
+  const bool vec = (reinterpret_cast<uintptr_t>(block_sum) & 15) == 0;
+  if (vec && b0 + 16 <= nb) {
+    const uint4* src = reinterpret_cast<const uint4*>(block_sum + b0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 x = src[q];
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = (b0 + q < nb) ? block_sum[b0 + q] : 0u;
   }
-  uint64_t run = (base_ptr ? *base_ptr : 0) + part[t] - s;
-  for (uint64_t b = lo; b < hi; ++b) {
-    block_off[b] = run;
-    run += block_sum[b];
+  uint64_t s = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s += v[q];
+  // A 32-bit wave scan suffices: a wave covers 64 x 16 blocks of <= 64 records of <= 10244 B,
+  // i.e. < 6.8e8 B.
+  const uint32_t inc = wave_incl_sum((uint32_t)s);
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  uint64_t pre = base_ptr ? *base_ptr : 0;
+  for (uint32_t w = 0; w < wave; ++w) pre += wtot[w];
+  uint64_t run = pre + inc - (uint32_t)s;
+  if (b0 + 16 <= nb) {
+    uint64_t o[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      o[q] = run;
+      run += v[q];
+    }
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(block_off + b0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dst[q] = make_ulonglong2(o[2 * q], o[2 * q + 1]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (b0 + q < nb) {
+        block_off[b0 + q] = run;
+        run += v[q];
+      }
   }
 }
 
