@@ -696,30 +696,47 @@ __device__ __forceinline__ void st(T* p, T v) {
     *p = v;
 }
 
+// Payload bytes [q, q + 4) of a record (4-B aligned base `pay`), all inside the record: two
+// aligned dword loads and a funnel shift (the second load only when q is unaligned).
+template <typename P8>
+__device__ __forceinline__ uint32_t pay_dw(P8 pay, uint32_t q) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&pay[0]);
+  const uint32_t i = q >> 2, sh = (q & 3u) * 8u;
+  const uint32_t lo = w[i];
+  return sh ? __builtin_amdgcn_alignbit(w[i + 1], lo, sh) : lo;
+}
+
+// Stores the payload bytes selected by `mask` (16 bits, chunk of 16 B at dst) from pay[pp..]:
+// one 16-B store for a whole chunk, one 8-B store per whole 8-B half, else dword stores for
+// whole dwords and byte stores for the rest. kNT = nontemporal (streaming) cache policy.
 template <bool kNT, typename P8>
 __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint32_t mask, P8 pay,
                                             uint32_t pp) {
   if (mask == 0xFFFFu) {
-    uint32_t w[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      w[d] = (uint32_t)pay[pp + 4 * d] | ((uint32_t)pay[pp + 4 * d + 1] << 8) |
-             ((uint32_t)pay[pp + 4 * d + 2] << 16) | ((uint32_t)pay[pp + 4 * d + 3] << 24);
-    st<kNT>(reinterpret_cast<u32x4*>(dst), (u32x4){w[0], w[1], w[2], w[3]});
+    st<kNT>(reinterpret_cast<u32x4*>(dst), (u32x4){pay_dw(pay, pp), pay_dw(pay, pp + 4),
+                                                    pay_dw(pay, pp + 8), pay_dw(pay, pp + 12)});
     return;
   }
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t nib = (mask >> (4 * d)) & 0xFu;
-    if (nib == 0xFu) {
-      const uint32_t v = (uint32_t)pay[pp] | ((uint32_t)pay[pp + 1] << 8) |
-                         ((uint32_t)pay[pp + 2] << 16) | ((uint32_t)pay[pp + 3] << 24);
-      st<kNT>(reinterpret_cast<uint32_t*>(dst + 4 * d), v);
-      pp += 4;
-    } else if (nib) {
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t hm = (mask >> (8 * h)) & 0xFFu;
+    if (hm == 0xFFu) {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      st<kNT>(reinterpret_cast<u32x2*>(dst + 8 * h), (u32x2){pay_dw(pay, pp), pay_dw(pay, pp + 4)});
+      pp += 8;
+      continue;
+    }
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if ((nib >> k) & 1u) st<kNT>(dst + 4 * d + k, (uint8_t)pay[pp++]);
+    for (int d = 2 * h; d < 2 * h + 2; ++d) {
+      const uint32_t nib = (mask >> (4 * d)) & 0xFu;
+      if (nib == 0xFu) {
+        st<kNT>(reinterpret_cast<uint32_t*>(dst + 4 * d), pay_dw(pay, pp));
+        pp += 4;
+      } else if (nib) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((nib >> k) & 1u) st<kNT>(dst + 4 * d + k, (uint8_t)pay[pp++]);
+      }
     }
   }
 }
