@@ -589,33 +589,41 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
   const uint32_t nvalid =
       kFull ? kCohK
             : (uint32_t)min((int64_t)kCohK, max((int64_t)0, (int64_t)cnt - (int64_t)first));
-  uint32_t hib = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k)
-    if (kFull || k < nvalid) hib |= (uint32_t)(e[k] >> 36);
-  if (hib) bad = 1;
   uint32_t pprev = from_prev_lane(page32(e[kCohK - 1]));
   uint32_t pnext = from_next_lane(page32(e[0]));
   if (lane == 0 && wfirst > 0 && wfirst <= n) pprev = page32(ev[wfirst - 1]);
   if (lane == 63 && wfirst + 64 * kCohK < n) pnext = page32(ev[wfirst + 64 * kCohK]);
   const uint64_t g0 = b0 + first;  // global index of e[0]
 
-  // ---- heads and segment ends
-  uint32_t hmask = 0, emask = 0;
+  // ---- heads, segment ends and the lane aggregate (its last CONST: a write, or a head whose
+  // page-table word is fetched below), one pass over the events
+  uint32_t hmask = 0, emask = 0, hib = 0, lw = 0, ra = 0, lastc = 0;  // lastc: 0 none, 1 write, 2 head
 #pragma unroll
   for (uint32_t k = 0; k < kCohK; ++k) {
     if (kFull || k < nvalid) {
+      const uint32_t x = (uint32_t)e[k], node = (x >> 1) & 7u, bit = 1u << node;
+      hib |= (uint32_t)(e[k] >> 32);
       const uint32_t pk = page32(e[k]);
       const uint32_t pp = k ? page32(e[k > 0 ? k - 1 : 0]) : pprev;
       if ((k == 0 && g0 == 0) || pk != pp) {
         hmask |= 1u << k;
         if ((k > 0 || g0 > 0) && pk < pp) bad = 1;
         if (pk >= n_pages) bad = 1;
+        lastc = 2;
+        ra = 0;
+      }
+      if (x & 1u) {
+        lastc = 1;
+        lw = (node << 8) | bit | 0x60000u;
+        ra = 0;
+      } else {
+        ra |= bit;
       }
       const uint32_t pn = (k + 1 < kCohK) ? page32(e[k + 1 < kCohK ? k + 1 : k]) : pnext;
       if (g0 + k + 1 >= n || pn != pk) emask |= 1u << k;
     }
   }
+  if (hib >> 4) bad = 1;  // page ids are u32 (SPEC §1)
   const uint32_t hc = (uint32_t)__popc(hmask);
   const uint32_t hinc = wave_incl_sum(hc);
   const uint32_t hb0 = hinc - hc, nh = lane_bcast(hinc, 63);
@@ -643,26 +651,9 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
   }
   wave_lds_sync();
 
-  // ---- lane aggregate: CONST(last CONST word) then READ(reads since), or READ(all reads)
-  uint32_t lc = 0, ra = 0, hasc = hmask;
-  hr = hb0;
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k)
-    if (kFull || k < nvalid) {
-      const uint32_t x = (uint32_t)e[k], node = (x >> 1) & 7u, bit = 1u << node;
-      if ((hmask >> k) & 1u) {
-        lc = (uint32_t)wd[hr++];
-        ra = 0;
-      }
-      hasc |= x & 1u;
-      if (x & 1u) {
-        lc = (node << 8) | bit | 0x60000u;
-        ra = 0;
-      } else {
-        ra |= bit;
-      }
-    }
-  const uint32_t a = hasc ? tcompose(kConst | lc, ra) : ra;
+  // ---- lane aggregate CONST(last CONST) then READ(reads since), or READ(all reads); scan
+  const uint32_t lc = (lastc == 2) ? (uint32_t)wd[hinc - 1] : lw;
+  const uint32_t a = lastc ? tcompose(kConst | lc, ra) : ra;
   const uint32_t inc = wave_incl_compose_dpp(a);
   if (lane == 63) slot[wave] = inc;
   __syncthreads();
@@ -671,7 +662,8 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
   const uint32_t cur = tcompose(carry, from_prev_lane(inc));
   if (!(cur & kConst) && (hmask & 1u) == 0u && (kFull || nvalid > 0)) bad = 1;
 
-  // ---- walk: faults, invalidations, transfers; final state of each segment end
+  // ---- walk: faults, invalidations, transfers; final state of each segment end (parked in its
+  // head's slot when the head is in this wave, else stored: the wave's first segment)
   uint32_t C = cur & ~kConst, R = 0, fmask = 0, run = 0;
   hr = hb0;
 #pragma unroll
@@ -702,9 +694,9 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
         R |= bit;
       }
       if ((emask >> k) & 1u) {
-        const uint32_t pk = page32(e[k]);
         const uint32_t flip = (((C >> 16) & 3u) == 2u && (R & ~C) != 0u) ? 0x30000u : 0u;
         const uint32_t st = (C | R) ^ flip;
+        const uint32_t pk = page32(e[k]);
         if (hr > 0)
           hpg[hr - 1] = st;  // segment inside the wave: parked in its head's slot
         else if (pk < n_pages && kMeasure == 0)
@@ -758,9 +750,9 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
 }
 
 // C' kernel: one 2048-event block per workgroup, four coh_wave bodies (no persistent loop and
-// no prefetch: at 82 VGPRs five workgroups per CU hide the latency; a persistent version with
-// the next block in flight ran at 3 waves/SIMD and was 1.3x slower), totals reduced per block
-// into a partial row.
+// no prefetch: at ~90 VGPRs five workgroups per CU hide the latency; persistent versions, with
+// or without the next block in registers, were 1.2-1.3x slower), one partial row of totals per
+// wave.
 template <int kMeasure>
 __global__ __launch_bounds__(256) void coh_apply_block_kernel(
     uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
@@ -768,7 +760,6 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
     const uint64_t* __restrict__ head_pt, uint32_t* __restrict__ partial,
     uint32_t* __restrict__ err) {
   __shared__ uint32_t slots[4];
-  __shared__ uint32_t red[4][10];
   __shared__ uint64_t wd[4][kCohHeads];
   __shared__ uint32_t hpg[4][kCohHeads];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -787,18 +778,21 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
   else
     coh_wave<false, kMeasure>(pt, n_pages, ev, n, e, b0, cnt, last_head[b], head_pt[b], carry[b],
                               slots, wd[wave], hpg[wave], A, bad);
-  const uint32_t v[10] = {A.inv, A.xfer,
-                          (uint32_t)(A.nf8 >> 0) & 0xFFu, (uint32_t)(A.nf8 >> 8) & 0xFFu,
-                          (uint32_t)(A.nf8 >> 16) & 0xFFu, (uint32_t)(A.nf8 >> 24) & 0xFFu,
-                          (uint32_t)(A.nf8 >> 32) & 0xFFu, (uint32_t)(A.nf8 >> 40) & 0xFFu,
-                          (uint32_t)(A.nf8 >> 48) & 0xFFu, (uint32_t)(A.nf8 >> 56) & 0xFFu};
+  // per thread: inv <= 7 x 8, xfer <= 8, faults per node <= 8, so 16-bit fields hold a wave's
+  // sums: five packed wave sums, one partial row per wave
+  const uint32_t lo = (uint32_t)A.nf8, hi = (uint32_t)(A.nf8 >> 32);
+  const uint32_t v[5] = {A.inv | (A.xfer << 16), (lo & 0xFFu) | ((lo & 0xFF00u) << 8),
+                         ((lo >> 16) & 0xFFu) | ((lo >> 8) & 0xFF0000u),
+                         (hi & 0xFFu) | ((hi & 0xFF00u) << 8),
+                         ((hi >> 16) & 0xFFu) | ((hi >> 8) & 0xFF0000u)};
+  uint32_t mine = 0;
 #pragma unroll
-  for (int q = 0; q < 10; ++q) {
+  for (int q = 0; q < 5; ++q) {
     const uint32_t s = wave_sum(v[q]);
-    if (lane == 0) red[wave][q] = s;
+    if (lane == 2u * q) mine = s & 0xFFFFu;
+    if (lane == 2u * q + 1u) mine = s >> 16;
   }
-  __syncthreads();
-  if (t < 10) partial[b * 10 + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+  if (lane < 10) partial[(b * 4 + wave) * 10 + lane] = mine;
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
@@ -867,8 +861,9 @@ static inline uint64_t coh_groups(uint64_t nb) { return (nb + kCohGroup - 1) / k
 
 uint64_t coh_workspace_bytes(uint64_t n_events) {
   const uint64_t nb = coh_blocks(n_events);
-  // head_pt (u64) + agg, last_head, carry (u32 each) + partial rows (10 u32) + groups
-  return nb * (8 + 4 * 3 + 40) + coh_groups(nb) * 4 + 512;
+  // head_pt (u64) + agg, last_head, carry (u32 each) + partial rows (10 u32, one per wave of
+  // pass C: 4 per block) + groups
+  return nb * (8 + 4 * 3 + 4 * 40) + coh_groups(nb) * 4 + 512;
 }
 
 hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hipStream_t s) {
@@ -892,8 +887,8 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* even
   uint32_t* lh = agg + nb;
   uint32_t* carry = lh + nb;
   uint32_t* partial = carry + nb;
-  uint32_t* groups = partial + nb * 10;
-  const uint64_t rows = nb;  // one partial row of totals per block
+  uint32_t* groups = partial + nb * 40;
+  uint64_t rows = nb;  // partial rows of totals: per block (kernel 1) or per wave (kernel 0)
   {
     ProfScope ps(prof, 5, s);
     hipLaunchKernelGGL(coh_tail_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, pt,
@@ -923,8 +918,9 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* even
     if (g_coh_variant != 1 && vec) {
       auto kern = g_coh_variant == 0 ? coh_apply_block_kernel<0>
                 : g_coh_variant == 2 ? coh_apply_block_kernel<1> : coh_apply_block_kernel<2>;
-      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, pt, n_pages,
-                         events, n_events, nb, carry, lh, head_pt, partial, err);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, pt, n_pages, events,
+                         n_events, nb, carry, lh, head_pt, partial, err);
+      rows = nb * 4;
     } else if (vec)
       hipLaunchKernelGGL(coh_apply_kernel<true>, dim3(g2), dim3(256), 0, s, pt, n_pages, events,
                          n_events, nb, carry, lh, head_pt, partial, err);
