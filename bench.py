@@ -185,7 +185,7 @@ def run_coherence(args):
            "data": f"synthetic ({args.dist} page popularity, SPEC §6 events)",
            "config": {"workload": f"{n} pages, 8 nodes, {ev.count} events/batch, {args.dist}, 20% writes",
                       "touched_pages": touched},
-           "roofline": {"bound": "hbm", "kernel": "coh_apply_kernel", "achieved": round(achieved, 1),
+           "roofline": {"bound": "hbm", "kernel": "gdsm::coh_apply_block_kernel", "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "traffic": None, "algorithmic_bytes_per_launch": int(alg),
                         "avg_launch_ms": round(main_ms, 4)},
