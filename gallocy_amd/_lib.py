@@ -75,6 +75,13 @@ SIGNATURES = {
     "gdsm_nw_diff": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p), C.c_char_p,
                                C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "gdsm_set_allocator": (C.c_int, [vp, vp]),
+    "gdsm_track_begin": (C.c_int, [C.POINTER(vp), vp, C.c_uint64]),
+    "gdsm_track_dirty": (C.c_int, [vp, vp, C.c_uint64, u64p]),
+    "gdsm_track_twin": (C.c_int, [vp, C.POINTER(vp)]),
+    "gdsm_track_faults": (C.c_int, [vp, u64p]),
+    "gdsm_track_rearm": (C.c_int, [vp]),
+    "gdsm_track_end": (C.c_int, [vp]),
+    "gdsm_track_diff": (C.c_int, [vp, vp, C.POINTER(GdsmRuns), vp, u64p]),
 }
 # The legacy C++ symbol (gallocy/include/gallocy/utils/diff.h:9-11), exported unmangled-equal.
 LEGACY_DIFF_SYMBOL = "_Z4diffPKcmRPcS0_mS2_"

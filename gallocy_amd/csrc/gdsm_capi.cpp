@@ -12,6 +12,7 @@
 
 #include "gdsm.h"
 #include "gdsm_launch.h"
+#include "gdsm_track.h"
 
 struct gdsm_ctx {
   int device = 0;
@@ -37,6 +38,11 @@ struct gdsm_ctx {
   std::map<const void*, hipEvent_t> runs_busy;   // rec_off -> last async apply reading it
   gdsm::Prof prof;
   gdsm::Prof* P() { return prof.on ? &prof : nullptr; }
+  // gdsm_track_diff staging: pinned host and device, 2 x n x 4 KiB pages + n ids
+  uint8_t* track_host = nullptr;
+  uint64_t track_host_bytes = 0;
+  uint8_t* track_dev = nullptr;
+  uint64_t track_dev_bytes = 0;
 };
 
 namespace {
@@ -108,6 +114,52 @@ int check_and_clear_err(gdsm_ctx* ctx) {
 
 extern "C" {
 
+int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* ids_dev,
+                    uint64_t* n_out) {
+  if (!ctx || !t || !out || !out->rec_off || !n_out) return -EINVAL;
+  uint64_t n = 0;
+  int rc = gdsm_track_dirty(t, nullptr, 0, &n);
+  if (rc) return rc;
+  if (n && !ids_dev) return -EINVAL;
+  if (out->n_cap ? n > out->n_cap : (out->owned && n > out->n)) return -EINVAL;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  const uint64_t bytes = n * 2 * GDSM_PAGE_SZ + n * sizeof(uint32_t);
+  if (bytes > ctx->track_host_bytes) {
+    if (ctx->track_host) (void)hipHostFree(ctx->track_host);
+    ctx->track_host = nullptr;
+    ctx->track_host_bytes = 0;
+    GDSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->track_host), bytes));
+    ctx->track_host_bytes = bytes;
+  }
+  rc = ensure(&ctx->track_dev, &ctx->track_dev_bytes, bytes ? bytes : 1);
+  if (rc) return rc;
+  uint8_t* h_twin = ctx->track_host;
+  uint8_t* h_cur = h_twin + n * GDSM_PAGE_SZ;
+  uint32_t* h_ids = reinterpret_cast<uint32_t*>(h_cur + n * GDSM_PAGE_SZ);
+  uint64_t m = 0;
+  rc = gdsm::track_pack(t, h_twin, h_cur, h_ids, n, &m);
+  if (rc) return rc;
+  if (m != n) return -EINVAL;  // written concurrently: the interval is not quiescent
+  if (n) {
+    GDSM_TRY(hipMemcpyAsync(ctx->track_dev, ctx->track_host, bytes, hipMemcpyHostToDevice,
+                            ctx->stream));
+    GDSM_TRY(hipMemcpyAsync(ids_dev, ctx->track_dev + 2 * n * GDSM_PAGE_SZ, n * sizeof(uint32_t),
+                            hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
+  rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk ? chunk : 1));
+  if (rc) return rc;
+  out->n = n;
+  GDSM_TRY(gdsm::launch_diff(ctx->track_dev, ctx->track_dev + n * GDSM_PAGE_SZ, nullptr, n,
+                             out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
+                             ctx->stream, ctx->P()));
+  // the pinned staging is reused by the next call: wait for the upload now
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  *n_out = n;
+  return 0;
+}
+
 const char* gdsm_version(void) { return "gdsm 0.1.0 (gfx950)"; }
 
 int gdsm_tune(const char* key, int64_t value) {
@@ -178,6 +230,8 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->coh_ws) (void)hipFree(ctx->coh_ws);
   if (ctx->coh_pt) (void)hipFree(ctx->coh_pt);
   if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
+  if (ctx->track_dev) (void)hipFree(ctx->track_dev);
+  if (ctx->track_host) (void)hipHostFree(ctx->track_host);
   for (auto& kv : ctx->runs_busy) (void)hipEventDestroy(kv.second);
   if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
   if (ctx->ev_aux) (void)hipEventDestroy(ctx->ev_aux);

@@ -314,6 +314,71 @@ class Context:
         return ev
 
 
+class Tracker:
+    """Write-fault capture over a host region (include/gdsm.h gdsm_track_*): the region is
+    protected read-only, the first write to a page in an interval copies it to the twin and
+    lists it as dirty. `region` is an anonymous mmap (page-aligned) or any page-aligned buffer
+    exporting the buffer protocol; n_pages = len(region) // 4096."""
+
+    def __init__(self, region):
+        self._region = region
+        self._view = np.frombuffer(region, dtype=np.uint8)
+        self.n_pages = len(self._view) // PAGE_SZ
+        base = self._view.ctypes.data
+        h = C.c_void_p()
+        check(lib().gdsm_track_begin(C.byref(h), base, self.n_pages), "gdsm_track_begin")
+        self.handle = h
+        self.base = base
+
+    def pages(self) -> np.ndarray:
+        """A (n_pages, 4096) uint8 view of the tracked region (writes are tracked)."""
+        return self._view[: self.n_pages * PAGE_SZ].reshape(self.n_pages, PAGE_SZ)
+
+    def dirty(self) -> np.ndarray:
+        n = C.c_uint64(0)
+        check(lib().gdsm_track_dirty(self.handle, None, 0, C.byref(n)), "gdsm_track_dirty")
+        ids = np.empty(max(1, n.value), np.uint32)
+        check(lib().gdsm_track_dirty(self.handle, ids.ctypes.data, len(ids), C.byref(n)),
+              "gdsm_track_dirty")
+        return ids[: n.value]
+
+    def twin(self) -> np.ndarray:
+        """The twin buffer as a (n_pages, 4096) array (rows of dirty pages are valid)."""
+        ptr = C.c_void_p()
+        check(lib().gdsm_track_twin(self.handle, C.byref(ptr)), "gdsm_track_twin")
+        buf = (C.c_uint8 * (self.n_pages * PAGE_SZ)).from_address(ptr.value)
+        return np.frombuffer(buf, dtype=np.uint8).reshape(self.n_pages, PAGE_SZ)
+
+    def faults(self) -> int:
+        f = C.c_uint64(0)
+        check(lib().gdsm_track_faults(self.handle, C.byref(f)), "gdsm_track_faults")
+        return f.value
+
+    def rearm(self):
+        check(lib().gdsm_track_rearm(self.handle), "gdsm_track_rearm")
+
+    def diff(self, ctx: "Context", cap: Optional[int] = None):
+        """GPU diff of this interval's dirty pages -> (Runs, DeviceBuffer of page ids, count)."""
+        n = len(self.dirty())
+        runs = Runs(ctx, max(1, n), cap if cap is not None else max(64, n * MAX_RECORD))
+        ids = ctx.buffer(max(4, 4 * n))
+        cnt = C.c_uint64(0)
+        check(lib().gdsm_track_diff(ctx.handle, self.handle, C.byref(runs.s), ids.ptr,
+                                    C.byref(cnt)), "gdsm_track_diff")
+        return runs, ids, cnt.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            check(lib().gdsm_track_end(self.handle), "gdsm_track_end")
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 def diff(mem1: bytes, mem2: bytes):
     """The reference diff() (gallocy/utils/diff.cpp:73-167): NW alignment -> (out1, out2)."""
     L = lib()

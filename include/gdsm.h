@@ -55,7 +55,7 @@ enum gdsm_init_flags {
 };
 /* Per-kernel stages timed by gdsm_prof_* (HIP events on the context stream). */
 enum gdsm_prof_stage {
-  GDSM_PROF_DIFF = 0, /* diff_pages_kernel: the dominant kernel of the hot path */
+  GDSM_PROF_DIFF = 0, /* diff_compact_kernel: the dominant kernel of the hot path */
   GDSM_PROF_SCAN,
   GDSM_PROF_PACK,
   GDSM_PROF_APPLY,
@@ -176,6 +176,35 @@ int gdsm_nw_diff(const char* mem1, size_t mem1_len, char** out1, const char* mem
 /* Installs the allocator used for diff()/gdsm_nw_diff outputs: gallocy passes
  * internal_malloc/internal_free so callers keep freeing with internal_free. */
 int gdsm_set_allocator(void* (*alloc_fn)(size_t), void (*free_fn)(void*));
+
+/* ---- Host write-fault capture (the step before the diff). The reference
+ * describes protecting shared pages and faulting on access (resources/NUTSHELL.md:52-69,
+ * resources/IMPLEMENTATION.md:246-249) but never implements it; its only mprotect use is the
+ * thread-stack guard (gallocy/threads.cpp:53-58). A tracker protects a page-aligned host region
+ * read-only; the first write to a page in an interval is caught by a SIGSEGV handler, which
+ * copies the page to the tracker's twin and makes it writable. CPU only (no GPU needed) except
+ * gdsm_track_diff. Faults outside every tracked region go to the previously installed handler. */
+typedef struct gdsm_tracker gdsm_tracker;
+int gdsm_track_begin(gdsm_tracker** out, void* base, uint64_t n_pages);
+/* Sorted ids of the pages written since begin / the last rearm; *n_out = their count. With
+ * ids == NULL only the count is returned; -ENOSPC if cap < count. */
+int gdsm_track_dirty(gdsm_tracker* t, uint32_t* ids, uint64_t cap, uint64_t* n_out);
+/* The twin buffer (n_pages x 4 KiB; page p valid while p is dirty): p's contents before the
+ * interval's first write to it. */
+int gdsm_track_twin(gdsm_tracker* t, const void** twin);
+/* Write faults taken so far (all intervals). */
+int gdsm_track_faults(gdsm_tracker* t, uint64_t* faults);
+/* Release point: re-protects the dirty pages and empties the dirty list. No thread may write
+ * the region during the call. */
+int gdsm_track_rearm(gdsm_tracker* t);
+int gdsm_track_end(gdsm_tracker* t);
+/* Packs the dirty pages' twin and current contents, uploads them (synchronous w.r.t. the host
+ * region: it may be written again once this returns) and diffs them on the GPU into `out`, one
+ * record per dirty page in id order; ids_dev (>= count entries, device) receives the sorted ids,
+ * so gdsm_apply(ctx, GDSM_REPLICA, ids_dev, out) applies the interval to a replica indexed by
+ * page id. *n_out = count. */
+int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* ids_dev,
+                    uint64_t* n_out);
 
 const char* gdsm_version(void);
 /* Process-wide kernel-variant knobs for measurement, e.g. ("diff_variant", 0..4). */
