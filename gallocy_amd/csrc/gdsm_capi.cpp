@@ -43,6 +43,11 @@ struct gdsm_ctx {
   uint64_t track_host_bytes = 0;
   uint8_t* track_dev = nullptr;
   uint64_t track_dev_bytes = 0;
+  // gdsm_nw_diff_batch: traceback workspace; host-offloaded diff() staging (device)
+  uint8_t* nw_ws = nullptr;
+  uint64_t nw_ws_bytes = 0;
+  uint8_t* nw_stage = nullptr;
+  uint64_t nw_stage_bytes = 0;
 };
 
 namespace {
@@ -127,6 +132,8 @@ int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* id
   const uint64_t bytes = n * 2 * GDSM_PAGE_SZ + n * sizeof(uint32_t);
   if (bytes > ctx->track_host_bytes) {
     if (ctx->track_host) (void)hipHostFree(ctx->track_host);
+  if (ctx->nw_ws) (void)hipFree(ctx->nw_ws);
+  if (ctx->nw_stage) (void)hipFree(ctx->nw_stage);
     ctx->track_host = nullptr;
     ctx->track_host_bytes = 0;
     GDSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->track_host), bytes));
@@ -232,6 +239,8 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
   if (ctx->track_dev) (void)hipFree(ctx->track_dev);
   if (ctx->track_host) (void)hipHostFree(ctx->track_host);
+  if (ctx->nw_ws) (void)hipFree(ctx->nw_ws);
+  if (ctx->nw_stage) (void)hipFree(ctx->nw_stage);
   for (auto& kv : ctx->runs_busy) (void)hipEventDestroy(kv.second);
   if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
   if (ctx->ev_aux) (void)hipEventDestroy(ctx->ev_aux);
@@ -644,4 +653,74 @@ int gdsm_gen_events(gdsm_ctx* ctx, uint64_t* events, const uint64_t* offsets, ui
   return 0;
 }
 
+// ---- GPU NW (legacy diff()) ---------------------------------------------------------------
+int gdsm_nw_diff_batch(gdsm_ctx* ctx, const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
+                       const uint64_t* b_off, uint64_t n, uint32_t max_len, uint8_t* out1,
+                       uint8_t* out2, uint64_t* out_len) {
+  if (!ctx || !a_off || !b_off || (n && (!out1 || !out2 || !out_len))) return -EINVAL;
+  if (max_len > (1u << 20)) return -EINVAL;  // scores travel as 24-bit fields
+  if (!n) return 0;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  // Up to 4 GiB of traceback workspace per chunk of pairs, at least one pair.
+  const uint64_t per = gdsm::nw_pair_ws_bytes(max_len);
+  uint64_t pairs = (4ull << 30) / per;
+  if (pairs < 1) pairs = 1;
+  if (pairs > n) pairs = n;
+  int rc = ensure(&ctx->nw_ws, &ctx->nw_ws_bytes, pairs * per);
+  if (rc) return rc;
+  GDSM_TRY(gdsm::launch_nw(a, a_off, b, b_off, n, max_len, out1, out2, out_len, ctx->nw_ws,
+                           pairs * per, ctx->err, ctx->stream, ctx->P()));
+  return check_and_clear_err(ctx);
+}
+
 }  // extern "C"
+
+namespace gdsm {
+// diff() offload (legacy_diff.cpp): one pair staged through the context. `alloc` allocates the
+// two L+1-byte outputs (the installed allocator).
+int nw_host(gdsm_ctx* ctx, const char* m1, size_t n1, const char* m2, size_t n2,
+            void* (*alloc)(size_t), void (*release)(void*), char** o1, char** o2, size_t* len) {
+  if (n1 > (1u << 20) || n2 > (1u << 20)) return -EINVAL;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  auto up16 = [](uint64_t v) { return (v + 15) & ~15ull; };
+  const uint64_t out_bytes = n1 + n2 + 1;
+  const uint64_t need = up16(n1 + 1) + up16(n2 + 1) + 64 + 2 * up16(out_bytes) + 16;
+  int rc = ensure(&ctx->nw_stage, &ctx->nw_stage_bytes, need);
+  if (rc) return rc;
+  uint8_t* da = ctx->nw_stage;
+  uint8_t* db = da + up16(n1 + 1);
+  uint64_t* offs = reinterpret_cast<uint64_t*>(db + up16(n2 + 1));
+  uint8_t* d1 = reinterpret_cast<uint8_t*>(offs) + 64;
+  uint8_t* d2 = d1 + up16(out_bytes);
+  uint64_t* dlen = reinterpret_cast<uint64_t*>(d2 + up16(out_bytes));
+  const uint64_t h_off[4] = {0, n1, 0, n2};
+  if (n1) GDSM_TRY(hipMemcpyAsync(da, m1, n1, hipMemcpyHostToDevice, ctx->stream));
+  if (n2) GDSM_TRY(hipMemcpyAsync(db, m2, n2, hipMemcpyHostToDevice, ctx->stream));
+  GDSM_TRY(hipMemcpyAsync(offs, h_off, sizeof h_off, hipMemcpyHostToDevice, ctx->stream));
+  const uint32_t max_len = (uint32_t)(n1 > n2 ? n1 : n2);
+  rc = gdsm_nw_diff_batch(ctx, da, offs, db, offs + 2, 1, max_len, d1, d2, dlen);
+  if (rc) return rc;
+  uint64_t L = 0;
+  GDSM_TRY(hipMemcpy(&L, dlen, 8, hipMemcpyDeviceToHost));
+  char* a1 = static_cast<char*>(alloc(L + 1));
+  char* a2 = static_cast<char*>(alloc(L + 1));
+  if (!a1 || !a2) {
+    if (a1) release(a1);
+    if (a2) release(a2);
+    return -ENOMEM;
+  }
+  hipError_t e = hipMemcpy(a1, d1, L + 1, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(a2, d2, L + 1, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    release(a1);
+    release(a2);
+    return map_err(e);
+  }
+  *o1 = a1;
+  *o2 = a2;
+  if (len) *len = L;
+  return 0;
+}
+}  // namespace gdsm

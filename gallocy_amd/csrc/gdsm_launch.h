@@ -42,4 +42,11 @@ hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t
                              uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,
                              hipStream_t s);
 
+// GPU NW alignment (legacy diff()): workspace per pair and the fill + trace launches.
+uint64_t nw_pair_ws_bytes(uint32_t max_len);
+hipError_t launch_nw(const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
+                     const uint64_t* b_off, uint64_t n, uint32_t max_len, uint8_t* out1,
+                     uint8_t* out2, uint64_t* out_len, uint8_t* ws, uint64_t ws_bytes,
+                     uint32_t* err, hipStream_t s, Prof* prof = nullptr);
+
 }  // namespace gdsm

@@ -23,12 +23,21 @@
 
 #include "gdsm.h"
 
+namespace gdsm {
+int nw_host(gdsm_ctx* ctx, const char* m1, size_t n1, const char* m2, size_t n2,
+            void* (*alloc)(size_t), void (*release)(void*), char** o1, char** o2, size_t* len);
+}
+
 namespace {
 void* (*g_alloc)(size_t) = malloc;
 void (*g_free)(void*) = free;
+gdsm_ctx* g_dev_ctx = nullptr;    // gdsm_set_diff_device
+uint64_t g_dev_min_cells = 0;
 
 int nw_align(const char* m1, size_t n1, const char* m2, size_t n2, char** o1, char** o2,
              size_t* len) {
+  if (g_dev_ctx && (uint64_t)n1 * n2 >= g_dev_min_cells)
+    return gdsm::nw_host(g_dev_ctx, m1, n1, m2, n2, g_alloc, g_free, o1, o2, len);
   const size_t C = n2 + 1;
   std::vector<int32_t> prev(C), row(C);
   std::vector<uint8_t> dir((n1 + 1) * C);  // 1 diag, 2 left, 3 up
@@ -87,6 +96,12 @@ extern "C" int gdsm_set_allocator(void* (*alloc_fn)(size_t), void (*free_fn)(voi
   return 0;
 }
 
+extern "C" int gdsm_set_diff_device(gdsm_ctx* ctx, uint64_t min_cells) {
+  g_dev_ctx = ctx;
+  g_dev_min_cells = min_cells;
+  return 0;
+}
+
 extern "C" int gdsm_nw_diff(const char* mem1, size_t mem1_len, char** out1, const char* mem2,
                             size_t mem2_len, char** out2, size_t* len) {
   if (!out1 || !out2 || (!mem1 && mem1_len) || (!mem2 && mem2_len)) return -EINVAL;
@@ -97,8 +112,10 @@ int diff(const char* mem1, size_t mem1_len, char*& mem1_alignment, const char* m
          size_t mem2_len, char*& mem2_alignment) {
   char* a = nullptr;
   char* b = nullptr;
-  nw_align(mem1, mem1_len, mem2, mem2_len, &a, &b, nullptr);
+  // 0 like the reference; a GPU failure (gdsm_set_diff_device) leaves both outputs NULL and
+  // returns its negative errno instead of falling back.
+  const int rc = nw_align(mem1, mem1_len, mem2, mem2_len, &a, &b, nullptr);
   mem1_alignment = a;
   mem2_alignment = b;
-  return 0;
+  return rc;
 }

@@ -191,15 +191,15 @@ class Context:
         check(lib().gdsm_sync(self.handle), "gdsm_sync")
 
     PROF_STAGES = ("diff", "scan", "pack", "apply", "twin", "coh_tail", "coh_scan", "coh_apply",
-                   "coh_reduce")
+                   "coh_reduce", "nw_fill", "nw_trace")
 
     def prof_enable(self, on: bool = True):
         check(lib().gdsm_prof_enable(self.handle, int(on)), "gdsm_prof_enable")
 
     def prof_read(self) -> dict:
         """{stage: (total_ms, launches)} from HIP events on the context stream."""
-        ms = (C.c_double * 9)()
-        ln = (C.c_uint64 * 9)()
+        ms = (C.c_double * len(self.PROF_STAGES))()
+        ln = (C.c_uint64 * len(self.PROF_STAGES))()
         check(lib().gdsm_prof_read(self.handle, ms, ln), "gdsm_prof_read")
         return {k: (ms[i], ln[i]) for i, k in enumerate(self.PROF_STAGES)}
 
@@ -312,6 +312,48 @@ class Context:
         d_off.free()
         ev.count = total
         return ev
+
+    def nw_diff_batch(self, pairs: Sequence, max_len: Optional[int] = None) -> list:
+        """GPU diff() over a batch: [(mem1, mem2), ...] -> [(out1, out2), ...] (bytes), the
+        alignment of gallocy/utils/diff.cpp:73-167 for every pair (gdsm_nw_diff_batch)."""
+        n = len(pairs)
+        if n == 0:
+            return []
+        la = np.array([len(p[0]) for p in pairs], np.uint64)
+        lb = np.array([len(p[1]) for p in pairs], np.uint64)
+        a_off = np.zeros(n + 1, np.uint64)
+        b_off = np.zeros(n + 1, np.uint64)
+        np.cumsum(la, out=a_off[1:])
+        np.cumsum(lb, out=b_off[1:])
+        ml = int(max(la.max(), lb.max())) if max_len is None else int(max_len)
+        a = np.frombuffer(b"".join(bytes(p[0]) for p in pairs) or b"\0", np.uint8)
+        b = np.frombuffer(b"".join(bytes(p[1]) for p in pairs) or b"\0", np.uint8)
+        out_bytes = int(a_off[-1] + b_off[-1]) + n
+        bufs = [self.buffer(max(x.nbytes, 1)).upload(x) for x in (a, a_off, b, b_off)]
+        o1, o2, ol = self.buffer(out_bytes), self.buffer(out_bytes), self.buffer(8 * n)
+        try:
+            check(lib().gdsm_nw_diff_batch(self.handle, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr,
+                                           bufs[3].ptr, n, ml, o1.ptr, o2.ptr, ol.ptr),
+                  "gdsm_nw_diff_batch")
+            h1 = o1.download(np.uint8, out_bytes)
+            h2 = o2.download(np.uint8, out_bytes)
+            lens = ol.download(np.uint64, n)
+        finally:
+            for x in (*bufs, o1, o2, ol):
+                x.free()
+        res = []
+        for i in range(n):
+            o = int(a_off[i] + b_off[i]) + i
+            L = int(lens[i])
+            res.append((h1[o:o + L].tobytes(), h2[o:o + L].tobytes()))
+        return res
+
+
+def set_diff_device(ctx: Optional["Context"], min_cells: int = 0):
+    """Routes diff() / gdsm_nw_diff through the GPU of ctx for inputs with n*m >= min_cells
+    (None: back to the CPU path)."""
+    check(lib().gdsm_set_diff_device(ctx.handle if ctx is not None else None, int(min_cells)),
+          "gdsm_set_diff_device")
 
 
 class Tracker:

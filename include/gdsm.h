@@ -64,6 +64,8 @@ enum gdsm_prof_stage {
   GDSM_PROF_COH_SCAN,
   GDSM_PROF_COH_APPLY,
   GDSM_PROF_COH_REDUCE,
+  GDSM_PROF_NW_FILL,  /* GPU diff(): DP fill */
+  GDSM_PROF_NW_TRACE, /* GPU diff(): traceback + alignment strings */
   GDSM_PROF_STAGES
 };
 
@@ -176,6 +178,21 @@ int gdsm_nw_diff(const char* mem1, size_t mem1_len, char** out1, const char* mem
 /* Installs the allocator used for diff()/gdsm_nw_diff outputs: gallocy passes
  * internal_malloc/internal_free so callers keep freeing with internal_free. */
 int gdsm_set_allocator(void* (*alloc_fn)(size_t), void (*free_fn)(void*));
+
+/* ---- reference diff() on the GPU: batched NW alignment --------------- */
+/* Aligns n pairs (a_i, b_i) exactly like diff() / gdsm_nw_diff (same scores, tie-break and
+ * traceback, gallocy/utils/diff.cpp:73-167), on the context's GPU. Device pointers: a and b hold
+ * the concatenated inputs, a_off/b_off[n+1] their exclusive offsets; every |a_i|, |b_i| must be
+ * <= max_len (-EINVAL otherwise). Pair i's alignment (L_i bytes + NUL) is written at
+ * out1/out2 + a_off[i] + b_off[i] + i, so each output buffer needs a_off[n] + b_off[n] + n
+ * bytes; out_len[i] = L_i. Synchronises (it checks the device error word). */
+int gdsm_nw_diff_batch(gdsm_ctx* ctx, const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
+                       const uint64_t* b_off, uint64_t n, uint32_t max_len, uint8_t* out1,
+                       uint8_t* out2, uint64_t* out_len);
+/* Routes the legacy diff() symbol (and gdsm_nw_diff) through gdsm_nw_diff_batch on ctx when
+ * mem1_len * mem2_len >= min_cells; ctx == NULL restores the CPU path (the default). Outputs
+ * still come from the installed allocator. The caller keeps ctx alive while it is installed. */
+int gdsm_set_diff_device(gdsm_ctx* ctx, uint64_t min_cells);
 
 /* ---- Host write-fault capture (the step before the diff). The reference
  * describes protecting shared pages and faulting on access (resources/NUTSHELL.md:52-69,
