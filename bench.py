@@ -54,9 +54,11 @@ def parse():
                          "for N > 1 (hides the RCCL exchange), off on one GPU (HBM-bound)")
     ap.add_argument("--compare-overlap", action="store_true",
                     help="also time the other overlap mode (reported beside the measured one)")
-    ap.add_argument("--workload", choices=["pages", "coherence", "mmult"], default="pages",
+    ap.add_argument("--workload", choices=["pages", "coherence", "mmult", "nw"], default="pages",
                     help="pages: BASELINE configs[1]/[2] (the headline); coherence: configs[3]; "
-                         "mmult: configs[4] trace replay")
+                         "mmult: configs[4] trace replay; nw: the reference diff() (NW alignment) "
+                         "on the GPU over configs[0]-shaped page pairs")
+    ap.add_argument("--nw-pairs", type=int, default=512, help="nw: 4 KiB page pairs per batch")
     ap.add_argument("--ndim", type=int, default=1000, help="mmult: matrix size (<= 1021)")
     ap.add_argument("--nodes", type=int, default=4, help="mmult: simulated DSM nodes (1-8)")
     ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
@@ -240,10 +242,108 @@ def run_mmult(args):
     R.close()
 
 
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (MICROARCH)
+NW_OPS_PER_CELL = 8  # cmp, addc, max3, 2 x (sub, alignbit), add: gdsm_nw.hip fill_block
+
+
+def run_nw(args):
+    """The reference diff() (gallocy/utils/diff.cpp:73-167) on the GPU: a batch of 4 KiB page
+    pairs (twin, current with 1 % of 8-byte words rewritten: BASELINE configs[0]'s shape, which
+    the reference itself cannot align: it crashes from 1181 bytes) through gdsm_nw_diff_batch.
+    A step = one batch: DP fill + traceback + alignment strings. VALU-bound (no HBM or MFMA
+    roofline applies: 2 bits of traceback per cell are the only HBM traffic)."""
+    import torch
+
+    import gallocy_amd as ga
+    from gallocy_amd import _lib
+    torch.cuda.set_device(0)
+    n, ln = args.nw_pairs, 4096
+    rng = np.random.default_rng(args.seed)
+    a = rng.integers(0, 256, (n, ln), dtype=np.uint8)
+    b = a.copy()
+    b.reshape(n, -1, 8)[rng.random((n, ln // 8)) < 0.01] ^= 0x5A
+    off = np.arange(n + 1, dtype=np.uint64) * ln
+    ctx = ga.Context(1, arenas=())
+    da, doff, db = (ctx.buffer(x.nbytes).upload(x) for x in (a, off, b))
+    ob = 2 * n * ln + n
+    o1, o2, ol = ctx.buffer(ob), ctx.buffer(ob), ctx.buffer(8 * n)
+    L = _lib.load()
+
+    def step():
+        _lib.check(L.gdsm_nw_diff_batch(ctx.handle, da.ptr, doff.ptr, db.ptr, doff.ptr, n, ln,
+                                        o1.ptr, o2.ptr, ol.ptr), "gdsm_nw_diff_batch")
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    ctx.prof_enable(True)
+    ctx.prof_read()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    prof = ctx.prof_read()
+    cells = n * (ln + 1) ** 2
+    fill_ms = prof["nw_fill"][0] / max(1, prof["nw_fill"][1])
+    # spot check against the oracle (first pair)
+    from oracle import oracle
+    L0 = int(ol.download(np.uint64, 1)[0])
+    g1 = o1.download(np.uint8, L0)
+    want = oracle.nw_diff(a[0].tobytes(), b[0].tobytes())
+    assert g1.tobytes() == want[0], "GPU alignment differs from the oracle"
+    achieved = cells * NW_OPS_PER_CELL / (fill_ms * 1e-3) / 1e12
+    peak = VALU_PEAK_OPS / 1e12
+    stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
+              for k, v in prof.items() if v[1]}
+    res = {"metric": "NW alignment DP cells/sec (reference diff() on GPU)",
+           "value": round(cells * args.steps / dt, 1), "unit": "cells/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "i32",
+           "data": "synthetic 4 KiB page pairs, 1 % of 8-byte words rewritten",
+           "config": {"workload": f"{n} pairs x 4096 x 4096 bytes, diff() alignment",
+                      "pairs_per_s": round(n * args.steps / dt, 1)},
+           "roofline": {"bound": "valu", "kernel": "gdsm::nw_fill_kernel",
+                        "achieved": round(achieved, 2), "peak": round(peak, 1),
+                        "unit": "Tops/s", "frac": round(achieved / peak, 4), "traffic": None,
+                        "ops_per_cell": NW_OPS_PER_CELL, "cells_per_launch": cells,
+                        "avg_launch_ms": round(fill_ms, 4)},
+           "stages": stages, "cpu_baseline": None}
+    if not args.no_cpu:
+        base = {}
+        drv = oracle.REF_DRIVER
+        if drv.exists():
+            r = subprocess.run([str(drv), "time", "1024", "3"], capture_output=True, text=True,
+                               timeout=120, check=True).stdout.split()
+            s, c = float(r[0]), int(r[1])
+            base = {"value": round(c / s, 1), "unit": "cells/s", "cores": 1,
+                    "kind": "reference",
+                    "sample": "reference diff() compiled -O0 from its sources (oracle/_ref), "
+                              "1024 x 1024 bytes (its largest size before the 1181-byte crash), "
+                              f"{s:.3f} s per call"}
+        reps, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < min(args.cpu_seconds, 5.0) or reps == 0:
+            oracle.nw_diff(a[reps % n].tobytes(), b[reps % n].tobytes())
+            reps += 1
+        ct = time.perf_counter() - t1
+        port = {"value": round(reps * (ln + 1) ** 2 / ct, 1), "unit": "cells/s", "cores": 1,
+                "kind": "port", "sample": f"{reps} 4 KiB pairs through oracle or_nw_diff"}
+        res["cpu_baseline"] = base or port
+        if base:
+            res["cpu_baseline"]["oracle_port"] = port
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
     if args.workload == "coherence":
         return run_coherence(args)
+    if args.workload == "nw":
+        return run_nw(args)
     if args.workload == "mmult":
         return run_mmult(args)
     rank = int(os.environ.get("RANK", "0"))

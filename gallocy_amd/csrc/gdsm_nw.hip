@@ -48,12 +48,19 @@ __device__ __forceinline__ uint32_t pack(int32_t score, uint32_t byte) {
   return ((uint32_t)score << 8) | byte;
 }
 
+// Scores are kept minus one (H - 1): then lf and up of the recurrence are the stored values,
+// dg = stored diag + 1 + (a == b) is one add-with-carry, mx = max3(dg, lf, up), and both
+// traceback bits are sign bits shifted in by v_alignbit (nd = dg < mx, u = lf < up).
 struct Strip {
   uint32_t a[kRows];
-  int32_t left[kRows];
-  int32_t diag;
-  uint32_t pass;
+  int32_t left[kRows];  // H[y][x-1] - 1
+  int32_t diag;         // H[ytop-1][x-1] - 1
+  uint32_t pass;        // (H[ybottom][x] - 1) << 8 | b byte
 };
+
+__device__ __forceinline__ uint32_t shift_in_sign(uint32_t acc, int32_t v) {
+  return __builtin_amdgcn_alignbit(acc, (uint32_t)v, 31);  // (acc << 1) | (v < 0)
+}
 
 // One block of 16 steps [t0, t0 + 16) of a strip. fv: lanes 0..15 hold the packed words lane 0
 // consumes at steps t0..t0+15. Returns (in lanes 0..15) the packed bottom words of lane 63.
@@ -73,24 +80,20 @@ __device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t fv, uint32_t 
       act = x >= 1 && x <= (int32_t)n2;
     }
     int32_t up = up_in, dgv = st.diag;
-    uint32_t nd[kRows], uu[kRows];
+    uint32_t* acc_nd[2] = {&ndA, &ndB};
+    uint32_t* acc_u[2] = {&uA, &uB};
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
       const int32_t lf = st.left[r];
-      const int32_t d = dgv + (st.a[r] == bb ? 1 : 0);
-      const int32_t m = max(lf, up) - 1;
-      nd[r] = d < m;
-      uu[r] = up > lf;
-      const int32_t mx = max(d, m);
+      const int32_t d = dgv + 1 + (st.a[r] == bb ? 1 : 0);
+      const int32_t mx = max(max(d, lf), up);
+      *acc_nd[r >> 1] = shift_in_sign(*acc_nd[r >> 1], d - mx);
+      *acc_u[r >> 1] = shift_in_sign(*acc_u[r >> 1], lf - up);
       dgv = lf;
-      up = mx;
-      if (kMasked) st.left[r] = act ? mx : lf;
-      else st.left[r] = mx;
+      up = mx - 1;
+      if (kMasked) st.left[r] = act ? up : lf;
+      else st.left[r] = up;
     }
-    ndA = ndA + ndA + nd[0]; ndA = ndA + ndA + nd[1];
-    ndB = ndB + ndB + nd[2]; ndB = ndB + ndB + nd[3];
-    uA = uA + uA + uu[0]; uA = uA + uA + uu[1];
-    uB = uB + uB + uu[2]; uB = uB + uB + uu[3];
     if (kMasked) st.diag = act ? up_in : st.diag;
     else st.diag = up_in;
     st.pass = pack(up, bb);
@@ -142,9 +145,9 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
 #pragma unroll
           for (uint32_t r = 0; r < kRows; ++r) {
             st.a[r] = (y0 + r <= n1) ? a[ao + y0 + r - 1] : 0u;
-            st.left[r] = -(int32_t)(y0 + r);
+            st.left[r] = -(int32_t)(y0 + r) - 1;
           }
-          st.diag = -(int32_t)(y0 - 1);
+          st.diag = -(int32_t)(y0 - 1) - 1;
           st.pass = 0;
         }
         for (uint32_t bi = 0; bi < kPhase / kBlk; ++bi) {
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
           const uint32_t x = t0 + 1 + (lane & 15);
           uint32_t fv = 0;
           if (s == 0) {
-            fv = (x <= n2) ? pack(-(int32_t)x, b[bo + x - 1]) : 0u;
+            fv = (x <= n2) ? pack(-(int32_t)x - 1, b[bo + x - 1]) : 0u;
           } else if (w == 0) {
             const uint32_t* src = rb + ((g - 1) & 1) * (max_len + 64);
             fv = (x <= n2) ? __hip_atomic_load(src + x - 1, __ATOMIC_RELAXED,
