@@ -77,6 +77,10 @@ SIGNATURES = {
     "gdsm_set_allocator": (C.c_int, [vp, vp]),
     "gdsm_nw_diff_batch": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
     "gdsm_set_diff_device": (C.c_int, [vp, C.c_uint64]),
+    "gdsm_wire_size": (C.c_uint64, [C.c_uint64, C.c_uint64]),
+    "gdsm_wire_encode": (C.c_int, [vp, vp, C.POINTER(GdsmRuns), vp, C.c_uint64, u64p]),
+    "gdsm_wire_decode": (C.c_int, [vp, C.c_char_p, C.c_uint64, vp, C.POINTER(GdsmRuns), u64p]),
+    "gdsm_wire_apply": (C.c_int, [vp, C.c_int, C.c_char_p, C.c_uint64, u64p]),
     "gdsm_track_begin": (C.c_int, [C.POINTER(vp), vp, C.c_uint64]),
     "gdsm_track_dirty": (C.c_int, [vp, vp, C.c_uint64, u64p]),
     "gdsm_track_twin": (C.c_int, [vp, C.POINTER(vp)]),

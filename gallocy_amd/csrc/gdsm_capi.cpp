@@ -9,6 +9,7 @@
 #include <mutex>
 #include <new>
 #include <set>
+#include <vector>
 
 #include "gdsm.h"
 #include "gdsm_launch.h"
@@ -48,6 +49,10 @@ struct gdsm_ctx {
   uint64_t nw_ws_bytes = 0;
   uint8_t* nw_stage = nullptr;
   uint64_t nw_stage_bytes = 0;
+  // gdsm_wire_*: text + frame + checksum word
+  uint8_t* wire_ws = nullptr;
+  uint64_t wire_ws_bytes = 0;
+  uint64_t wire_hdr[4] = {};  // host staging of the frame header
 };
 
 namespace {
@@ -134,6 +139,7 @@ int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* id
     if (ctx->track_host) (void)hipHostFree(ctx->track_host);
   if (ctx->nw_ws) (void)hipFree(ctx->nw_ws);
   if (ctx->nw_stage) (void)hipFree(ctx->nw_stage);
+  if (ctx->wire_ws) (void)hipFree(ctx->wire_ws);
     ctx->track_host = nullptr;
     ctx->track_host_bytes = 0;
     GDSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->track_host), bytes));
@@ -241,6 +247,7 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->track_host) (void)hipHostFree(ctx->track_host);
   if (ctx->nw_ws) (void)hipFree(ctx->nw_ws);
   if (ctx->nw_stage) (void)hipFree(ctx->nw_stage);
+  if (ctx->wire_ws) (void)hipFree(ctx->wire_ws);
   for (auto& kv : ctx->runs_busy) (void)hipEventDestroy(kv.second);
   if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
   if (ctx->ev_aux) (void)hipEventDestroy(ctx->ev_aux);
@@ -672,6 +679,189 @@ int gdsm_nw_diff_batch(gdsm_ctx* ctx, const uint8_t* a, const uint64_t* a_off, c
   GDSM_TRY(gdsm::launch_nw(a, a_off, b, b_off, n, max_len, out1, out2, out_len, ctx->nw_ws,
                            pairs * per, ctx->err, ctx->stream, ctx->P()));
   return check_and_clear_err(ctx);
+}
+
+// ---- diff wire format (SPEC §7) -------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+constexpr char kWirePrefix[] = "GDSM1:";
+constexpr uint64_t kWirePrefixLen = 6;
+constexpr uint32_t kWireMagic = 0x4D534447u;  // "GDSM"
+
+uint64_t up16(uint64_t v) { return (v + 15) & ~15ull; }
+uint64_t ids_bytes(uint64_t n) { return 4 * ((n + 1) & ~1ull); }
+
+// Host base64 of the first 44 characters (the 32-byte header); false on a bad character.
+bool b64_head(const char* t, uint8_t* out32) {
+  uint8_t buf[33];
+  for (int q = 0; q < 11; ++q) {
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k) {
+      const unsigned char c = (unsigned char)t[4 * q + k];
+      uint32_t x;
+      if (c >= 'A' && c <= 'Z') x = c - 'A';
+      else if (c >= 'a' && c <= 'z') x = c - 'a' + 26;
+      else if (c >= '0' && c <= '9') x = c - '0' + 52;
+      else if (c == '+') x = 62;
+      else if (c == '/') x = 63;
+      else return false;
+      v = (v << 6) | x;
+    }
+    buf[3 * q] = (uint8_t)(v >> 16);
+    buf[3 * q + 1] = (uint8_t)(v >> 8);
+    buf[3 * q + 2] = (uint8_t)v;
+  }
+  memcpy(out32, buf, 32);
+  return true;
+}
+
+struct WireFrame {
+  uint64_t n = 0, D = 0, F = 0;
+  uint8_t* frame = nullptr;  // device
+  const uint32_t* ids() const { return reinterpret_cast<const uint32_t*>(frame + 32); }
+  const uint64_t* rec_off() const {
+    return reinterpret_cast<const uint64_t*>(frame + 32 + ids_bytes(n));
+  }
+  const uint8_t* data() const { return frame + 32 + ids_bytes(n) + 8 * (n + 1); }
+};
+
+// Decodes and verifies a command text into the context's wire workspace (SPEC §7 "Decode").
+int wire_decode_frame(gdsm_ctx* ctx, const char* text, uint64_t len, uint64_t n_pages,
+                      WireFrame* wf) {
+  if (!text || len < kWirePrefixLen || memcmp(text, kWirePrefix, kWirePrefixLen)) return -EINVAL;
+  const char* body = text + kWirePrefixLen;
+  const uint64_t T = len - kWirePrefixLen;
+  if (T % 4 || T < 44) return -EINVAL;
+  const uint32_t pad = body[T - 1] == '=' ? (body[T - 2] == '=' ? 2 : 1) : 0;
+  const uint64_t F = T / 4 * 3 - pad;
+  uint8_t hdr[32];
+  if (F % 8 || !b64_head(body, hdr)) return -EINVAL;
+  uint32_t magic;
+  uint16_t ver, flags;
+  uint64_t n, D, sum;
+  memcpy(&magic, hdr, 4);
+  memcpy(&ver, hdr + 4, 2);
+  memcpy(&flags, hdr + 6, 2);
+  memcpy(&n, hdr + 8, 8);
+  memcpy(&D, hdr + 16, 8);
+  memcpy(&sum, hdr + 24, 8);
+  if (magic != kWireMagic || ver != 1 || flags != 0 || D % 4 || n >= (1ull << 32) ||
+      D > F || gdsm::wire_frame_bytes(n, D) != F)
+    return -EINVAL;
+  int rc = ensure(&ctx->wire_ws, &ctx->wire_ws_bytes, up16(T) + up16(F) + 16);
+  if (rc) return rc;
+  uint8_t* dtext = ctx->wire_ws;
+  uint8_t* frame = dtext + up16(T);
+  uint64_t* dsum = reinterpret_cast<uint64_t*>(frame + up16(F));
+  GDSM_TRY(hipMemcpyAsync(dtext, body, T, hipMemcpyHostToDevice, ctx->stream));
+  GDSM_TRY(gdsm::launch_b64_decode(dtext, T, pad, frame, F, ctx->err, ctx->stream));
+  GDSM_TRY(gdsm::launch_wire_sum(frame, F, dsum, ctx->stream));
+  wf->n = n;
+  wf->D = D;
+  wf->F = F;
+  wf->frame = frame;
+  GDSM_TRY(gdsm::launch_wire_check(wf->ids(), wf->rec_off(), n, D, n_pages, ctx->err,
+                                   ctx->stream));
+  uint64_t got = 0;
+  GDSM_TRY(hipMemcpyAsync(&got, dsum, 8, hipMemcpyDeviceToHost, ctx->stream));
+  rc = check_and_clear_err(ctx);  // synchronises
+  if (rc) return rc;
+  return got == sum ? 0 : -EINVAL;
+}
+}  // namespace
+
+extern "C" {
+
+uint64_t gdsm_wire_size(uint64_t n, uint64_t data_bytes) {
+  const uint64_t F = gdsm::wire_frame_bytes(n, (data_bytes + 3) & ~3ull);
+  return kWirePrefixLen + 4 * ((F + 2) / 3);
+}
+
+int gdsm_wire_encode(gdsm_ctx* ctx, const uint32_t* ids, const gdsm_runs* runs, char* out,
+                     uint64_t cap, uint64_t* len) {
+  if (!ctx || !runs || !runs->rec_off || !len || (cap && !out)) return -EINVAL;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  const uint64_t n = runs->n;
+  uint64_t D = 0;
+  GDSM_TRY(hipMemcpyAsync(&D, runs->rec_off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  if (D % 4 || D > runs->cap) return -EINVAL;
+  const uint64_t F = gdsm::wire_frame_bytes(n, D);
+  const uint64_t T = 4 * ((F + 2) / 3);
+  *len = kWirePrefixLen + T;
+  if (cap < kWirePrefixLen + T + 1) return -ENOSPC;
+  int rc = ensure(&ctx->wire_ws, &ctx->wire_ws_bytes, up16(T) + up16(F) + 16);
+  if (rc) return rc;
+  uint8_t* dtext = ctx->wire_ws;
+  uint8_t* frame = dtext + up16(T);
+  uint64_t* dsum = reinterpret_cast<uint64_t*>(frame + up16(F));
+  const uint64_t ib = ids_bytes(n);
+  ctx->wire_hdr[0] = (uint64_t)kWireMagic | (1ull << 32);  // magic, version 1, flags 0
+  ctx->wire_hdr[1] = n;
+  ctx->wire_hdr[2] = D;
+  ctx->wire_hdr[3] = 0;
+  GDSM_TRY(hipMemcpyAsync(frame, ctx->wire_hdr, 32, hipMemcpyHostToDevice, ctx->stream));
+  if (ib) GDSM_TRY(hipMemsetAsync(frame + 32 + ib - 4, 0, 4, ctx->stream));  // odd-n padding
+  if (n && ids) {
+    GDSM_TRY(hipMemcpyAsync(frame + 32, ids, 4 * n, hipMemcpyDeviceToDevice, ctx->stream));
+  } else if (n) {
+    std::vector<uint32_t> iota(n);
+    for (uint64_t i = 0; i < n; ++i) iota[i] = (uint32_t)i;
+    GDSM_TRY(hipMemcpy(frame + 32, iota.data(), 4 * n, hipMemcpyHostToDevice));
+  }
+  uint8_t* dro = frame + 32 + ib;
+  GDSM_TRY(hipMemcpyAsync(dro, runs->rec_off, 8 * (n + 1), hipMemcpyDeviceToDevice, ctx->stream));
+  uint8_t* ddata = dro + 8 * (n + 1);
+  if (D) GDSM_TRY(hipMemcpyAsync(ddata, runs->data, D, hipMemcpyDeviceToDevice, ctx->stream));
+  if (D % 8) GDSM_TRY(hipMemsetAsync(ddata + D, 0, 4, ctx->stream));
+  GDSM_TRY(gdsm::launch_wire_sum(frame, F, dsum, ctx->stream));
+  GDSM_TRY(hipMemcpyAsync(frame + 24, dsum, 8, hipMemcpyDeviceToDevice, ctx->stream));
+  GDSM_TRY(gdsm::launch_b64_encode(frame, F, dtext, ctx->stream));
+  memcpy(out, kWirePrefix, kWirePrefixLen);
+  GDSM_TRY(hipMemcpyAsync(out + kWirePrefixLen, dtext, T, hipMemcpyDeviceToHost, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  out[kWirePrefixLen + T] = 0;
+  return 0;
+}
+
+int gdsm_wire_decode(gdsm_ctx* ctx, const char* text, uint64_t len, uint32_t* ids_out,
+                     gdsm_runs* out, uint64_t* n_out) {
+  if (!ctx || !out || !out->rec_off || !n_out) return -EINVAL;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  WireFrame wf;
+  int rc = wire_decode_frame(ctx, text, len, ~0ull, &wf);
+  if (rc) return rc;
+  const uint64_t ncap = out->n_cap ? out->n_cap : out->n;
+  if (wf.n > ncap || wf.D > out->cap) return -ENOSPC;
+  if (wf.n && !ids_out) return -EINVAL;
+  if (wf.n)
+    GDSM_TRY(hipMemcpyAsync(ids_out, wf.ids(), 4 * wf.n, hipMemcpyDeviceToDevice, ctx->stream));
+  GDSM_TRY(hipMemcpyAsync(out->rec_off, wf.rec_off(), 8 * (wf.n + 1), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  if (wf.D)
+    GDSM_TRY(hipMemcpyAsync(out->data, wf.data(), wf.D, hipMemcpyDeviceToDevice, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  out->n = wf.n;
+  *n_out = wf.n;
+  return 0;
+}
+
+int gdsm_wire_apply(gdsm_ctx* ctx, int target, const char* text, uint64_t len, uint64_t* n_out) {
+  if (!ctx || target < 0 || target > 2 || !ctx->arena[target] || !n_out) return -EINVAL;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  WireFrame wf;
+  int rc = wire_decode_frame(ctx, text, len, ctx->n_pages, &wf);
+  if (rc) return rc;
+  GDSM_TRY(gdsm::launch_apply(ctx->arena[target], wf.ids(), wf.n, wf.rec_off(), wf.data(),
+                              ctx->err, ctx->stream, ctx->P()));
+  rc = check_and_clear_err(ctx);
+  if (rc) return rc;
+  *n_out = wf.n;
+  return 0;
 }
 
 }  // extern "C"

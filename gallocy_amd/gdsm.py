@@ -348,6 +348,45 @@ class Context:
             res.append((h1[o:o + L].tobytes(), h2[o:o + L].tobytes()))
         return res
 
+    # -- diff wire format (docs/SPEC.md §7): Raft log command text
+    def wire_encode(self, runs: Runs, ids=None) -> bytes:
+        """The command text "GDSM1:" + base64(frame) of `runs` (pages `ids`, a DeviceBuffer or
+        None = 0..n-1), encoded on the GPU (gdsm_wire_encode)."""
+        need = C.c_uint64(0)
+        rc = lib().gdsm_wire_encode(self.handle, self._ptr(ids), C.byref(runs.s), None, 0,
+                                    C.byref(need))
+        if rc != -28:
+            check(rc, "gdsm_wire_encode")
+        buf = C.create_string_buffer(need.value + 1)
+        check(lib().gdsm_wire_encode(self.handle, self._ptr(ids), C.byref(runs.s), buf,
+                                     need.value + 1, C.byref(need)), "gdsm_wire_encode")
+        return buf.raw[:need.value]
+
+    def wire_decode(self, text: bytes, n_cap: int, cap: int):
+        """-> (ids DeviceBuffer, Runs) decoded and verified on the GPU (gdsm_wire_decode)."""
+        ids = self.buffer(4 * max(n_cap, 1))
+        out = Runs(self, n_cap, cap)
+        n = C.c_uint64(0)
+        try:
+            check(lib().gdsm_wire_decode(self.handle, text, len(text), ids.ptr, C.byref(out.s),
+                                         C.byref(n)), "gdsm_wire_decode")
+        except Exception:
+            ids.free()
+            out.free()
+            raise
+        return ids, out
+
+    def wire_apply(self, text: bytes, target="replica") -> int:
+        """Follower try_apply: verify the command text and apply it to `target`; -> records."""
+        n = C.c_uint64(0)
+        check(lib().gdsm_wire_apply(self.handle, _ARENA[target], text, len(text), C.byref(n)),
+              "gdsm_wire_apply")
+        return n.value
+
+
+def wire_size(n: int, data_bytes: int) -> int:
+    return lib().gdsm_wire_size(n, data_bytes)
+
 
 def set_diff_device(ctx: Optional["Context"], min_cells: int = 0):
     """Routes diff() / gdsm_nw_diff through the GPU of ctx for inputs with n*m >= min_cells

@@ -223,6 +223,30 @@ int gdsm_track_end(gdsm_tracker* t);
 int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* ids_dev,
                     uint64_t* n_out);
 
+/* ---- diff wire format (docs/SPEC.md §7): a diff stream as a Raft log command text --------
+ * The step after the diff: gallocy replicates Command{string}
+ * (gallocy/include/gallocy/consensus/log.h:18-27) inside append-entries JSON
+ * (consensus/client.cpp:133-142) and applies committed entries in try_apply
+ * (consensus/state.cpp:308-316). The text is "GDSM1:" + base64(frame): printable, no NUL, no
+ * JSON escapes. Framing, checksum and base64 run on the GPU. */
+/* Length of the command text (without its NUL) for n records carrying data_bytes. */
+uint64_t gdsm_wire_size(uint64_t n, uint64_t data_bytes);
+/* Encodes the stream `runs` of pages ids[0..runs->n) (device; NULL = pages 0..n-1) into `out`
+ * (host, cap bytes including the NUL); *len = text length. -ENOSPC (and *len = the length
+ * needed) when cap is too small. Synchronises. */
+int gdsm_wire_encode(gdsm_ctx* ctx, const uint32_t* ids, const gdsm_runs* runs, char* out,
+                     uint64_t cap, uint64_t* len);
+/* Decodes and verifies a command text (host, len bytes, no NUL needed) into device ids_out
+ * (>= n entries) and `out` (n <= out->n_cap, data <= out->cap); *n_out = n. -EINVAL for any
+ * malformed text (SPEC §7), -ENOSPC when out is too small. Synchronises. */
+int gdsm_wire_decode(gdsm_ctx* ctx, const char* text, uint64_t len, uint32_t* ids_out,
+                     gdsm_runs* out, uint64_t* n_out);
+/* Follower side of try_apply: decodes, verifies (including page ids < the arena's pages) and
+ * applies the command's records to arena `target`; nothing is applied when the text is rejected
+ * (-EINVAL); a malformed record inside a well-formed frame fails during the apply (SPEC §7).
+ * *n_out = records applied. Synchronises. */
+int gdsm_wire_apply(gdsm_ctx* ctx, int target, const char* text, uint64_t len, uint64_t* n_out);
+
 const char* gdsm_version(void);
 /* Process-wide kernel-variant knobs for measurement, e.g. ("diff_variant", 0..4). */
 int gdsm_tune(const char* key, int64_t value);
