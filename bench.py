@@ -141,6 +141,20 @@ def read_traffic(pages: int, mode: str, ppm: int):
     return None, None
 
 
+def read_coh_traffic(dist: str, pages: int, events: int):
+    """Per-launch HBM bytes of coherence pass C from the newest committed PMC summary of the same
+    batch shape (profiles/*coh_traffic*.json, scripts/coh_traffic.sh), else None."""
+    want = {"workload": "coherence", "dist": dist, "pages": pages, "events": events}
+    for p in sorted((ROOT / "profiles").glob("*coh_traffic*.json"), reverse=True):
+        try:
+            j = json.loads(p.read_text())
+        except Exception:  # noqa: BLE001
+            continue
+        if j.get("workload") == want and j.get("main_kernel_bytes_per_launch"):
+            return j["main_kernel_bytes_per_launch"], p.name
+    return None, None
+
+
 def run_coherence(args):
     """BASELINE configs[3]: batched coherence, 16M pages, 8 nodes, 1B events (Zipf 0.8 or
     uniform pages, 20 % writes), one GPU. A step = one whole batch through the page table."""
@@ -179,6 +193,7 @@ def run_coherence(args):
     main_ms = prof["coh_apply"][0] / max(1, prof["coh_apply"][1])
     alg = ev.count * 8 + touched * 16  # events read + state/faults words read and written
     achieved = alg / (main_ms * 1e-3) / 1e9
+    traffic, traffic_src = read_coh_traffic(args.dist, n, E)
     stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]} for k, v in prof.items() if v[1]}
     res = {"metric": "coherence events/sec", "value": round(ev.count * args.steps / dt, 1),
            "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -189,7 +204,8 @@ def run_coherence(args):
                       "touched_pages": touched},
            "roofline": {"bound": "hbm", "kernel": "gdsm::coh_apply_block_kernel", "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": None, "algorithmic_bytes_per_launch": int(alg),
+                        "traffic": traffic, "traffic_source": traffic_src,
+                        "algorithmic_bytes_per_launch": int(alg),
                         "avg_launch_ms": round(main_ms, 4)},
            "stages": stages,
            "last_batch_totals": {"invalidations": int(totals[0]), "transfers": int(totals[1]),
