@@ -730,6 +730,8 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
             const uint32_t fl = (uint32_t)(wd[hr - 1] >> 32) + running;
             wd[hr - 1] = (uint64_t)st | ((uint64_t)fl << 32);
             hpg[hr - 1] = pk;
+          } else {
+            hpg[hr - 1] = kSent;  // the slot holds the state word: never a page id to store to
           }
         } else if (running && pk < n_pages && kMeasure == 0) {
           atomicAdd(&pfl[2 * (uint64_t)pk], running);

@@ -102,6 +102,21 @@ def test_unsorted_batch_is_rejected():
             c.coherence_batch(np.array([99 << 4], np.uint64))  # page out of range
 
 
+def test_out_of_range_page_writes_nothing():
+    """A rejected batch whose segment lies on a page >= n_pages must not store its final state
+    anywhere: the state word it computed is not a page id (a read by node 0 ends in state 1, which
+    once landed on page 1's entry)."""
+    with ga.Context(16, arenas=()) as c:
+        c.coh_init(8)
+        st0, fl0 = c.coh_download()
+        for e in ((99 << 4), (99 << 4) | (3 << 1), (40 << 4) | 1):
+            with pytest.raises(GdsmError) as ei:
+                c.coherence_batch(np.array([e], np.uint64))
+            assert ei.value.errno == 22
+            st, fl = c.coh_download()
+            assert np.array_equal(st, st0) and np.array_equal(fl, fl0), hex(e)
+
+
 def test_device_event_generation_matches_oracle():
     n = 4000
     counts = zipf_counts(n, 60000, seed=2)
