@@ -53,6 +53,10 @@ struct gdsm_ctx {
   uint8_t* wire_ws = nullptr;
   uint64_t wire_ws_bytes = 0;
   uint64_t wire_hdr[4] = {};  // host staging of the frame header
+  // checked copies of caller page-id lists (launch_check_ids): one per stream, so an async
+  // apply's list is never overwritten by a call on the main stream
+  uint32_t* ids_safe[2] = {nullptr, nullptr};
+  uint64_t ids_safe_bytes[2] = {0, 0};
 };
 
 namespace {
@@ -112,6 +116,21 @@ int ensure(uint8_t** buf, uint64_t* have, uint64_t need) {
   return 0;
 }
 
+// A caller's device id list, checked against the arenas on stream `which` (0 main, 1 aux):
+// returns the list the kernels may use (out-of-range ids -> the guard page n_pages).
+int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const uint32_t** out) {
+  *out = ids;
+  if (!ids || n == 0) return 0;
+  uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[which]);
+  int rc = ensure(&buf, &ctx->ids_safe_bytes[which], 4 * n);
+  ctx->ids_safe[which] = reinterpret_cast<uint32_t*>(buf);
+  if (rc) return rc;
+  GDSM_TRY(gdsm::launch_check_ids(ids, n, ctx->n_pages, ctx->ids_safe[which], ctx->err,
+                                  which ? ctx->aux : ctx->stream));
+  *out = ctx->ids_safe[which];
+  return 0;
+}
+
 int check_and_clear_err(gdsm_ctx* ctx) {
   uint32_t h = 0;
   GDSM_TRY(hipMemcpyAsync(&h, ctx->err, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -137,9 +156,6 @@ int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* id
   const uint64_t bytes = n * 2 * GDSM_PAGE_SZ + n * sizeof(uint32_t);
   if (bytes > ctx->track_host_bytes) {
     if (ctx->track_host) (void)hipHostFree(ctx->track_host);
-  if (ctx->nw_ws) (void)hipFree(ctx->nw_ws);
-  if (ctx->nw_stage) (void)hipFree(ctx->nw_stage);
-  if (ctx->wire_ws) (void)hipFree(ctx->wire_ws);
     ctx->track_host = nullptr;
     ctx->track_host_bytes = 0;
     GDSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->track_host), bytes));
@@ -217,7 +233,8 @@ int gdsm_init(gdsm_ctx** out, int device, uint64_t n_pages, uint32_t flags) {
     (void)hipMemset(ctx->err, 0, 256);
     for (int a = 0; a < 3 && !rc; ++a) {
       if (!(flags & (1u << a)) || n_pages == 0) continue;
-      if (hipMalloc(reinterpret_cast<void**>(&ctx->arena[a]), n_pages * GDSM_PAGE_SZ) !=
+      // + one guard page (index n_pages): where a checked id list sends out-of-range ids
+      if (hipMalloc(reinterpret_cast<void**>(&ctx->arena[a]), (n_pages + 1) * GDSM_PAGE_SZ) !=
           hipSuccess)
         rc = -ENOMEM;
     }
@@ -248,6 +265,8 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->nw_ws) (void)hipFree(ctx->nw_ws);
   if (ctx->nw_stage) (void)hipFree(ctx->nw_stage);
   if (ctx->wire_ws) (void)hipFree(ctx->wire_ws);
+  for (auto* p : ctx->ids_safe)
+    if (p) (void)hipFree(p);
   for (auto& kv : ctx->runs_busy) (void)hipEventDestroy(kv.second);
   if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
   if (ctx->ev_aux) (void)hipEventDestroy(ctx->ev_aux);
@@ -426,6 +445,8 @@ int gdsm_twin(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n) {
   if (!ids && n > ctx->n_pages) return -EINVAL;
   CtxGuard g(ctx);
   if (g.rc) return g.rc;
+  int rc = safe_ids(ctx, ids, n, 0, &ids);
+  if (rc) return rc;
   GDSM_TRY(gdsm::launch_twin(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              ctx->stream, ctx->P()));
   return 0;
@@ -487,6 +508,7 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
   if (busy != ctx->runs_busy.end()) GDSM_TRY(hipStreamWaitEvent(ctx->stream, busy->second, 0));
   const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
   int rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk ? chunk : 1));
+  if (!rc) rc = safe_ids(ctx, ids, n, 0, &ids);
   if (rc) return rc;
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
@@ -511,6 +533,8 @@ int gdsm_apply(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_runs* 
   if (!ids && in->n > ctx->n_pages) return -EINVAL;
   CtxGuard g(ctx);
   if (g.rc) return g.rc;
+  int rc = safe_ids(ctx, ids, in->n, 0, &ids);
+  if (rc) return rc;
   GDSM_TRY(gdsm::launch_apply(ctx->arena[target], ids, in->n, in->rec_off, in->data, ctx->err,
                               ctx->stream, ctx->P()));
   return 0;
@@ -529,6 +553,8 @@ int gdsm_apply_async(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_
   if (!busy) GDSM_TRY(hipEventCreateWithFlags(&busy, hipEventDisableTiming));
   GDSM_TRY(hipEventRecord(ctx->ev_main, ctx->stream));  // after the diff that produced `in`
   GDSM_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_main, 0));
+  int rc = safe_ids(ctx, ids, in->n, 1, &ids);
+  if (rc) return rc;
   GDSM_TRY(gdsm::launch_apply(ctx->arena[target], ids, in->n, in->rec_off, in->data, ctx->err,
                               ctx->aux, ctx->P()));
   GDSM_TRY(hipEventRecord(busy, ctx->aux));

@@ -30,6 +30,10 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
 hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         const uint64_t* rec_off, const uint8_t* data, uint32_t* err,
                         hipStream_t s, Prof* prof = nullptr);
+// Caller page-id lists at the context level: safe[i] = ids[i] if < n_pages, else n_pages (the
+// arenas' guard page), and err |= 8 when any id was out of range.
+hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, uint32_t* safe,
+                            uint32_t* err, hipStream_t s);
 
 // Coherence (SPEC §5).
 uint64_t coh_workspace_bytes(uint64_t n_events);

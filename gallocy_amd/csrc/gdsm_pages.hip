@@ -83,6 +83,25 @@ __global__ __launch_bounds__(256) void twin_kernel(uint8_t* __restrict__ twin,
   }
 }
 
+// ------------------------------------------------------------------------- page-id guard
+// A context-level id list is copied with every out-of-range id replaced by n_pages, the guard
+// page every arena carries past its last page, so a bad list can never address outside the
+// arenas; the call then fails at the next gdsm_sync (err bit 8).
+__global__ __launch_bounds__(256) void check_ids_kernel(const uint32_t* __restrict__ ids,
+                                                        uint64_t n, uint64_t n_pages,
+                                                        uint32_t* __restrict__ safe,
+                                                        uint32_t* __restrict__ err) {
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = ids[i];
+    const bool ok = p < n_pages;
+    safe[i] = ok ? p : (uint32_t)n_pages;
+    bad |= !ok;
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(err, 8u);
+}
+
 // ------------------------------------------------------------------------- diff (SPEC §3)
 // Bit j of the result is set iff byte j of x is non-zero (j = 0..3).
 __device__ __forceinline__ uint32_t nz4(uint32_t x) {
@@ -937,6 +956,14 @@ hipError_t launch_gen_pages(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint6
   const uint64_t chunks = n * 256;
   hipLaunchKernelGGL(gen_pages_kernel, dim3(grid_for(chunks, 256, 65536)), dim3(256), 0, s, twin,
                      cur, replica, chunks, first_global, stride ? stride : 1, seed, mode, ppm);
+  return hipGetLastError();
+}
+
+hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, uint32_t* safe,
+                            uint32_t* err, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(check_ids_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, ids, n,
+                     n_pages, safe, err);
   return hipGetLastError();
 }
 

@@ -113,6 +113,44 @@ def test_page_id_lists_and_duplicates():
         assert np.array_equal(tw[rest], t[rest])
 
 
+def test_out_of_range_page_ids_touch_no_listed_page_and_fail():
+    """Context-level id lists are checked on the device: an id >= n_pages goes to the arenas'
+    guard page (never outside them), the valid ids are processed as usual and the next
+    gdsm_sync reports -EINVAL."""
+    n = 16
+    t, cur = oracle.gen_pages(n, seed=9, mode=0, ppm=50000)
+    ids = np.array([2, 16, 5, 0xFFFFFFFF, 7], np.uint32)
+    ok = np.array([0, 2, 4])
+    rest = np.setdiff1d(np.arange(n), ids[ok])
+    with ga.Context(n) as c:
+        c.upload("twin", t)
+        c.upload("current", cur)
+        c.upload("replica", t)
+        d_ids = c.ids(ids)
+        runs = c.diff(d_ids)
+        with pytest.raises(GdsmError) as ei:
+            c.sync()
+        assert ei.value.errno == 22
+        host = runs.to_host()
+        for i in ok:
+            assert host.record(i) == oracle.diff_pages(t[ids[i]][None], cur[ids[i]][None])[1].tobytes()
+        for apply in (c.apply, c.apply_async):
+            c.upload("replica", t)
+            apply(runs, "replica", d_ids)
+            with pytest.raises(GdsmError):
+                c.sync()
+            rep = c.download("replica")
+            assert np.array_equal(rep[ids[ok]], cur[ids[ok]])
+            assert np.array_equal(rep[rest], t[rest])
+        c.twin(d_ids)
+        with pytest.raises(GdsmError):
+            c.sync()
+        tw = c.download("twin")
+        assert np.array_equal(tw[ids[ok]], cur[ids[ok]]) and np.array_equal(tw[rest], t[rest])
+        assert np.array_equal(c.download("current"), cur)
+        c.sync()  # the error word was cleared
+
+
 def test_chunked_diff_small_workspace():
     """The diff loops over chunks when its workspace is small (raw C-ABI entry point)."""
     n = 1000
