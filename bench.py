@@ -399,9 +399,19 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # GDSM_BENCH_BACKEND=gloo: REHEARSAL ONLY of the N > 1 step (several ranks may share one GPU,
+    # the exchange goes through host memory); the line it prints is not a measurement.
+    backend = os.environ.get("GDSM_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit("GDSM_BENCH_BACKEND must be nccl or gloo")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     import gallocy_amd as ga
     from gallocy_amd import exchange
 
@@ -492,6 +502,10 @@ def main():
                                      chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes,
                                      ctx.stream)
     replica_ok = rc == 0 and chk.total() == 0 if shard is None else shard.verify()
+    if world > 1:  # every rank's home block checked, reported as one flag
+        t = torch.tensor([1 if replica_ok else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        replica_ok = bool(t.item())
 
     # The diff runs as ceil(n / 1M) chunk launches per step (kDiffChunk): bytes per launch and
     # time per launch are both taken over one chunk launch on average.
@@ -525,7 +539,9 @@ def main():
                                    f"{'8-B word' if mode == ga.GEN_UNIFORM else '64-B cluster'} writes, "
                                    f"diff+apply" + (", RCCL all-to-all exchange" if world > 1 else ""),
                        "pages_per_gpu": n, "seed": args.seed, "parallelism": f"page-shard x{world}",
-                       "diff_bytes_per_step": int(total), "payload_bytes_per_step": int(pay)},
+                       "diff_bytes_per_step": int(total), "payload_bytes_per_step": int(pay),
+                       **({"backend": "gloo (REHEARSAL, not a measurement)"}
+                          if world > 1 and backend == "gloo" else {})},
             "step_hbm_gbs": round(step_bytes * args.steps / dt / 1e9, 1),
             "pipelined": pipelined,
             ("serial_ms_per_step" if pipelined else "pipelined_ms_per_step"):
