@@ -141,3 +141,29 @@ def test_config4_scaled_parity():
     rc, otot = oracle.coherence(st, fl, host_ev)
     assert rc == 0 and tot == otot
     assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+
+
+@pytest.mark.parametrize("dist", ["uniform", "zipf"])
+def test_config4_full_size_parity(dist):
+    """BASELINE config 4 at its full size (16M pages, 8 nodes, 1B events, 20 % writes), the
+    events generated on the device as bench.py does, and the whole batch folded by the C oracle
+    on the host: page-table words, per-page faults and totals bit-exact. Also the checksum
+    property Σ per-page faults == Σ per-node faults (both start at 0)."""
+    from gallocy_amd.workloads import event_counts
+    n, total = 16 << 20, 1 << 30
+    counts = event_counts(n, total, dist=dist, seed=2026)
+    with ga.Context(n, arenas=()) as c:
+        ev = c.gen_events(counts, seed=2026)
+        c.coh_init(8)
+        tot = c.coherence_batch(ev)
+        host_ev = ev.download(np.uint64, ev.count)
+        ev.free()
+        gst, gfl = c.coh_download()
+    assert len(host_ev) == total
+    assert int(gfl.astype(np.uint64).sum()) == sum(tot["node_faults"])
+    st, fl = oracle.coh_init(n, 8)
+    rc, otot = oracle.coherence(st, fl, host_ev)
+    del host_ev
+    assert rc == 0 and tot == otot
+    assert np.array_equal(gst, st), np.flatnonzero(gst != st)[:10]
+    assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]

@@ -270,6 +270,22 @@ def test_config2_full_size_properties():
         assert c.diff(cap=1 << 20).total() == 0
 
 
+def test_config2_full_stream_bit_exact():
+    """BASELINE config 2 at full size (1M pages, 1 % word writes, the bench's seed): the whole
+    diff stream (rec_off and record bytes) equals the C oracle's over the same pages, and the
+    device-generated arenas equal the oracle's generator page for page."""
+    n = 1 << 20
+    twin, cur = oracle.gen_pages(n, seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+    oro, odata = oracle.diff_pages(twin, cur, cap=256 << 20)
+    del twin
+    with ga.Context(n) as c:
+        c.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+        h = c.diff(cap=256 << 20).to_host()
+        assert np.array_equal(c.download("current"), cur)
+    assert np.array_equal(h.rec_off, oro), np.flatnonzero(h.rec_off != oro)[:10]
+    assert len(h.data) == len(odata) and np.array_equal(h.data, odata)
+
+
 def test_config3_shard_properties():
     """BASELINE config 3 shard shape (2M pages = 16M / 8 GPUs, clustered 10 %), one GPU."""
     n = 2 << 20
@@ -293,6 +309,20 @@ def test_config3_shard_properties():
         for j, p in enumerate(ids):
             t, cur = oracle.gen_pages(1, seed=77, mode=1, ppm=100000, first_page=3 * n + int(p))
             assert h.record(j) == oracle.diff_pages(t, cur)[1].tobytes()
+
+
+def test_config3_shard_full_stream_bit_exact():
+    """BASELINE config 3 shard (2M pages of the 16M-page space, clustered 10 %): the whole diff
+    stream equals the C oracle's for the same global pages."""
+    n = 2 << 20
+    twin, cur = oracle.gen_pages(n, seed=77, mode=ga.GEN_CLUSTERED, ppm=100000, first_page=5 * n)
+    oro, odata = oracle.diff_pages(twin, cur, cap=2 << 30)
+    del twin, cur
+    with ga.Context(n) as c:
+        c.gen_pages(seed=77, mode=ga.GEN_CLUSTERED, ppm=100000, first_global=5 * n)
+        h = c.diff(cap=2 << 30).to_host()
+    assert np.array_equal(h.rec_off, oro), np.flatnonzero(h.rec_off != oro)[:10]
+    assert len(h.data) == len(odata) and np.array_equal(h.data, odata)
 
 
 def _one_record(runs, pay_fill=0xAB):
