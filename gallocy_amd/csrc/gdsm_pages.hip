@@ -670,17 +670,34 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ w
     for (uint32_t r = 0; r < kDiffPagesPerBlock; ++r)
       if (base + off[r + 1] <= cap) limit = off[r + 1];
   }
+  // kPackU dwords per thread per pass, every load issued before the first store: a typical
+  // block (64 records of ~66 B) is one pass, i.e. one memory round trip instead of four.
+  constexpr uint32_t kPackU = 8;
   uint32_t* dst = reinterpret_cast<uint32_t*>(data + base);
-  for (uint32_t g = threadIdx.x; g < limit / 4; g += 256) {
-    const uint32_t byte = g * 4;
-    uint32_t r = 0;
+  const uint32_t ndw = limit / 4;
+  for (uint32_t g0 = threadIdx.x; g0 < ndw; g0 += 256 * kPackU) {
+    uint32_t v[kPackU];
+    uint32_t live = 0;
 #pragma unroll
-    for (uint32_t step = 32; step; step >>= 1)
-      if (off[r + step] <= byte) r += step;
-    if ((sm >> r) & 1u) continue;
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(
-        ws + (b0 + (r & ~(kDiffPagesPerWave - 1))) * kRecSlot + src[r] + (byte - off[r]));
-    dst[g] = *p;
+    for (uint32_t u = 0; u < kPackU; ++u) {
+      const uint32_t g = g0 + u * 256;
+      v[u] = 0;
+      if (g < ndw) {
+        const uint32_t byte = g * 4;
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+          if (off[r + step] <= byte) r += step;
+        if (!((sm >> r) & 1u)) {
+          v[u] = *reinterpret_cast<const uint32_t*>(
+              ws + (b0 + (r & ~(kDiffPagesPerWave - 1))) * kRecSlot + src[r] + (byte - off[r]));
+          live |= 1u << u;
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPackU; ++u)
+      if ((live >> u) & 1u) dst[g0 + u * 256] = v[u];
   }
   for (uint64_t rem = sm; rem;) {  // wave-uniform
     const uint32_t r = (uint32_t)__builtin_ctzll(rem);
