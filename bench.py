@@ -559,7 +559,7 @@ def main():
             "replica_equals_current": bool(replica_ok),
             "cpu_baseline": None,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the host baseline is a 1-GPU figure (rank 0, N = 1)
             res["cpu_baseline"] = cpu_baseline(mode, ppm, args.seed, args.cpu_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
