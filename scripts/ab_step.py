@@ -11,10 +11,16 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 
+import os  # noqa: E402
+
+CLUSTERED = os.environ.get("AB_MODE") == "clustered"  # config-3 density (442 B records)
 n = 1 << 20
 ctx = ga.Context(n)
-ctx.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
-runs = ga.Runs(ctx, n, cap=n * 256)
+if CLUSTERED:
+    ctx.gen_pages(seed=77, mode=ga.GEN_CLUSTERED, ppm=100000)
+else:
+    ctx.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+runs = ga.Runs(ctx, n, cap=n * (1024 if CLUSTERED else 256))
 ctx.diff(out=runs)
 ctx.apply(runs)
 ctx.sync()
