@@ -17,8 +17,13 @@ VALUES = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0"
 ROUNDS, REPS = 6, 10
 n = 1 << 20
 ctx = ga.Context(n)
-ctx.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
-runs = ga.Runs(ctx, n, cap=n * 256)
+import os  # noqa: E402
+
+if os.environ.get("AB_MODE") == "clustered":  # config-3 density (442 B records)
+    ctx.gen_pages(seed=77, mode=ga.GEN_CLUSTERED, ppm=100000)
+else:
+    ctx.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+runs = ga.Runs(ctx, n, cap=n * 1024)
 total = None
 res = {v: [] for v in VALUES}
 for r in range(ROUNDS):
