@@ -931,12 +931,13 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
 //   4  MEASUREMENT ONLY: loads + a change count per page (the read roofline of this kernel)
 //   5  compacted, one page at a time, plain stores, 8 waves/SIMD
 //   6  MEASUREMENT ONLY: variant 0 without the record stores
+//   7  variant 0 with plain (temporal) record stores
 static int g_diff_variant = -1;
 static int diff_variant() {
   if (g_diff_variant < 0) {
     const char* e = getenv("GDSM_DIFF_VARIANT");
     g_diff_variant = e ? atoi(e) : 0;
-    if (g_diff_variant < 0 || g_diff_variant > 6) g_diff_variant = 0;
+    if (g_diff_variant < 0 || g_diff_variant > 7) g_diff_variant = 0;
   }
   return g_diff_variant;
 }
@@ -947,7 +948,7 @@ int tune(const char* key, int64_t value) {
     g_apply_variant = (int)value;
     return 0;
   }
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 6) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 7) {
     g_diff_variant = (int)value;
     return 0;
   }
@@ -1018,7 +1019,7 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
           diff_compact_kernel<true, 2, 5>, diff_pages_kernel<0>,
           diff_pages_kernel<2>,            diff_pages_kernel<3>,
           diff_pages_kernel<4>,            diff_compact_kernel<false, 0, 4>,
-          diff_compact_kernel<true, 1, 5>};
+          diff_compact_kernel<true, 1, 5>, diff_compact_kernel<true, 0, 5>};
       auto kern = kVariants[diff_variant()];
       hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids, first, m,
                          slots, sizes, block_sum);
