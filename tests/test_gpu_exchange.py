@@ -72,3 +72,28 @@ def test_shard_pipelined_run_single_rank_rccl():
             assert shard.verify()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ranks,overlap", [(2, "on"), (3, "off")])
+def test_bench_multi_rank_rehearsal_gloo(ranks, overlap):
+    """bench.py's N > 1 step end to end with `ranks` processes sharing cuda:0 and exchanging over
+    gloo (GDSM_BENCH_BACKEND=gloo, a rehearsal of the RCCL path: same Shard pipeline, barriers,
+    max-over-ranks timing): every rank's home REPLICA must equal CURRENT afterwards."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, GDSM_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ranks}", "--master-addr", "127.0.0.1", "--master-port",
+           str(_port()), str(root / "bench.py"), "--gpus", str(ranks), "--steps", "3",
+           "--warmup", "1", "--pages", str(ranks * 16384), "--no-cpu", "--overlap", overlap]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == ranks and d["replica_equals_current"] is True
+    assert d["exchange"]["received_bytes_per_step"] > 0
+    assert d["pipelined"] is (overlap == "on")
