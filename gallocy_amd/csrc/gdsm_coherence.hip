@@ -725,14 +725,13 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
       const uint32_t pk = page32(e[k]);
       if ((emask >> k) & 1u) {
         if (hr > 0) {
-          if (pk < n_pages) {
-            const uint32_t st = hpg[hr - 1];
-            const uint32_t fl = (uint32_t)(wd[hr - 1] >> 32) + running;
-            wd[hr - 1] = (uint64_t)st | ((uint64_t)fl << 32);
-            hpg[hr - 1] = pk;
-          } else {
-            hpg[hr - 1] = kSent;  // the slot holds the state word: never a page id to store to
-          }
+          // branch-free: the slot of an out-of-range page (a rejected batch) gets kSent, so the
+          // state word parked in it is never taken for a page id; its wd is never stored. (The
+          // branchy form of this guard ran pass C at 4.64 ms instead of 4.14, config 4 uniform.)
+          const uint32_t st = hpg[hr - 1];
+          const uint32_t fl = (uint32_t)(wd[hr - 1] >> 32) + running;
+          wd[hr - 1] = (uint64_t)st | ((uint64_t)fl << 32);
+          hpg[hr - 1] = pk < n_pages ? pk : kSent;
         } else if (running && pk < n_pages && kMeasure == 0) {
           atomicAdd(&pfl[2 * (uint64_t)pk], running);
         }
