@@ -11,12 +11,16 @@ import errno
 import os
 from pathlib import Path
 
-try:  # share torch's HIP runtime when torch is present
-    import torch  # noqa: F401
-except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
-    torch = None
+if os.environ.get("GDSM_NO_TORCH") != "1":  # share torch's HIP runtime when torch is present
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
+        torch = None
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libgdsm.so"
+# GDSM_LIB: another build of the same library, e.g. the host-sanitizer build
+# (gallocy_amd/lib_san/libgdsm.so, scripts/sanitize.sh).
+LIB_PATH = Path(os.environ.get("GDSM_LIB") or
+                Path(__file__).resolve().parent / "lib" / "libgdsm.so").resolve()
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)

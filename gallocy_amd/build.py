@@ -62,16 +62,57 @@ def build_lib(force: bool = False, verbose: bool = False) -> Path:
     return LIB
 
 
+SAN_DIR = PKG / "lib_san"
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-g"]
+
+
+def build_sanitized(verbose: bool = False) -> Path:
+    """Host AddressSanitizer + UBSan build of libgdsm.so (gallocy_amd/lib_san/) and of the C
+    oracle (oracle/_san/liboracle.so), both with the clang that hipcc drives, so one runtime
+    (libclang_rt.asan) serves the process. The device code is compiled as usual (GPU sanitizers
+    are not used). Run the CPU tests against it with scripts/sanitize.sh."""
+    SAN_DIR.mkdir(exist_ok=True)
+    objs = []
+    for s in SOURCES:
+        obj = SAN_DIR / (Path(s).stem + ".o")
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O1", "-fPIC", "-std=c++17", *SAN_FLAGS,
+               "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s), "-o", str(obj)]
+        if s.endswith(".cpp"):
+            cmd[1:1] = ["-x", "hip"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(str(obj))
+    lib = SAN_DIR / "libgdsm.so"
+    subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC",
+                    "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+                    "-shared-libsan", "-o", str(lib), *objs], check=True)
+    clang = Path(_hipcc()).resolve().parent.parent / "lib" / "llvm" / "bin" / "clang"
+    if not clang.exists():
+        clang = Path("/opt/rocm/lib/llvm/bin/clang")
+    (ROOT / "oracle" / "_san").mkdir(exist_ok=True)
+    subprocess.run([str(clang), "-std=c99", "-O1", "-g", "-fPIC", "-shared", "-Wall",
+                    "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                    "-shared-libsan", "-fno-omit-frame-pointer",
+                    "-o", str(ROOT / "oracle" / "_san" / "liboracle.so"),
+                    str(ROOT / "oracle" / "gdsm_oracle.c")], check=True)
+    return lib
+
+
 def build_oracle(verbose: bool = False) -> None:
     """Test oracle (oracle/liboracle.so) and, when the reference tree exists, oracle/_ref."""
     targets = ["oracle"]
     if Path("/root/reference/gallocy/utils/diff.cpp").exists():
-        targets.append("ref")
+        targets += ["ref", "caller"]
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), *targets], check=True,
                    stdout=None if verbose else subprocess.DEVNULL)
 
 
 if __name__ == "__main__":
+    if "--sanitize" in sys.argv:
+        print(build_sanitized(verbose=True))
+        sys.exit(0)
     build_lib(force="--force" in sys.argv, verbose=True)
     build_oracle(verbose=True)
     print(LIB)

@@ -829,14 +829,12 @@ int gdsm_wire_encode(gdsm_ctx* ctx, const uint32_t* ids, const gdsm_runs* runs, 
   ctx->wire_hdr[2] = D;
   ctx->wire_hdr[3] = 0;
   GDSM_TRY(hipMemcpyAsync(frame, ctx->wire_hdr, 32, hipMemcpyHostToDevice, ctx->stream));
-  if (ib) GDSM_TRY(hipMemsetAsync(frame + 32 + ib - 4, 0, 4, ctx->stream));  // odd-n padding
-  if (n && ids) {
+  if (n & 1) GDSM_TRY(hipMemsetAsync(frame + 32 + ib - 4, 0, 4, ctx->stream));  // odd-n padding
+  // Every frame write is ordered on ctx->stream (the identity list is filled on the device).
+  if (n && ids)
     GDSM_TRY(hipMemcpyAsync(frame + 32, ids, 4 * n, hipMemcpyDeviceToDevice, ctx->stream));
-  } else if (n) {
-    std::vector<uint32_t> iota(n);
-    for (uint64_t i = 0; i < n; ++i) iota[i] = (uint32_t)i;
-    GDSM_TRY(hipMemcpy(frame + 32, iota.data(), 4 * n, hipMemcpyHostToDevice));
-  }
+  else if (n)
+    GDSM_TRY(gdsm::launch_iota(reinterpret_cast<uint32_t*>(frame + 32), n, ctx->stream));
   uint8_t* dro = frame + 32 + ib;
   GDSM_TRY(hipMemcpyAsync(dro, runs->rec_off, 8 * (n + 1), hipMemcpyDeviceToDevice, ctx->stream));
   uint8_t* ddata = dro + 8 * (n + 1);

@@ -56,6 +56,8 @@ hipError_t launch_nw(const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
 // Diff wire format (SPEC §7).
 uint64_t wire_frame_bytes(uint64_t n, uint64_t data_bytes);
 hipError_t launch_wire_sum(const uint8_t* frame, uint64_t F, uint64_t* sum, hipStream_t s);
+// dst[i] = i for i < n (identity page-id lists on the device).
+hipError_t launch_iota(uint32_t* dst, uint64_t n, hipStream_t s);
 hipError_t launch_b64_encode(const uint8_t* frame, uint64_t F, uint8_t* text, hipStream_t s);
 hipError_t launch_b64_decode(const uint8_t* text, uint64_t T, uint32_t pad, uint8_t* frame,
                              uint64_t F, uint32_t* err, hipStream_t s);

@@ -20,13 +20,19 @@
 //
 // Per page state (atomic u8): 0 clean and protected, 1 being captured, 2 dirty and writable.
 // Concurrent first writes to one page: one thread captures, the others wait for state 2.
-// The handler only does memcpy, mprotect and atomics.
+// The handler only does memcpy, mprotect and atomics. Only write faults are claimed (x86-64:
+// the page-fault error code's W bit); any other fault, e.g. an instruction fetch from a tracked
+// PROT_READ page, goes to the previous handler. gdsm_track_end unpublishes the tracker and then
+// waits until no handler is in flight (g_inflight) before freeing it, so a handler that loaded
+// the tracker just before never touches freed memory.
 #include <errno.h>
 #include <signal.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
 #include <sys/mman.h>
+#include <ucontext.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -51,6 +57,7 @@ namespace {
 
 constexpr int kMaxTrackers = 64;
 std::atomic<gdsm_tracker*> g_trackers[kMaxTrackers];
+std::atomic<int> g_inflight{0};  // SIGSEGV handlers currently inside the tracker scan
 std::mutex g_install_mu;
 struct sigaction g_prev;
 bool g_installed = false;
@@ -74,11 +81,29 @@ bool capture(gdsm_tracker* t, uintptr_t addr) {
   return true;
 }
 
+// True when the fault was a data write (only those are the tracker's: tracked pages are
+// always readable).
+bool is_write_fault(void* uctx) {
+#if defined(__x86_64__)
+  const ucontext_t* uc = static_cast<const ucontext_t*>(uctx);
+  return (uc->uc_mcontext.gregs[REG_ERR] & 0x2) != 0;
+#else
+  (void)uctx;
+  return true;
+#endif
+}
+
 void on_segv(int sig, siginfo_t* si, void* uctx) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(si->si_addr);
-  for (int i = 0; i < kMaxTrackers; ++i) {
-    gdsm_tracker* t = g_trackers[i].load(std::memory_order_acquire);
-    if (t && capture(t, addr)) return;
+  if (is_write_fault(uctx)) {
+    g_inflight.fetch_add(1, std::memory_order_seq_cst);
+    bool mine = false;
+    for (int i = 0; i < kMaxTrackers && !mine; ++i) {
+      gdsm_tracker* t = g_trackers[i].load(std::memory_order_seq_cst);
+      mine = t && capture(t, addr);
+    }
+    g_inflight.fetch_sub(1, std::memory_order_seq_cst);
+    if (mine) return;
   }
   // Not ours: hand the fault to the handler that was installed before us.
   if (g_prev.sa_flags & SA_SIGINFO) {
@@ -210,8 +235,11 @@ int gdsm_track_end(gdsm_tracker* t) {
   if (!t) return -EINVAL;
   for (int i = 0; i < kMaxTrackers; ++i) {
     gdsm_tracker* self = t;
-    g_trackers[i].compare_exchange_strong(self, nullptr);
+    g_trackers[i].compare_exchange_strong(self, nullptr, std::memory_order_seq_cst);
   }
+  // Quiesce: a handler that loaded `t` before it was unpublished incremented g_inflight first
+  // (both seq_cst), so it is seen here; wait for it to leave before freeing the tracker.
+  while (g_inflight.load(std::memory_order_seq_cst) != 0) sched_yield();
   const int rc = mprotect(t->base, t->n_pages * GDSM_PAGE_SZ, PROT_READ | PROT_WRITE) ? -errno : 0;
   destroy(t);
   return rc;

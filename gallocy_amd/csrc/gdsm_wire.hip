@@ -132,6 +132,11 @@ __global__ __launch_bounds__(256) void wire_check_kernel(const uint32_t* __restr
   if (bad) atomicOr(err, 16u);
 }
 
+__global__ __launch_bounds__(256) void iota_kernel(uint32_t* __restrict__ dst, uint64_t n) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    dst[i] = (uint32_t)i;
+}
+
 uint32_t grid(uint64_t threads) {
   const uint64_t b = (threads + 255) / 256;
   return (uint32_t)(b ? (b < (1u << 30) ? b : (1u << 30)) : 1);
@@ -150,6 +155,13 @@ hipError_t launch_wire_sum(const uint8_t* frame, uint64_t F, uint64_t* sum, hipS
   const uint32_t blocks = grid(nw) < 4096 ? grid(nw) : 4096;
   hipLaunchKernelGGL(wire_sum_kernel, dim3(blocks), dim3(256), 0, s,
                      reinterpret_cast<const uint64_t*>(frame), nw, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_iota(uint32_t* dst, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t blocks = grid(n) < 4096 ? grid(n) : 4096;
+  hipLaunchKernelGGL(iota_kernel, dim3(blocks), dim3(256), 0, s, dst, n);
   return hipGetLastError();
 }
 

@@ -19,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "gdsm.h"
@@ -33,11 +34,17 @@ void* (*g_alloc)(size_t) = malloc;
 void (*g_free)(void*) = free;
 gdsm_ctx* g_dev_ctx = nullptr;    // gdsm_set_diff_device
 uint64_t g_dev_min_cells = 0;
+// The offload path stages through one context (its stream, staging buffers and error word):
+// concurrent diff() calls are serialised there. The CPU path is reentrant like the reference's
+// (every call allocates its own DP rows).
+std::mutex g_dev_mu;
 
 int nw_align(const char* m1, size_t n1, const char* m2, size_t n2, char** o1, char** o2,
              size_t* len) {
-  if (g_dev_ctx && (uint64_t)n1 * n2 >= g_dev_min_cells)
+  if (g_dev_ctx && (uint64_t)n1 * n2 >= g_dev_min_cells) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
     return gdsm::nw_host(g_dev_ctx, m1, n1, m2, n2, g_alloc, g_free, o1, o2, len);
+  }
   const size_t C = n2 + 1;
   std::vector<int32_t> prev(C), row(C);
   std::vector<uint8_t> dir((n1 + 1) * C);  // 1 diag, 2 left, 3 up

@@ -191,7 +191,9 @@ int gdsm_nw_diff_batch(gdsm_ctx* ctx, const uint8_t* a, const uint64_t* a_off, c
                        uint8_t* out2, uint64_t* out_len);
 /* Routes the legacy diff() symbol (and gdsm_nw_diff) through gdsm_nw_diff_batch on ctx when
  * mem1_len * mem2_len >= min_cells; ctx == NULL restores the CPU path (the default). Outputs
- * still come from the installed allocator. The caller keeps ctx alive while it is installed. */
+ * still come from the installed allocator. The caller keeps ctx alive while it is installed and
+ * does not use it for other work meanwhile: offloaded calls stage through its stream and buffers
+ * (concurrent diff() calls are serialised on an internal lock; the CPU path stays reentrant). */
 int gdsm_set_diff_device(gdsm_ctx* ctx, uint64_t min_cells);
 
 /* ---- Host write-fault capture (the step before the diff). The reference
@@ -214,6 +216,8 @@ int gdsm_track_faults(gdsm_tracker* t, uint64_t* faults);
 /* Release point: re-protects the dirty pages and empties the dirty list. No thread may write
  * the region during the call. */
 int gdsm_track_rearm(gdsm_tracker* t);
+/* Unprotects the region and frees the tracker once no fault handler is still inside it. Only
+ * write faults are claimed by a tracker; any other fault goes to the previous handler. */
 int gdsm_track_end(gdsm_tracker* t);
 /* Packs the dirty pages' twin and current contents, uploads them (synchronous w.r.t. the host
  * region: it may be written again once this returns) and diffs them on the GPU into `out`, one

@@ -3,13 +3,14 @@ tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the pr
 from __future__ import annotations
 
 import ctypes as C
+import os
 import subprocess
 from pathlib import Path
 
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB = HERE / "liboracle.so"
+LIB = Path(os.environ.get("GDSM_ORACLE_LIB") or HERE / "liboracle.so")
 REF_DRIVER = HERE / "_ref" / "ref_nw_driver"
 _lib = None
 

@@ -9,6 +9,14 @@
   pages.npz      page diff vectors from the C oracle (docs/SPEC.md §3): edge-case pages and
                  seeded synthetic pages with their expected rec_off/data. PARITY UNPINNED by the
                  reference (it has no page diff); these pin the oracle against drift.
+  c1_windows.npz BASELINE config 1 (64 x 4 KiB pages, SPEC §6 seed 1, 1 % word writes) cut into
+                 256 windows of 1024 B (test/test_diff.cpp:38-57 shape, under the reference's
+                 1180-B limit) after the byte remap tests/helpers.py:c1_remap (no NUL, no '-': the reference
+                 returns NUL-terminated alignments with '-' gaps and no length, diff.h:9-11),
+                 each window pair run through the REFERENCE diff() (oracle/_ref). Stored: the
+                 alignment length, crc32 of both alignment strings, and the positions where
+                 out1[i] != out2[i] (bit-packed). This pins the page diff / apply to the
+                 reference itself wherever its alignment is gap-free.
   coherence.npz  a seeded event batch and its expected page table / totals from the C oracle
                  (SPEC §5, parity unpinned by the reference, which has no coherence logic).
 """
@@ -22,6 +30,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 from oracle import oracle  # noqa: E402
+from tests.helpers import c1_windows  # noqa: E402
 
 OUT = Path(__file__).resolve().parent
 
@@ -122,6 +131,25 @@ def make_pages():
     print("pages.npz", twin.shape[0], "edge pages;", int(ro2[-1]), "B for config 1")
 
 
+def make_c1_windows():
+    import zlib
+    t, c = c1_windows()
+    tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+    cases = [(tw[i].tobytes(), cw[i].tobytes()) for i in range(len(tw))]
+    outs = oracle.ref_nw_batch(cases)
+    L = np.array([len(o1) for o1, _ in outs], np.int64)
+    crc = np.array([[zlib.crc32(o1), zlib.crc32(o2)] for o1, o2 in outs], np.uint32)
+    mask = np.zeros((len(cases), 128), np.uint8)
+    gapfree = np.zeros(len(cases), bool)
+    for i, (o1, o2) in enumerate(outs):
+        if len(o1) == 1024 and b"-" not in o1 + o2:
+            gapfree[i] = True
+            a, b = np.frombuffer(o1, np.uint8), np.frombuffer(o2, np.uint8)
+            mask[i] = np.packbits(a != b)
+    np.savez_compressed(OUT / "c1_windows.npz", L=L, crc=crc, gapfree=gapfree, mask=mask)
+    print("c1_windows.npz", len(cases), "windows,", int(gapfree.sum()), "gap-free")
+
+
 def make_coherence():
     rng = np.random.default_rng(11)
     n_pages = 64
@@ -140,6 +168,7 @@ def make_coherence():
 if __name__ == "__main__":
     if not oracle.ref_available():
         raise SystemExit("oracle/_ref/ref_nw_driver missing: run `make -C oracle ref` here first")
-    make_nw()
-    make_pages()
-    make_coherence()
+    which = sys.argv[1:] or ["nw", "pages", "coherence", "c1_windows"]
+    for w in which:
+        {"nw": make_nw, "pages": make_pages, "coherence": make_coherence,
+         "c1_windows": make_c1_windows}[w]()

@@ -31,6 +31,45 @@ def np_diff(twin, cur, ids=None):
     return off, np.frombuffer(b"".join(recs), np.uint8)
 
 
+C1_NUL, C1_DASH = 0xFE, 0xFD  # replacement bytes for 0x00 and '-' (0x2D)
+
+
+def c1_remap(pages: np.ndarray) -> np.ndarray:
+    """The byte remap of the config-1 windows (tests/golden/c1_windows.npz): 0x00 -> 0xFE,
+    '-' -> 0xFD, others unchanged, so the reference diff(), which returns NUL-terminated
+    alignments with '-' gaps (gallocy/utils/diff.h:9-11), can take the bytes. Applied to TWIN and
+    CURRENT alike; the remapped pages are the inputs of every side of the comparison."""
+    out = pages.copy()
+    out[pages == 0] = C1_NUL
+    out[pages == 0x2D] = C1_DASH
+    return out
+
+
+def c1_windows():
+    """Remapped BASELINE config-1 pages (64 x 4 KiB, SPEC §6 seed 1, 1 % word writes):
+    (twin', cur'), each (64, 4096) uint8; window w = bytes [1024 w, 1024 w + 1024) of the flat
+    arrays."""
+    from oracle import oracle
+    t, c = oracle.gen_pages(64, seed=1, mode=0, ppm=10000)
+    return c1_remap(t), c1_remap(c)
+
+
+def runs_positions(rec_off, data, n_pages: int) -> np.ndarray:
+    """bool[n_pages * 4096]: True at every byte covered by a run of the stream (SPEC §3),
+    record i describing page i."""
+    out = np.zeros(n_pages * 4096, bool)
+    w = np.frombuffer(np.ascontiguousarray(data).tobytes() + b"\0" * 4, "<u4")
+    for i in range(n_pages):
+        a, b = int(rec_off[i]), int(rec_off[i + 1])
+        if a == b:
+            continue
+        nr = int(w[a // 4])
+        for h in w[a // 4 + 1:a // 4 + 1 + nr]:
+            o, ln = int(h & 0xFFFF), int(h >> 16)
+            out[i * 4096 + o:i * 4096 + o + ln] = True
+    return out
+
+
 def mix64(z):
     M = (1 << 64) - 1
     z ^= z >> 30

@@ -97,3 +97,18 @@ def test_workspace_sizing():
     lib = _lib.load()
     assert lib.gdsm_diff_workspace_bytes(1) >= 10244
     assert lib.gdsm_diff_workspace_bytes(1 << 24) == lib.gdsm_diff_workspace_bytes(1 << 20)
+
+
+CALLER = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "legacy_caller"
+
+
+@pytest.mark.skipif(not CALLER.exists(), reason="oracle/_ref/legacy_caller not built (no reference tree)")
+def test_legacy_caller_on_gallocy_internal_heap():
+    """A compiled C++ caller (oracle/legacy_caller.cpp, linked with the reference's own
+    allocators/internal.cpp + utils/constants.cpp) installs internal_malloc / internal_free via
+    gdsm_set_allocator, replays the three test/test_diff.cpp bodies through libgdsm's diff()
+    symbol, checks every output lies in the internal heap's zone, and frees it with
+    internal_free (gallocy/utils/diff.cpp:135-136, allocators/internal.cpp:31-57)."""
+    r = subprocess.run([str(CALLER)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("ok ")

@@ -9,7 +9,7 @@ import gallocy_amd as ga
 from gallocy_amd import _lib
 from gallocy_amd.gdsm import GdsmError, HostRuns, Runs
 from oracle import oracle
-from tests.helpers import np_diff
+from tests.helpers import c1_windows, np_diff, runs_positions
 
 pytestmark = pytest.mark.gpu
 
@@ -286,6 +286,47 @@ def test_config2_full_stream_bit_exact():
     assert len(h.data) == len(odata) and np.array_equal(h.data, odata)
 
 
+def test_north_star_16M_pages_1pct():
+    """The north-star size on one GPU: 16M x 4 KiB pages (3 arenas = 192 GiB of HBM), 1 % random
+    word writes. Sampled records of the full stream equal the oracle's for the same pages; record
+    sizes are sane everywhere; apply makes REPLICA == CURRENT (the diff of the two is empty),
+    a second apply changes nothing, and twin() empties the diff."""
+    n = 16 << 20
+    L = _lib.load()
+    with ga.Context(n) as c:
+        c.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+        runs = c.diff(cap=2 << 30)
+        total = runs.total()
+        assert 50 * n < total < 72 * n
+        ro = np.empty(n + 1, np.uint64)
+        assert L.gdsm_memcpy_d2h(c.handle, ro.ctypes.data, runs.s.rec_off, ro.nbytes) == 0
+        sizes = np.diff(ro.astype(np.int64))
+        assert ro[0] == 0 and ro[-1] == total and (sizes >= 0).all() and (sizes % 4 == 0).all()
+        assert abs((sizes > 0).mean() - (1 - 0.99 ** 512)) < 0.001
+        rng = np.random.default_rng(16)
+        sample = np.concatenate([[0, n - 1], rng.choice(n, 254, replace=False)])
+        for p in sample.tolist():
+            a, b = int(ro[p]), int(ro[p + 1])
+            got = np.empty(max(1, b - a), np.uint8)
+            if b > a:
+                assert L.gdsm_memcpy_d2h(c.handle, got.ctypes.data, runs.s.data + a, b - a) == 0
+            t, cur = oracle.gen_pages(1, seed=2026, mode=0, ppm=10000, first_page=p)
+            assert got[:b - a].tobytes() == oracle.diff_pages(t, cur)[1].tobytes(), p
+        c.apply(runs)
+        c.apply(runs)
+        c.sync()
+        runs.free()
+        chk = ga.Runs(c, n, cap=1 << 20)
+        ws = c.buffer(L.gdsm_diff_workspace_bytes(n))
+        assert L.gdsm_diff_raw(c.arena_ptr("replica"), c.arena_ptr("current"), None, n,
+                               chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes,
+                               c.stream) == 0
+        assert chk.total() == 0
+        ws.free()
+        c.twin()
+        assert c.diff(out=chk).total() == 0
+
+
 def test_config3_shard_properties():
     """BASELINE config 3 shard shape (2M pages = 16M / 8 GPUs, clustered 10 %), one GPU."""
     n = 2 << 20
@@ -477,3 +518,30 @@ def test_diff_variants_bit_exact(variant, golden):
                 _eq_runs(c.diff(cap=max(64, int(ro[-1]))).to_host(), ro, data)
     finally:
         L.gdsm_tune(b"diff_variant", 0)
+
+
+def test_c1_windows_pinned_by_reference_diff(golden):
+    """BASELINE config 1 pinned to the REFERENCE diff() (gallocy/utils/diff.cpp:73-167): the
+    remapped config-1 pages, cut into 1024-B windows, were aligned by oracle/_ref (fixture
+    tests/golden/c1_windows.npz, every alignment gap-free). On the GPU, per window:
+    {i : out1[i] != out2[i]} equals the union of gdsm_diff's runs, and gdsm_apply of the stream
+    to the twin gives out2 (whose crc32 the fixture holds)."""
+    import zlib
+    g = golden["c1_windows"]
+    t, cur = c1_windows()
+    assert g["gapfree"].all()
+    ref = np.unpackbits(g["mask"], axis=1).astype(bool)
+    with ga.Context(64) as c:
+        c.upload("twin", t)
+        c.upload("current", cur)
+        c.upload("replica", t)
+        runs = c.diff()
+        h = runs.to_host()
+        pos = runs_positions(h.rec_off, h.data, 64).reshape(-1, 1024)
+        bad = np.flatnonzero((pos != ref).any(axis=1))
+        assert len(bad) == 0, f"windows whose runs differ from the reference alignment: {bad[:8]}"
+        c.apply(runs)
+        c.sync()
+        rep = c.download("replica").reshape(-1, 1024)
+    for w in range(len(rep)):
+        assert zlib.crc32(rep[w].tobytes()) == int(g["crc"][w][1]), w

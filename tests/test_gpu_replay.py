@@ -10,8 +10,11 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("ndim,nodes", [(64, 1), (64, 2), (96, 4), (64, 8), (257, 3)])
+@pytest.mark.parametrize("ndim,nodes", [(64, 1), (64, 2), (96, 4), (64, 8), (257, 3),
+                                        (1000, 1), (1000, 2), (1000, 4), (1000, 8)])
 def test_mmult_replay_end_to_end(ndim, nodes):
+    """NDIM = 1000 is BASELINE config 5's size (test/test_mmult.cpp:103-180 uses
+    NDIM up to 1021 before the reference heap aborts)."""
     R = MmultReplay(ndim=ndim, nodes=nodes, seed=7)
     try:
         R.run()

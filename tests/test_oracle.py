@@ -10,7 +10,8 @@ import numpy as np
 import pytest
 
 from oracle import oracle
-from tests.helpers import hash3, np_diff, np_runs, py_coherence, zipf_counts
+from tests.helpers import (c1_windows, hash3, np_diff, np_runs, py_coherence, runs_positions,
+                           zipf_counts)
 
 
 # ---------------------------------------------------------------- NW (reference diff())
@@ -191,3 +192,31 @@ def test_gen_events_and_zipf_counts():
     pages = ev >> 4
     assert np.all(np.diff(pages.astype(np.int64)) >= 0)
     assert abs((ev & 1).mean() - 0.2) < 0.02
+
+
+# ---------------------------------------------------------------- config 1 pinned by the reference
+def test_c1_windows_pinned_by_reference_diff(golden):
+    """BASELINE config 1 cut into 256 windows of 1024 B (test/test_diff.cpp:38-57 shape) and run
+    through the REFERENCE diff() (gallocy/utils/diff.cpp:73-167, oracle/_ref; fixture made by
+    tests/golden/make_golden.py). Where its alignment is gap-free (all 256 windows), out1 / out2
+    are the window's twin / current bytes and {i : out1[i] != out2[i]} must equal the positions
+    the oracle's page-diff runs cover; applying the oracle stream to the twin gives out2."""
+    import zlib
+    g = golden["c1_windows"]
+    t, c = c1_windows()
+    assert g["gapfree"].all() and (g["L"] == 1024).all()
+    tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+    for i in range(len(tw)):
+        assert [zlib.crc32(tw[i].tobytes()), zlib.crc32(cw[i].tobytes())] == g["crc"][i].tolist()
+    ro, data = oracle.diff_pages(t, c)
+    pos = runs_positions(ro, data, 64).reshape(-1, 1024)
+    ref = np.unpackbits(g["mask"], axis=1).astype(bool)
+    assert ref.any(axis=1).sum() > 150  # 1 - 0.99^128 = 72 % of windows hold a write
+    assert np.array_equal(pos, ref)
+    rep = t.copy()
+    assert oracle.apply(rep, ro, data) == 0
+    assert np.array_equal(rep, c)
+    # the oracle's own NW restatement agrees with the reference on a sample of the windows
+    for i in range(0, 256, 32):
+        o1, o2 = oracle.nw_diff(tw[i].tobytes(), cw[i].tobytes())
+        assert [zlib.crc32(o1), zlib.crc32(o2)] == g["crc"][i].tolist()

@@ -125,3 +125,20 @@ def test_rejects_unaligned_region():
     if addr % 4096 == 0:
         addr += 1
     assert L.gdsm_track_begin(C.byref(h), addr, 1) == -22
+
+
+def test_non_write_fault_in_tracked_page_is_not_swallowed():
+    """Only write faults belong to a tracker: an instruction fetch from a tracked (PROT_READ,
+    not executable) page goes to the previous handler, so the process dies of SIGSEGV instead of
+    retrying the fetch forever."""
+    code = ("import mmap, ctypes, gallocy_amd as ga\n"
+            "mm = mmap.mmap(-1, 4 * 4096)\n"
+            "t = ga.Tracker(mm)\n"
+            "t.pages()[2, 0] = 1\n"
+            "print('tracked ok', flush=True)\n"
+            "fn = ctypes.CFUNCTYPE(None)(t.base + 4096)\n"
+            "fn()\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120)
+    assert "tracked ok" in r.stdout
+    assert r.returncode == -11, (r.returncode, r.stderr[-500:])
