@@ -2,17 +2,18 @@
 """Benchmark of the DSM hot path: pages diffed + applied per second (4 KiB pages).
 
 One step = diff of every page of the shard (TWIN vs CURRENT -> canonical run stream, SPEC §3)
-+ apply of that stream to the REPLICA arena (SPEC §4); for N > 1 the records whose home shard
-is another rank are exchanged over RCCL (all-to-all) between the two (gallocy_amd/exchange.py).
-With --overlap on (the default for N > 1) steps are double-buffered: the exchange and apply of
-step k run on a second stream while step k+1 is diffed, hiding the RCCL all-to-all. On one GPU
-the default is serial (diff k+1 starts after apply k): the step is HBM-bound there and an
-overlapped apply only takes its bandwidth from the diff (measured within a few % either way).
-Every step is complete when the clock stops; the line reports the other mode's ms/step too.
++ apply of that stream to the REPLICA arena (SPEC §4). On one GPU the step is serial (diff k+1
+starts after apply k): it is HBM-bound and an overlapped apply only takes bandwidth from the
+diff. For N > 1 each rank diffs its pages into one stream per home GPU and libgdsm's
+gdsm_exchange ships them over RCCL (xGMI) and applies them at the homes
+(gallocy_amd/exchange.py); releases are double-buffered (the exchange and home-side apply of k
+run on a second stream while k+1 is diffed) and, after the first release has fixed every
+stream's byte budget, never synchronise the host. Every step is complete when the clock stops.
 
-Workload (BASELINE.json configs[1]): 1M x 4 KiB pages per GPU, 1 % random 8-byte word writes,
-synthetic (SPEC §6), inputs resident in HBM before the timed region. Weak scaling: every rank
-owns 1M pages.
+Workloads: N = 1 (default): BASELINE.json configs[1], 1M x 4 KiB pages, 1 % random 8-byte word
+writes. N > 1 (default): configs[2], 16M pages in all (64 GiB), clustered 10 % writes,
+page-sharded over the N GPUs: strong scaling. `--scaling weak` keeps 1M pages per GPU instead.
+Synthetic inputs (SPEC §6), resident in HBM before the timed region.
 
 Prints ONE JSON line on rank 0 (contract in the task statement); everything else -> stderr.
 """
@@ -43,8 +44,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pages", type=int, default=1 << 20, help="pages per GPU")
-    ap.add_argument("--mode", choices=["uniform", "clustered"], default="uniform")
+    ap.add_argument("--pages", type=int, default=1 << 20, help="pages per GPU (weak scaling)")
+    ap.add_argument("--total-pages", type=int, default=None,
+                    help="pages in all (strong scaling; default 16M for N > 1: configs[2])")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="default: weak (1M pages) on one GPU, strong (16M in all) for N > 1")
+    ap.add_argument("--mode", choices=["uniform", "clustered"], default=None,
+                    help="default: uniform 1 %% words (configs[1]); clustered 10 %% (configs[2]) "
+                         "for strong scaling over N > 1 GPUs")
     ap.add_argument("--ppm", type=int, default=None, help="write density in parts per million")
     ap.add_argument("--seed", type=int, default=2026)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -399,8 +406,10 @@ def main():
     import torch
     import torch.distributed as dist
 
-    # GDSM_BENCH_BACKEND=gloo: REHEARSAL ONLY of the N > 1 step (several ranks may share one GPU,
-    # the exchange goes through host memory); the line it prints is not a measurement.
+    # The control plane (barriers, max-over-ranks time, the RCCL unique id) runs over gloo; the
+    # page data goes GPU to GPU over RCCL inside libgdsm (gdsm_exchange). GDSM_BENCH_BACKEND=gloo:
+    # REHEARSAL ONLY of the N > 1 step (several ranks may share one GPU, the records go through
+    # host memory); the line it prints is not a measurement.
     backend = os.environ.get("GDSM_BENCH_BACKEND", "nccl")
     if backend not in ("nccl", "gloo"):
         raise SystemExit("GDSM_BENCH_BACKEND must be nccl or gloo")
@@ -408,41 +417,44 @@ def main():
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")
     import gallocy_amd as ga
     from gallocy_amd import exchange
 
-    mode = ga.GEN_UNIFORM if args.mode == "uniform" else ga.GEN_CLUSTERED
+    # N = 1: BASELINE configs[1] (1M pages, 1 % word writes). N > 1: configs[2] by default: 16M
+    # pages in all, clustered 10 %, page-sharded over the N GPUs (strong scaling).
+    scaling = args.scaling or ("strong" if world > 1 else "weak")
+    mode_name = args.mode or ("clustered" if scaling == "strong" and world > 1 else "uniform")
+    mode = ga.GEN_UNIFORM if mode_name == "uniform" else ga.GEN_CLUSTERED
     ppm = args.ppm if args.ppm is not None else (10000 if mode == ga.GEN_UNIFORM else 100000)
-    n = args.pages
-    if n % world:
-        raise SystemExit("--pages must be a multiple of the GPU count")
+    if scaling == "strong":
+        total_pages = args.total_pages if args.total_pages else (16 << 20 if world > 1 else args.pages)
+        if total_pages % (world * world):
+            raise SystemExit("--total-pages must be a multiple of GPUs^2")
+        n = total_pages // world
+    else:
+        n = args.pages
+        if n % world:
+            raise SystemExit("--pages must be a multiple of the GPU count")
     ctx = ga.Context(n, device=local)
     # writer(p) = p mod G, home(p) = p // n (gallocy_amd/exchange.py); N = 1 is the identity
     ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank, stride=world,
                   arenas=("twin", "current"))
     ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n, stride=1,
                   arenas=("replica",))
-    cap = n * (256 if mode == ga.GEN_UNIFORM else 1024)
-    # Two diff streams: release k+1 is diffed while release k is exchanged / applied
-    # (gdsm_apply_async on one GPU, exchange.Shard's comm stream for N > 1).
-    runs = [ga.Runs(ctx, n, cap=cap) for _ in range(2)]
-    shard = exchange.Shard(ctx, runs, rank, world, n) if world > 1 else None
-    if shard is not None:
-        shard.gen_args = (args.seed, mode, ppm)
+    cap_pp = 256 if mode == ga.GEN_UNIFORM else 1024  # stream bytes per page reserved
+    shard = None
+    if world > 1:
+        shard = exchange.Shard(ctx, rank, world, n, cap_pp,
+                               transport="gloo" if backend == "gloo" else "rccl")
+        runs = None
+    else:
+        # Two diff streams: release k+1 may be diffed while release k is applied
+        runs = [ga.Runs(ctx, n, cap=n * cap_pp) for _ in range(2)]
 
     def steps(k: int, pipelined: bool):
         if shard is not None:
-            if pipelined:
-                shard.run(k)
-            else:
-                for _ in range(k):
-                    ctx.diff(out=runs[0])
-                    shard.exchange_and_apply()
-                    shard.drain()
+            shard.run(k, pipelined)
             return
         for i in range(k):
             r = runs[i % 2] if pipelined else runs[0]
@@ -455,12 +467,27 @@ def main():
         ctx.sync()
 
     pipelined = args.overlap == "on" or (args.overlap == "auto" and world > 1)
-    steps(args.warmup, pipelined)
+    if shard is not None:
+        # release 0 with exact sizes (one host read), then fixed byte budgets: no host sync
+        shard.run(1, pipelined=False)
+        drain()
+        if shard.transport == "rccl":
+            shard.calibrate()
+        steps(max(0, args.warmup - 1), pipelined)
+        total = sum(r.total() for d, r in enumerate(shard.send[0]) if shard.counts[d])
+        host = None
+        pay = 0
+        for d, r in enumerate(shard.send[0]):
+            if shard.counts[d]:
+                h = r.to_host()
+                pay += payload_bytes(h.rec_off, h.data)
+    else:
+        steps(args.warmup, pipelined)
+        total = runs[0].total()  # raises ENOSPC if the capacity was too small
+        assert not pipelined or args.warmup < 2 or runs[1].total() == total
+        host = runs[0].to_host()
+        pay = payload_bytes(host.rec_off, host.data)
     drain()
-    total = runs[0].total()  # raises ENOSPC if the capacity was too small
-    assert not pipelined or args.warmup < 2 or runs[1].total() == total
-    host = runs[0].to_host()
-    pay = payload_bytes(host.rec_off, host.data)
     del host
 
     def barrier():
@@ -471,6 +498,7 @@ def main():
         barrier()
         drain()
         torch.cuda.synchronize()
+        barrier()
         if prof:
             ctx.prof_enable(True)
         t0 = time.perf_counter()
@@ -484,7 +512,7 @@ def main():
             ctx.prof_enable(False)
         dt = t1 - t0
         if world > 1:
-            t = torch.tensor([dt], device="cuda")
+            t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         return dt, p
@@ -496,19 +524,21 @@ def main():
     dt, prof = timed(pipelined, True)
 
     # correctness of the measured work: REPLICA == CURRENT afterwards (diff of the two is empty)
-    chk = ga.Runs(ctx, n, cap=1 << 20)
-    ws = ctx.buffer(ga.gdsm.lib().gdsm_diff_workspace_bytes(n))
-    rc = ga.gdsm.lib().gdsm_diff_raw(ctx.arena_ptr("replica"), ctx.arena_ptr("current"), None, n,
-                                     chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes,
-                                     ctx.stream)
-    replica_ok = rc == 0 and chk.total() == 0 if shard is None else shard.verify()
-    if world > 1:  # every rank's home block checked, reported as one flag
-        t = torch.tensor([1 if replica_ok else 0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if shard is None:
+        chk = ga.Runs(ctx, n, cap=1 << 20)
+        ws = ctx.buffer(ga.gdsm.lib().gdsm_diff_workspace_bytes(n))
+        rc = ga.gdsm.lib().gdsm_diff_raw(ctx.arena_ptr("replica"), ctx.arena_ptr("current"), None,
+                                         n, chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes,
+                                         ctx.stream)
+        replica_ok = rc == 0 and chk.total() == 0
+    else:
+        replica_ok = shard.verify(args.seed, mode, ppm)
+        t = torch.tensor([1 if replica_ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)  # every rank's home block, one flag
         replica_ok = bool(t.item())
 
-    # The diff runs as ceil(n / 1M) chunk launches per step (kDiffChunk): bytes per launch and
-    # time per launch are both taken over one chunk launch on average.
+    # The diff runs as one launch per destination per step: bytes per launch and time per launch
+    # are both averaged over the step's launches.
     diff_ms, diff_launches = prof["diff"]
     avg_diff_ms = diff_ms / max(1, diff_launches)
     per_step = max(1, diff_launches // args.steps)
@@ -517,11 +547,19 @@ def main():
     step_bytes = n * 8192 + 2 * total + pay  # B_page summed
     ms_step = dt / args.steps * 1e3
     value = world * n * args.steps / dt
-    traffic, traffic_src = read_traffic(n, args.mode, ppm)
+    traffic, traffic_src = read_traffic(n, mode_name, ppm)
 
     if rank == 0:
         stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
                   for k, v in prof.items() if v[1]}
+        if scaling == "strong":
+            workload = (f"{world * n} x 4 KiB pages in all, {n} per GPU, {mode_name} "
+                        f"{ppm / 1e4:g}% {'8-B word' if mode == ga.GEN_UNIFORM else '64-B cluster'}"
+                        f" writes, diff+apply" + (", RCCL exchange to home GPUs" if world > 1 else ""))
+        else:
+            workload = (f"{n} x 4 KiB pages per GPU, {mode_name} {ppm / 1e4:g}% "
+                        f"{'8-B word' if mode == ga.GEN_UNIFORM else '64-B cluster'} writes, "
+                        f"diff+apply" + (", RCCL exchange to home GPUs" if world > 1 else ""))
         res = {
             "metric": "pages diffed+applied/sec (4 KiB)",
             "value": round(value, 1),
@@ -531,14 +569,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (counter-hash pages, docs/SPEC.md §6)",
-            "config": {"workload": f"{n} x 4 KiB pages per GPU, {args.mode} {ppm / 1e4:g}% "
-                                   f"{'8-B word' if mode == ga.GEN_UNIFORM else '64-B cluster'} writes, "
-                                   f"diff+apply" + (", RCCL all-to-all exchange" if world > 1 else ""),
-                       "pages_per_gpu": n, "seed": args.seed, "parallelism": f"page-shard x{world}",
+            "config": {"workload": workload, "pages_per_gpu": n, "total_pages": world * n,
+                       "seed": args.seed, "parallelism": f"page-shard x{world}",
                        "diff_bytes_per_step": int(total), "payload_bytes_per_step": int(pay),
                        **({"backend": "gloo (REHEARSAL, not a measurement)"}
                           if world > 1 and backend == "gloo" else {})},
@@ -554,6 +590,7 @@ def main():
                          "avg_launch_ms": round(avg_diff_ms, 4)},
             "stages": stages,
             "exchange": None if shard is None else {
+                "transport": shard.transport, "fixed_budgets": bool(shard.flags),
                 "sent_remote_bytes_per_step": shard.sent_remote,
                 "received_bytes_per_step": shard.received},
             "replica_equals_current": bool(replica_ok),
@@ -562,6 +599,8 @@ def main():
         if not args.no_cpu and world == 1:  # the host baseline is a 1-GPU figure (rank 0, N = 1)
             res["cpu_baseline"] = cpu_baseline(mode, ppm, args.seed, args.cpu_seconds)
         print(json.dumps(res), flush=True)
+    if shard is not None:
+        shard.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -92,6 +92,12 @@ SIGNATURES = {
     "gdsm_track_rearm": (C.c_int, [vp]),
     "gdsm_track_end": (C.c_int, [vp]),
     "gdsm_track_diff": (C.c_int, [vp, vp, C.POINTER(GdsmRuns), vp, u64p]),
+    "gdsm_comm_unique_id": (C.c_int, [vp]),
+    "gdsm_comm_init": (C.c_int, [C.POINTER(vp), vp, C.c_int, C.c_int, vp]),
+    "gdsm_comm_fini": (C.c_int, [vp]),
+    "gdsm_comm_size": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "gdsm_exchange": (C.c_int, [vp, vp, C.POINTER(GdsmRuns), C.POINTER(vp), C.POINTER(GdsmRuns),
+                                C.POINTER(vp), C.c_int, C.c_uint32]),
 }
 # The legacy C++ symbol (gallocy/include/gallocy/utils/diff.h:9-11), exported unmangled-equal.
 LEGACY_DIFF_SYMBOL = "_Z4diffPKcmRPcS0_mS2_"

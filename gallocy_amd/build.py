@@ -17,8 +17,8 @@ CSRC = PKG / "csrc"
 LIBDIR = PKG / "lib"
 LIB = LIBDIR / "libgdsm.so"
 SOURCES = ["gdsm_pages.hip", "gdsm_coherence.hip", "gdsm_capi.cpp", "legacy_diff.cpp",
-           "gdsm_track.cpp", "gdsm_nw.hip", "gdsm_wire.hip"]
-HEADERS = ["gdsm_common.h", "gdsm_launch.h", "gdsm_prof.h", "gdsm_track.h"]
+           "gdsm_track.cpp", "gdsm_nw.hip", "gdsm_wire.hip", "gdsm_exchange.cpp"]
+HEADERS = ["gdsm_common.h", "gdsm_launch.h", "gdsm_prof.h", "gdsm_track.h", "gdsm_ctx.h"]
 ARCH = os.environ.get("GDSM_ARCH", "gfx950")
 
 
@@ -54,7 +54,7 @@ def build_lib(force: bool = False, verbose: bool = False) -> Path:
         objs.append(str(obj))
     tmp = LIB.with_suffix(".so.tmp")
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs,
-           "-Wl,--no-undefined"]
+           "-ldl", "-Wl,--no-undefined"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -87,7 +87,7 @@ def build_sanitized(verbose: bool = False) -> Path:
     lib = SAN_DIR / "libgdsm.so"
     subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC",
                     "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
-                    "-shared-libsan", "-o", str(lib), *objs], check=True)
+                    "-shared-libsan", "-o", str(lib), *objs, "-ldl"], check=True)
     clang = Path(_hipcc()).resolve().parent.parent / "lib" / "llvm" / "bin" / "clang"
     if not clang.exists():
         clang = Path("/opt/rocm/lib/llvm/bin/clang")

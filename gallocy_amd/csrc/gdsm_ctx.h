@@ -1,0 +1,96 @@
+// The context object behind the C ABI and the host helpers shared by the .cpp files that
+// implement include/gdsm.h (internal header).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include <map>
+#include <set>
+
+#include "gdsm.h"
+#include "gdsm_prof.h"
+
+struct gdsm_ctx {
+  int device = 0;
+  uint64_t n_pages = 0;
+  hipStream_t stream = nullptr;
+  uint8_t* arena[3] = {nullptr, nullptr, nullptr};
+  uint32_t* err = nullptr;       // device error word (bit 0: malformed record, bit 1: bad events)
+  uint8_t* diff_ws = nullptr;    // diff workspace
+  uint64_t diff_ws_bytes = 0;
+  uint8_t* coh_ws = nullptr;
+  uint64_t coh_ws_bytes = 0;
+  uint64_t* coh_pt = nullptr;      // page table: state | faults << 32 per page
+  uint64_t* coh_totals = nullptr;  // device 10 x u64
+  uint32_t n_nodes = 0;
+  std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks
+  // gdsm_apply_async: applies run on `aux`, ordered after everything enqueued on `stream` before
+  // them; every other operation joins `aux` first, except gdsm_diff, which only waits for the
+  // apply still reading its output stream (runs_busy) or writing an arena it reads.
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_main = nullptr, ev_aux = nullptr;
+  bool aux_pending = false;
+  uint32_t aux_targets = 0;                      // arenas written by pending async applies
+  std::map<const void*, hipEvent_t> runs_busy;   // rec_off -> last async apply reading it
+  gdsm::Prof prof;
+  gdsm::Prof* P() { return prof.on ? &prof : nullptr; }
+  // gdsm_track_diff staging: pinned host and device, 2 x n x 4 KiB pages + n ids
+  uint8_t* track_host = nullptr;
+  uint64_t track_host_bytes = 0;
+  uint8_t* track_dev = nullptr;
+  uint64_t track_dev_bytes = 0;
+  // gdsm_nw_diff_batch: traceback workspace; host-offloaded diff() staging (device)
+  uint8_t* nw_ws = nullptr;
+  uint64_t nw_ws_bytes = 0;
+  uint8_t* nw_stage = nullptr;
+  uint64_t nw_stage_bytes = 0;
+  // gdsm_wire_*: text + frame + checksum word
+  uint8_t* wire_ws = nullptr;
+  uint64_t wire_ws_bytes = 0;
+  uint64_t wire_hdr[4] = {};  // host staging of the frame header
+  // checked copies of caller page-id lists (launch_check_ids): one per stream, so an async
+  // apply's list is never overwritten by a call on the main stream
+  uint32_t* ids_safe[2] = {nullptr, nullptr};
+  uint64_t ids_safe_bytes[2] = {0, 0};
+};
+
+namespace gdsm {
+namespace detail {
+
+int map_err(hipError_t e);
+// hipMalloc-backed buffer that only grows (contents are not kept).
+int ensure(uint8_t** buf, uint64_t* have, uint64_t need);
+// Makes ctx->stream wait for every pending operation on ctx->aux.
+int join_aux(gdsm_ctx* ctx);
+// Creates ctx->aux and its events on first use.
+int ensure_aux(gdsm_ctx* ctx);
+// A caller's device id list checked against the arenas on stream `which` (0 main, 1 aux).
+int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const uint32_t** out);
+int check_and_clear_err(gdsm_ctx* ctx);
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Device guard for an operation on the context's stream: ordered after pending async work.
+struct CtxGuard : DeviceGuard {
+  int rc;
+  explicit CtxGuard(gdsm_ctx* c) : DeviceGuard(c->device), rc(join_aux(c)) {}
+};
+
+}  // namespace detail
+}  // namespace gdsm
+
+#define GDSM_TRY(expr)                                              \
+  do {                                                              \
+    hipError_t e_ = (expr);                                         \
+    if (e_ != hipSuccess) return ::gdsm::detail::map_err(e_);       \
+  } while (0)

@@ -30,6 +30,10 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
 hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         const uint64_t* rec_off, const uint8_t* data, uint32_t* err,
                         hipStream_t s, Prof* prof = nullptr);
+// A received fixed-budget stream: zeroes rec_off (nothing applied) and err |= 4 unless
+// rec_off[0] == 0 and rec_off[n] <= cap.
+hipError_t launch_guard_stream(uint64_t* rec_off, uint64_t n, uint64_t cap, uint32_t* err,
+                               hipStream_t s);
 // Caller page-id lists at the context level: safe[i] = ids[i] if < n_pages, else n_pages (the
 // arenas' guard page), and err |= 8 when any id was out of range.
 hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, uint32_t* safe,

@@ -102,6 +102,22 @@ __global__ __launch_bounds__(256) void check_ids_kernel(const uint32_t* __restri
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(err, 8u);
 }
 
+// ------------------------------------------------------------------------- received streams
+// A stream received with a fixed byte budget (gdsm_exchange GDSM_XCHG_FIXED) is applied only if
+// it is well-formed at its ends: rec_off[0] == 0 and rec_off[n] <= cap (the bytes past rec_off[n]
+// are the sender's padding). Otherwise every offset is zeroed (all records empty: the apply
+// writes nothing) and err |= 4.
+__global__ __launch_bounds__(256) void guard_stream_kernel(uint64_t* __restrict__ rec_off,
+                                                           uint64_t n, uint64_t cap,
+                                                           uint32_t* __restrict__ err) {
+  const bool bad = rec_off[0] != 0 || rec_off[n] > cap || (rec_off[n] & 3u);
+  if (!bad) return;  // uniform: every thread read the same two words
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    rec_off[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 4u);
+}
+
 // ------------------------------------------------------------------------- diff (SPEC §3)
 // Bit j of the result is set iff byte j of x is non-zero (j = 0..3).
 __device__ __forceinline__ uint32_t nz4(uint32_t x) {
@@ -566,6 +582,192 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   diff_compact_body<kPrefetch, kStore>(twin, cur, ids, first, n, ws, sizes, block_sum);
 }
 
+// ---- single-pass diff (default): every record is written straight to its final place in the
+// packed stream, so the stream crosses HBM once (no workspace slots, no scan, no pack).
+// A WAVE is the unit of work: it draws a ticket (atomic counter; tickets are drawn in dispatch
+// order, so every lower ticket belongs to a wave that is already running) and diffs the kSpU
+// consecutive list entries of unit `ticket` exactly like the compacted kernel above (next page's
+// loads in flight, ballot/mbcnt compaction, DPP scans, record image built in LDS). Records that
+// fit the wave's LDS buffer stay there; a page with > 64 dirty 16-B chunks, or one that no longer
+// fits, is only sized ("late"). The wave then publishes its byte total as an 8-B {flag, value}
+// granule (agent-scope relaxed atomic store, i.e. one sc1 store: MI355X_MICROARCH.md
+// "granule") and finds its exclusive offset by decoupled look-back over the 64 nearest
+// predecessors' granules (agent-scope relaxed loads, s_sleep while one is unpublished). It
+// publishes its inclusive prefix, writes rec_off for its pages, copies its buffered records
+// from LDS to the stream with coalesced dword stores (nontemporal), and re-reads its late pages
+// from the arenas to emit them byte-wise in place. No wave ever waits for a ticket that a
+// non-running wave holds, so the look-back cannot deadlock whatever the dispatch order.
+constexpr uint32_t kSpU = 16;          // list entries per unit (one wave)
+constexpr uint32_t kSpBuf = 8192;      // per-wave LDS record buffer (bytes)
+constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+template <uint32_t kU, uint32_t kBuf, int kWaves>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
+    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, uint64_t n, uint64_t* __restrict__ rec_off,
+    uint8_t* __restrict__ data, uint64_t cap, uint64_t* __restrict__ ws) {
+  static_assert(kU <= 32 && (kU & (kU - 1)) == 0, "unit size");
+  __shared__ uint32_t sel_tab[16];
+  __shared__ uint32_t ent_all[4][64];
+  __shared__ uint4 dat_all[4][64];
+  __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kBuf / 4];
+  __shared__ uint32_t tab_all[4][2 * kU + 1];  // [0, kU]: record offsets; [kU+1, 2kU]: LDS source
+  if (threadIdx.x < 16) sel_tab[threadIdx.x] = compact_sel(threadIdx.x);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* ent = ent_all[wave];
+  uint4* dat = dat_all[wave];
+  uint32_t* buf = buf_all[wave];
+  uint32_t* tab = tab_all[wave];
+  const uint64_t nunits = (n + kU - 1) / kU;
+  // one ticket per workgroup (a single counter takes ~88 returning atomics per us, so per-wave
+  // tickets would queue on it); unit = 4 * ticket + wave
+  __shared__ uint32_t ticket;
+  if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u);
+  __syncthreads();
+  const uint64_t u = (uint64_t)ticket * 4 + wave;
+  if (u >= nunits) return;  // wave-uniform: the grid's spare waves
+  uint64_t* status = ws + 1;
+  const uint64_t i0 = u * kU;
+  const uint32_t cnt = (uint32_t)min((uint64_t)kU, n - i0);
+
+  uint32_t acc = 0;       // LDS bytes used by buffered records
+  uint32_t late = 0;      // bit j: page j is emitted from the arenas after the look-back
+  uint32_t my_size = 0;   // lane j: record size of page j
+  uint32_t my_src = 0;    // lane j: LDS byte offset of page j's record
+  uint4 t[4], c[4];
+  load_page(twin, cur, ids ? ids[i0] : i0, lane, t, c);
+  for (uint32_t j = 0; j < cnt; ++j) {
+    uint32_t m[4], D = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m[k] = diffmask16(t[k], c[k]);
+      const uint64_t B = __ballot(m[k] != 0u);
+      const uint32_t rank = D + __builtin_amdgcn_mbcnt_hi(
+                                    (uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+      if (m[k] && rank < 64u) {
+        ent[rank] = ((uint32_t)(k * 64 + lane) << 16) | m[k];
+        dat[rank] = c[k];
+      }
+      D += (uint32_t)__popcll(B);
+    }
+    if (j + 1 < cnt) load_page(twin, cur, ids ? ids[i0 + j + 1] : i0 + j + 1, lane, t, c);
+    uint32_t size = 0;
+    const uint32_t src = acc;
+    if (D > 64u) {
+      size = record_size_masks(m, lane);
+      late |= 1u << j;
+    } else if (D) {
+      wave_lds_sync();
+      const bool valid = lane < D;
+      const uint32_t E = valid ? ent[lane] : 0u;
+      const uint32_t Ep = from_prev_lane(E), En = from_next_lane(E);
+      const uint32_t g = E >> 16, mm = E & 0xFFFFu;
+      const uint32_t up = (Ep != 0u && (Ep >> 16) + 1u == g) ? (Ep >> 15) & 1u : 0u;
+      const uint32_t dn = (En != 0u && (En >> 16) == g + 1u) ? En & 1u : 0u;
+      const uint32_t s = mm & ~((mm << 1) | up) & 0xFFFFu;
+      const uint32_t e = mm & ~((mm >> 1) | (dn << 15)) & 0xFFFFu;
+      const uint32_t v = (uint32_t)__popc(e) | ((uint32_t)__popc(mm) << 16);
+      const uint32_t inc = wave_incl_sum(v);
+      const uint32_t tot = lane_bcast(inc, 63);
+      const uint32_t ls = s ? g * 16u + 32u - (uint32_t)__builtin_clz(s) : 0u;
+      const uint32_t ps = from_prev_lane(wave_incl_max(ls));
+      const uint32_t NR = tot & 0xFFFFu, NP = tot >> 16;
+      size = 4u + 4u * NR + ((NP + 3u) & ~3u);
+      if (acc + size > kBuf) {
+        late |= 1u << j;
+      } else {
+        uint32_t* img = buf + acc / 4u;
+        for (uint32_t q = lane; q < size / 4u; q += 64) img[q] = 0u;
+        const uint4 cc = valid ? dat[lane] : make_uint4(0, 0, 0, 0);
+        wave_lds_sync();
+        if (lane == 0) img[0] = NR;
+        if (valid) emit_compact(g, s, e, mm, ps, inc - v, cc, img, 4u + 4u * NR, sel_tab);
+        wave_lds_sync();
+        acc += size;
+      }
+    }
+    if (lane == j) {
+      my_size = size;
+      my_src = src;
+    }
+  }
+
+  // ---- publish the aggregate, look back for the exclusive offset, publish the inclusive prefix
+  const uint32_t incl = wave_incl_sum(my_size);  // lanes >= cnt hold 0
+  const uint32_t agg = lane_bcast(incl, 63);
+  if (lane == 0)
+    __hip_atomic_store(status + u, (u == 0 ? kStIncl : kStAgg) | agg, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  if (u > 0) {
+    int64_t pos = (int64_t)u - 1;
+    for (;;) {
+      const int64_t q = pos - (int64_t)lane;
+      uint64_t st = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : kStIncl;  // before unit 0: an inclusive prefix of 0
+      while (__ballot((st >> 62) == 0)) {  // a predecessor has not published yet
+        __builtin_amdgcn_s_sleep(1);
+        if ((st >> 62) == 0)
+          st = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint64_t im = __ballot((st >> 62) == 2);
+      if (im) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(im);
+        excl += wave_sum_u64(lane <= k ? (st & kStVal) : 0ull);
+        break;
+      }
+      excl += wave_sum_u64(st & kStVal);
+      pos -= 64;
+    }
+    if (lane == 0)
+      __hip_atomic_store(status + u, kStIncl | (excl + agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  // ---- rec_off, then the records: buffered ones from LDS, late ones from the arenas
+  if (lane < cnt) rec_off[i0 + lane + 1] = excl + incl;
+  if (u == 0 && lane == 0) rec_off[0] = 0;
+  if (lane < kU) {
+    tab[lane] = lane < cnt ? incl - my_size : agg;
+    tab[kU + 1 + lane] = ((late >> lane) & 1u) ? 0xFFFFFFFFu : my_src;
+  }
+  if (lane == 0) tab[kU] = agg;
+  // only records that end inside the capacity are stored (SPEC §3)
+  uint32_t limit = agg;
+  if (excl + agg > cap) {
+    const bool fits = lane < cnt && excl + incl <= cap;
+    limit = lane_bcast(wave_incl_max(fits ? incl : 0u), 63);
+  }
+  wave_lds_sync();
+  uint32_t* dst = reinterpret_cast<uint32_t*>(data + excl);
+  for (uint32_t g = lane; g < limit / 4u; g += 64) {
+    const uint32_t byte = 4u * g;
+    uint32_t j = 0;
+#pragma unroll
+    for (uint32_t step = kU / 2; step; step >>= 1)
+      if (tab[j + step] <= byte) j += step;
+    const uint32_t src = tab[kU + 1 + j];
+    if (src != 0xFFFFFFFFu) __builtin_nontemporal_store(buf[(src + byte - tab[j]) / 4u], dst + g);
+  }
+  for (uint32_t rem = late; rem;) {  // wave-uniform
+    const uint32_t j = (uint32_t)__builtin_ctz(rem);
+    rem &= rem - 1;
+    if (excl + tab[j + 1] > cap) continue;
+    const uint64_t i = i0 + j;
+    load_page(twin, cur, ids ? ids[i] : i, lane, t, c);
+    PageRuns P;
+    scan_page(t, c, lane, P);
+    emit_bytes(P, c, lane, data + excl + tab[j]);
+  }
+}
+
 // One workgroup: block_off[b] = base + sum(block_sum[0..b)), base = rec_off[first].
 // Thread t owns blocks [16t, 16t + 16) (four 16-B loads), sums them, the 1024 thread sums are
 // scanned by DPP inside each wave and through LDS across the 16 waves, then every thread writes
@@ -937,7 +1139,7 @@ static int diff_variant() {
   if (g_diff_variant < 0) {
     const char* e = getenv("GDSM_DIFF_VARIANT");
     g_diff_variant = e ? atoi(e) : 0;
-    if (g_diff_variant < 0 || g_diff_variant > 7) g_diff_variant = 0;
+    if (g_diff_variant < 0 || g_diff_variant > 12) g_diff_variant = 0;
   }
   return g_diff_variant;
 }
@@ -948,7 +1150,7 @@ int tune(const char* key, int64_t value) {
     g_apply_variant = (int)value;
     return 0;
   }
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 7) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 12) {
     g_diff_variant = (int)value;
     return 0;
   }
@@ -985,6 +1187,13 @@ hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, u
   return hipGetLastError();
 }
 
+hipError_t launch_guard_stream(uint64_t* rec_off, uint64_t n, uint64_t cap, uint32_t* err,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(guard_stream_kernel, dim3(grid_for(n + 1, 256, 1024)), dim3(256), 0, s,
+                     rec_off, n, cap, err);
+  return hipGetLastError();
+}
+
 hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
@@ -998,6 +1207,34 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
+  if (diff_variant() == 0) {
+    // single pass: ws = ticket counter + one status granule per unit, zeroed per launch
+    const uint64_t nunits = (n + kSpU - 1) / kSpU;
+    if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
+    if (e != hipSuccess) return e;
+    ProfScope ps(prof, 0, s);
+    hipLaunchKernelGGL((diff_single_kernel<kSpU, kSpBuf, 4>), dim3((unsigned)((nunits + 3) / 4)),
+                       dim3(256), 0, s, twin, cur, ids, n, rec_off, data, cap,
+                       reinterpret_cast<uint64_t*>(ws));
+    return hipGetLastError();
+  }
+  if (diff_variant() >= 9) {  // single-pass geometry A/B: (pages per wave, LDS bytes, waves/SIMD)
+    typedef void (*K)(const uint8_t*, const uint8_t*, const uint32_t*, uint64_t, uint64_t*,
+                      uint8_t*, uint64_t, uint64_t*);
+    static const K kk[] = {diff_single_kernel<8, 6144, 5>, diff_single_kernel<16, 6144, 5>,
+                           diff_single_kernel<8, 4096, 6>, diff_single_kernel<32, 8192, 4>};
+    static const uint32_t uu[] = {8, 16, 8, 32};
+    const int v = diff_variant() - 9;
+    const uint64_t nunits = (n + uu[v] - 1) / uu[v];
+    if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
+    if (e != hipSuccess) return e;
+    ProfScope ps(prof, 0, s);
+    hipLaunchKernelGGL(kk[v], dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids,
+                       n, rec_off, data, cap, reinterpret_cast<uint64_t*>(ws));
+    return hipGetLastError();
+  }
   // Largest chunk whose workspace fits.
   uint64_t chunk = n < kDiffChunk ? n : kDiffChunk;
   while (chunk > kDiffPagesPerBlock && diff_workspace_bytes(chunk) > ws_bytes) chunk >>= 1;
@@ -1019,7 +1256,8 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
           diff_compact_kernel<true, 2, 5>, diff_pages_kernel<0>,
           diff_pages_kernel<2>,            diff_pages_kernel<3>,
           diff_pages_kernel<4>,            diff_compact_kernel<false, 0, 4>,
-          diff_compact_kernel<true, 1, 5>, diff_compact_kernel<true, 0, 5>};
+          diff_compact_kernel<true, 1, 5>, diff_compact_kernel<true, 0, 5>,
+          diff_compact_kernel<true, 2, 5>};
       auto kern = kVariants[diff_variant()];
       hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids, first, m,
                          slots, sizes, block_sum);

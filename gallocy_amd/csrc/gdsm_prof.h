@@ -8,7 +8,7 @@
 namespace gdsm {
 
 struct Prof {
-  static constexpr int kStages = 11;
+  static constexpr int kStages = 12;
   bool on = false;
   hipStream_t stream = nullptr;
   struct Mark { int stage; hipEvent_t a, b; };

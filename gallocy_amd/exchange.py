@@ -1,31 +1,34 @@
-"""Diff propagation between page shards: one process per GPU, RCCL all-to-all over xGMI.
+"""Diff propagation between page shards: one process per GPU, the records of every release
+shipped to their home GPU over RCCL (xGMI) by libgdsm's `gdsm_exchange` (C ABI, include/gdsm.h).
 
 The reference sends its (unimplemented) page updates over HTTP with a per-peer std::async
-fan-out (gallocy/http/client.cpp:39-91, gallocy/consensus/client.cpp:15-42); here the records a
-shard produces for pages whose home is another rank travel in one all-to-all per step.
+fan-out (gallocy/http/client.cpp:39-91, gallocy/consensus/client.cpp:15-42).
 
-Layout (SURVEY §8e, config 3 shape, weak scaling): G ranks, n pages homed per rank, N = G·n.
-  home(p)   = p // n                 (contiguous page blocks, REPLICA arena index p - home·n)
+Layout (G ranks, N pages in all, n = N / G homed per rank):
+  home(p)   = p // n                 (contiguous page blocks; REPLICA index p - home·n)
   writer(p) = p mod G                (rank r writes pages r, r+G, r+2G, ...: TWIN/CURRENT arena
                                       index i holds global page i·G + r)
-A writer's page list is increasing in p, so its records for one home are one contiguous slice
-of its canonical diff stream (docs/SPEC.md §3); rank d receives from every source s the n/G
-records of pages p ≡ s (mod G) of its block, in increasing p, i.e. REPLICA indices s, s+G, ...
-
-`exchange_stream` is device-agnostic (CUDA tensors over RCCL, or CPU tensors over gloo in the
-tests); `Shard` wires it to a gdsm Context on the GPU.
+A writer's pages for home d are the arena indices [bounds[d], bounds[d+1]) (dest_bounds), which
+it diffs into its own stream send[d]; each record travels with its page's REPLICA index at the
+home (send_ids). Protocol per release (gdsm_exchange; `GlooTransport` restates it for CPU tests):
+  1. sizes: (records, bytes) per destination, all-to-all (or fixed by the caller: no host sync);
+  2. per peer pair: rec_off, ids, data;
+  3. the home applies every source's stream to its REPLICA (its own stream in place).
 """
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
-import torch
-import torch.distributed as dist
+
+from . import gdsm
+from ._lib import GdsmRuns, check
+
+XCHG_FIXED = 1
 
 
 def dest_bounds(rank: int, world: int, n: int) -> list[int]:
-    """Writer-local record index ranges per destination: [bounds[d], bounds[d+1])."""
+    """Writer-local arena index ranges per destination: [bounds[d], bounds[d+1])."""
     b = []
     for d in range(world + 1):
         # smallest i with i*G + rank >= d*n
@@ -33,130 +36,223 @@ def dest_bounds(rank: int, world: int, n: int) -> list[int]:
     return b
 
 
-def recv_ids(world: int, n: int) -> np.ndarray:
-    """REPLICA indices of the received records, in (source, page) order."""
-    return np.concatenate([np.arange(s, n, world, dtype=np.uint32) for s in range(world)])
+def send_ids(rank: int, world: int, n: int) -> list[np.ndarray]:
+    """Per destination d: the REPLICA index at rank d of each page rank `rank` sends there."""
+    b = dest_bounds(rank, world, n)
+    return [(np.arange(b[d], b[d + 1], dtype=np.int64) * world + rank - d * n).astype(np.uint32)
+            for d in range(world)]
 
 
-def exchange_stream(rec_off: torch.Tensor, data: torch.Tensor, bounds: list[int], world: int,
-                    group=None):
-    """All-to-all of a canonical diff stream split by destination.
+def budget(nbytes: int) -> int:
+    """Fixed-size exchange byte budget for a stream of `nbytes` (same formula on both sides)."""
+    return ((nbytes + nbytes // 32 + 4096) + 255) // 256 * 256
 
-    rec_off: int64[n+1] (the stream's offsets), data: uint8[>= rec_off[n]]. Returns the received
-    (rec_off int64[m+1], data uint8[rec_off[m]]) with the sources' records concatenated in rank
-    order. Two small collectives (byte counts, record sizes) and one payload all-to-all."""
-    dev = rec_off.device
-    bt = torch.tensor(bounds, dtype=torch.int64, device=dev)
-    edges = rec_off.index_select(0, bt)
-    send_bytes = (edges[1:] - edges[:-1]).contiguous()
-    recv_bytes = torch.empty_like(send_bytes)
-    dist.all_to_all_single(recv_bytes, send_bytes, group=group)
-    sizes = (rec_off[1:] - rec_off[:-1]).to(torch.int32)
-    send_recs = [bounds[d + 1] - bounds[d] for d in range(world)]
-    recv_recs_t = torch.tensor(send_recs, dtype=torch.int64, device=dev)
-    recv_recs_o = torch.empty_like(recv_recs_t)
-    dist.all_to_all_single(recv_recs_o, recv_recs_t, group=group)
-    counts = torch.stack([send_bytes, recv_bytes, recv_recs_o]).cpu().tolist()  # one host sync
-    sb, rb, rr = counts
-    recv_sizes = torch.empty(sum(rr), dtype=torch.int32, device=dev)
-    dist.all_to_all_single(recv_sizes, sizes, output_split_sizes=rr, input_split_sizes=send_recs,
-                           group=group)
-    total_in = int(sum(sb))
-    recv_data = torch.empty(max(1, sum(rb)), dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(recv_data[:sum(rb)], data[:total_in], output_split_sizes=rb,
-                           input_split_sizes=sb, group=group)
-    out_off = torch.zeros(len(recv_sizes) + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(recv_sizes.to(torch.int64), 0, out=out_off[1:])
-    return out_off, recv_data, int(sum(sb) - sb[dist.get_rank(group)]), int(sum(rb))
+
+# ---------------------------------------------------------------- CPU restatement (tests)
+class GlooTransport:
+    """The gdsm_exchange protocol restated over torch.distributed (gloo, CPU tensors): the
+    checker for multi-rank runs without GPUs (tests/test_exchange.py) and the transport of the
+    one-GPU multi-rank rehearsal (several ranks cannot share a GPU under RCCL)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+
+    def exchange(self, send: list) -> list:
+        """send[d] = (rec_off uint64[n+1], ids uint32[n], data uint8[>= rec_off[n]]) for every
+        destination d. Returns recv[s] = (rec_off, ids, data) as rank s sent them (recv[rank] is
+        send[rank] itself)."""
+        import torch
+        dist, g = self.dist, self.group
+        world, me = dist.get_world_size(g), dist.get_rank(g)
+        sizes = torch.tensor([[len(s[1]), int(s[0][-1])] for s in send], dtype=torch.int64)
+        got = torch.empty_like(sizes)
+        dist.all_to_all_single(got, sizes, group=g)                     # 1. sizes
+        rn, rb = got[:, 0].tolist(), got[:, 1].tolist()
+
+        def a2a(parts, recv_lens, dtype):
+            inp = torch.from_numpy(np.concatenate(parts).astype(dtype, copy=False))
+            out = torch.empty(sum(recv_lens), dtype=inp.dtype)
+            dist.all_to_all_single(out, inp, output_split_sizes=recv_lens,
+                                   input_split_sizes=[len(p) for p in parts], group=g)
+            return torch.split(out, recv_lens)
+        ro = a2a([s[0].astype(np.int64) for s in send], [x + 1 for x in rn], np.int64)  # 2.
+        ids = a2a([s[1].astype(np.int32) for s in send], rn, np.int32)
+        data = a2a([np.asarray(s[2][:int(s[0][-1])], np.uint8) for s in send], rb, np.uint8)
+        out = []
+        for s in range(world):
+            if s == me:
+                out.append(send[s])
+            else:
+                out.append((ro[s].numpy().astype(np.uint64), ids[s].numpy().astype(np.uint32),
+                            data[s].numpy()))
+        return out
+
+
+# ---------------------------------------------------------------- the GPU shard
+class Comm:
+    """An RCCL communicator owned by libgdsm (gdsm_comm_*), bootstrapped with a torch.distributed
+    group (any backend) that carries the 128-byte unique id."""
+
+    def __init__(self, ctx: gdsm.Context, rank: int, world: int, group=None):
+        import torch
+        import torch.distributed as dist
+        L = gdsm.lib()
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            check(L.gdsm_comm_unique_id(uid), "gdsm_comm_unique_id")
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        if world > 1:
+            obj = [bytes(t.tolist())]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            uid = (C.c_uint8 * 128)(*obj[0])
+        h = C.c_void_p()
+        check(L.gdsm_comm_init(C.byref(h), ctx.handle, world, rank, uid), "gdsm_comm_init")
+        self.handle = h.value
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if self.handle:
+            gdsm.lib().gdsm_comm_fini(self.handle)
+            self.handle = None
 
 
 class Shard:
-    """One rank's release pipeline: diff -> exchange -> apply to REPLICA.
+    """One rank's release pipeline: per-destination diffs -> exchange -> apply at the homes.
 
-    The diff runs on the context's stream, the exchange (RCCL) and the apply of the received
-    records on a second stream, with the diff stream double-buffered: diff k+1 is enqueued
-    before exchange k, so the all-to-all and the home-side apply of step k overlap the diff of
-    step k+1 (the only host synchronisation, the byte counts of exchange k, then waits for
-    diff k alone). Buffer b is reused by diff k+2 only after exchange k has read it."""
+    `n` arena pages per rank (TWIN/CURRENT: the pages this rank writes; REPLICA: its home block).
+    Two sets of per-destination send streams alternate, so diff k+1 (main stream) overlaps the
+    exchange and home-side apply of release k (the context's second stream); a diff into set b
+    waits for the exchange that last read it (libgdsm orders that itself).
 
-    def __init__(self, ctx, runs, rank: int, world: int, n: int):
-        from . import gdsm
+    transport "rccl": gdsm_exchange (RCCL inside libgdsm). After `calibrate()`, releases use
+    GDSM_XCHG_FIXED byte budgets: no host synchronisation at all per release.
+    transport "gloo": the GlooTransport restatement with host staging (rehearsal of several ranks
+    on one GPU, where RCCL cannot run); not a measurement."""
+
+    def __init__(self, ctx: gdsm.Context, rank: int, world: int, n: int, cap_per_page: int,
+                 transport: str = "rccl", group=None, sets: int = 2):
         if n % world:
             raise ValueError("pages per rank must be a multiple of the rank count")
-        runs = list(runs) if isinstance(runs, (list, tuple)) else [runs]
-        self.ctx, self.runs, self.rank, self.world, self.n = ctx, runs, rank, world, n
-        self.lib = gdsm.lib()
-        dev = torch.device("cuda", torch.cuda.current_device())
-        self.stream = torch.cuda.ExternalStream(ctx.stream, device=dev)   # diff
-        self.comm = torch.cuda.Stream(device=dev)                          # exchange + apply
+        self.ctx, self.rank, self.world, self.n = ctx, rank, world, n
+        self.L = gdsm.lib()
         self.bounds = dest_bounds(rank, world, n)
-        # Tensors aliasing the diff streams that libgdsm writes (device memory owned by ctx).
-        self.views = [(_tensor_at(r.s.rec_off, (n + 1,), torch.int64, dev),
-                       _tensor_at(r.s.data, (r.cap,), torch.uint8, dev)) for r in runs]
-        self.ready = [torch.cuda.Event() for _ in runs]      # diff into buffer b done
-        self.consumed = [None for _ in runs]                  # exchange of buffer b done
-        with torch.cuda.stream(self.comm):
-            self.recv_ids = torch.from_numpy(recv_ids(world, n)).to(dev)
-            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.sent_remote = 0
-        self.received = 0
+        self.counts = [self.bounds[d + 1] - self.bounds[d] for d in range(world)]
+        self.iota = ctx.ids(np.arange(n, dtype=np.uint32))             # arena index lists
+        self.sids = [ctx.ids(x) for x in send_ids(rank, world, n)]    # REPLICA index at home
+        self.send = [[gdsm.Runs(ctx, max(1, c), cap=max(4096, c * cap_per_page))
+                      for c in self.counts] for _ in range(sets)]
+        for st in self.send:
+            for d, r in enumerate(st):
+                r.s.n = self.counts[d]
+        rmax = max(self.counts) + 1  # records from any source: n/G or n/G + 1
+        self.recv = [gdsm.Runs(ctx, rmax, cap=max(4096, rmax * cap_per_page)) for _ in range(world)]
+        self.rids = [ctx.buffer(4 * rmax) for _ in range(world)]
+        self.transport = transport
+        self.comm = Comm(ctx, rank, world, group) if transport == "rccl" else None
+        self.gloo = GlooTransport(group) if transport == "gloo" else None
+        self.flags = 0
+        self.sent_remote = self.received = 0
+        self.k = 0
 
-    def _diff(self, k: int):
-        b = k % len(self.runs)
-        if self.consumed[b] is not None:
-            self.stream.wait_event(self.consumed[b])
-        self.ctx.diff(out=self.runs[b])
-        self.ready[b].record(self.stream)
+    # -- one release
+    def diff(self, k: int):
+        st = self.send[k % len(self.send)]
+        for d in range(self.world):
+            c = self.counts[d]
+            if c:
+                self.ctx.diff(self.iota.ptr + 4 * self.bounds[d], n=c, out=st[d])
 
-    def _exchange_apply(self, k: int):
-        b = k % len(self.runs)
-        rec_off, data = self.views[b]
-        self.comm.wait_event(self.ready[b])
-        with torch.cuda.stream(self.comm):
-            off, rdata, sent_remote, received = exchange_stream(rec_off, data, self.bounds,
-                                                               self.world)
-            ev = torch.cuda.Event()
-            ev.record(self.comm)
-            self.consumed[b] = ev
-            rc = self.lib.gdsm_apply_raw(self.ctx.arena_ptr("replica"), self.recv_ids.data_ptr(),
-                                         self.n, off.data_ptr(), rdata.data_ptr(),
-                                         self.err.data_ptr(), self.comm.cuda_stream)
-            if rc:
-                raise RuntimeError(f"gdsm_apply_raw: {rc}")
-        self.sent_remote, self.received = sent_remote, received
+    def exchange(self, k: int):
+        st = self.send[k % len(self.send)]
+        if self.comm is not None:
+            G = self.world
+            send = (GdsmRuns * G)(*[r.s for r in st])
+            recv = (GdsmRuns * G)(*[r.s for r in self.recv])
+            sid = (C.c_void_p * G)(*[b.ptr for b in self.sids])
+            rid = (C.c_void_p * G)(*[b.ptr for b in self.rids])
+            check(self.L.gdsm_exchange(self.ctx.handle, self.comm.handle, send, sid, recv, rid,
+                                       gdsm.REPLICA, self.flags), "gdsm_exchange")
+            for s in range(G):  # gdsm_exchange sets recv[s].n
+                self.recv[s].s.n = recv[s].n
+        else:
+            self._exchange_gloo(st)
 
-    def run(self, steps: int):
-        """`steps` releases, pipelined as described above; returns with work still in flight."""
+    def _exchange_gloo(self, st):
+        parts = []
+        for d, r in enumerate(st):
+            h = r.to_host() if self.counts[d] else gdsm.HostRuns(np.zeros(1, np.uint64),
+                                                                  np.zeros(0, np.uint8))
+            ids = (self.sids[d].download(np.uint32, self.counts[d]) if self.counts[d]
+                   else np.zeros(0, np.uint32))
+            parts.append((h.rec_off, ids, h.data))
+        got = self.gloo.exchange(parts)
+        self.received = sum(int(g[0][-1]) for g in got)
+        self.sent_remote = sum(int(p[0][-1]) for d, p in enumerate(parts) if d != self.rank)
+        for s, (ro, ids, data) in enumerate(got):
+            if len(ids) == 0:
+                continue
+            runs = gdsm.Runs.from_host(self.ctx, gdsm.HostRuns(ro, data))
+            d_ids = self.ctx.ids(ids)
+            self.ctx.apply(runs, "replica", d_ids)
+            self.ctx.sync()
+            runs.free()
+            d_ids.free()
+
+    def step(self, k: int):
+        self.diff(k)
+        self.exchange(k)
+
+    def run(self, steps: int, pipelined: bool = True):
+        """`steps` releases. Pipelined: diff k+1 is enqueued before exchange k, so with RCCL the
+        transfer and the home-side apply of k overlap the diff of k+1."""
         if steps <= 0:
             return
-        self._diff(0)
+        if not pipelined or self.comm is None:
+            for k in range(steps):
+                self.step(self.k + k)
+                if not pipelined:
+                    self.ctx.sync()
+            self.k += steps
+            return
+        self.diff(self.k)
         for k in range(steps):
             if k + 1 < steps:
-                self._diff(k + 1)
-            self._exchange_apply(k)
+                self.diff(self.k + k + 1)
+            self.exchange(self.k + k)
+        self.k += steps
 
-    def exchange_and_apply(self):
-        """One unpipelined step (the diff already enqueued on the context stream)."""
-        self.ready[0].record(self.stream)
-        self._exchange_apply(0)
+    def calibrate(self):
+        """After an exact-size release: fixes every stream's byte budget (budget()) on both
+        sides so later releases exchange with GDSM_XCHG_FIXED (no host synchronisation)."""
+        self.ctx.sync()
+        sent = [r.total() if self.counts[d] else 0 for d, r in enumerate(self.send[0])]
+        for st in self.send:
+            for d, r in enumerate(st):
+                r.s.cap = min(r.cap_alloc, budget(sent[d]))
+        recvd = []
+        for s, r in enumerate(self.recv):
+            if s == self.rank:
+                recvd.append(0)
+                continue
+            t = np.empty(1, np.uint64)
+            check(self.L.gdsm_memcpy_d2h(self.ctx.handle, t.ctypes.data, r.s.rec_off + 8 * r.s.n,
+                                         8), "d2h")
+            recvd.append(int(t[0]))
+            r.s.cap = min(r.cap_alloc, budget(int(t[0])))
+        self.sent_remote = sum(b for d, b in enumerate(sent) if d != self.rank)
+        self.received = sum(recvd) + sent[self.rank]
+        self.flags = XCHG_FIXED
 
     def drain(self):
-        """Waits for both streams; raises if an apply found a malformed record."""
-        self.comm.synchronize()
-        self.stream.synchronize()
-        if int(self.err.item()) != 0:
-            raise RuntimeError("apply: malformed record in the received stream")
+        """Waits for both streams; raises on a malformed or over-budget stream."""
+        self.ctx.sync()
 
-    def verify(self) -> bool:
+    def verify(self, seed: int, mode: int, ppm: int) -> bool:
         """REPLICA (home block) == CURRENT content of those pages, generated independently."""
-        from . import gdsm
-        n = self.n
+        n, L = self.n, self.L
         scratch = self.ctx.buffer(n * 4096)
-        seedinfo = getattr(self, "gen_args", None)
-        if seedinfo is None:
-            return False
-        seed, mode, ppm = seedinfo
-        L = self.lib
         if L.gdsm_gen_pages_raw(None, scratch.ptr, None, n, self.rank * n, 1, seed, mode, ppm,
                                 self.ctx.stream):
             return False
@@ -165,23 +261,11 @@ class Shard:
         rc = L.gdsm_diff_raw(self.ctx.arena_ptr("replica"), scratch.ptr, None, n, chk.s.rec_off,
                              chk.s.data, chk.cap, ws.ptr, ws.nbytes, self.ctx.stream)
         ok = rc == 0 and chk.total() == 0
-        scratch.free()
-        ws.free()
+        for x in (scratch, ws):
+            x.free()
         chk.free()
         return ok
 
-
-def _tensor_at(ptr: int, shape, dtype, device) -> torch.Tensor:
-    """A torch tensor viewing existing device memory (no copy, not owned)."""
-    itemsize = torch.empty((), dtype=dtype).element_size()
-
-    class _Iface:
-        pass
-
-    holder = _Iface()
-    typestr = {torch.int64: "<i8", torch.uint8: "|u1", torch.int32: "<i4"}[dtype]
-    holder.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr,
-                                       "data": (int(ptr), False), "version": 2, "strides": None}
-    t = torch.as_tensor(holder, device=device)
-    assert t.data_ptr() == int(ptr) and t.element_size() == itemsize
-    return t
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()

@@ -103,6 +103,7 @@ class Runs:
         self.ctx = ctx
         self.s = GdsmRuns()
         check(lib().gdsm_runs_alloc(ctx.handle, n, cap, C.byref(self.s)), "gdsm_runs_alloc")
+        self.cap_alloc = self.s.cap  # bytes allocated; s.cap may be lowered to a byte budget
 
     @property
     def n(self) -> int:
@@ -191,7 +192,7 @@ class Context:
         check(lib().gdsm_sync(self.handle), "gdsm_sync")
 
     PROF_STAGES = ("diff", "scan", "pack", "apply", "twin", "coh_tail", "coh_scan", "coh_apply",
-                   "coh_reduce", "nw_fill", "nw_trace")
+                   "coh_reduce", "nw_fill", "nw_trace", "exchange")
 
     def prof_enable(self, on: bool = True):
         check(lib().gdsm_prof_enable(self.handle, int(on)), "gdsm_prof_enable")

@@ -66,6 +66,7 @@ enum gdsm_prof_stage {
   GDSM_PROF_COH_REDUCE,
   GDSM_PROF_NW_FILL,  /* GPU diff(): DP fill */
   GDSM_PROF_NW_TRACE, /* GPU diff(): traceback + alignment strings */
+  GDSM_PROF_EXCHANGE, /* gdsm_exchange: the RCCL transfer of the record streams */
   GDSM_PROF_STAGES
 };
 
@@ -250,6 +251,49 @@ int gdsm_wire_decode(gdsm_ctx* ctx, const char* text, uint64_t len, uint32_t* id
  * (-EINVAL); a malformed record inside a well-formed frame fails during the apply (SPEC §7).
  * *n_out = records applied. Synchronises. */
 int gdsm_wire_apply(gdsm_ctx* ctx, int target, const char* text, uint64_t len, uint64_t* n_out);
+
+/* ---- multi-GPU diff propagation over RCCL / xGMI -------------------------------
+ * One process and one context per GPU; pages are sharded by home rank. At a release, each rank
+ * diffs the pages it wrote, grouped by home rank d, into one stream per destination (send[d]);
+ * gdsm_exchange ships every stream to its home and applies what arrives to the home's arena.
+ * This replaces the reference's page-update transport, an HTTP POST per peer fanned out with
+ * std::async (gallocy/http/client.cpp:39-91, driven by gallocy/consensus/client.cpp:15-42).
+ * RCCL is bound at run time (the librccl already loaded in the process, e.g. by torch, else
+ * librccl.so.1); without it gdsm_comm_* return -ENOSYS. */
+typedef struct gdsm_comm gdsm_comm;
+#define GDSM_COMM_ID_BYTES 128
+/* ncclGetUniqueId: call on ONE rank and hand the 128 bytes to every rank (Raft, HTTP, env). */
+int gdsm_comm_unique_id(uint8_t* id);
+/* Collective over the nranks processes (ncclCommInitRank on ctx's device). */
+int gdsm_comm_init(gdsm_comm** out, gdsm_ctx* ctx, int nranks, int rank, const uint8_t* id);
+int gdsm_comm_fini(gdsm_comm* comm);
+int gdsm_comm_size(const gdsm_comm* comm, int* nranks, int* rank);
+
+/* gdsm_exchange flags */
+enum gdsm_exchange_flags {
+  /* No host synchronisation: every record count and byte count is fixed by the caller.
+   * send[d] ships exactly send[d].n records and send[d].cap data bytes (cap is the byte budget:
+   * the stream's real size, rec_off[n], must not exceed it; the bytes past it are padding);
+   * recv[s].n and recv[s].cap must equal what rank s ships here. A stream found larger than its
+   * budget is not applied and the next gdsm_sync reports -EINVAL. Without the flag the library
+   * learns the sizes with one device all-to-all of (records, bytes) and one host read, and agrees
+   * on capacity with every rank (all return -ENOSPC when any receive stream is too small). */
+  GDSM_XCHG_FIXED = 1u << 0,
+};
+/* Collective: every rank of `comm` calls it with arrays of nranks entries.
+ *   send[d], send_ids[d]: this rank's stream for home rank d and, per record, the page's index
+ *                         in rank d's arena `target` (device, send[d].n entries);
+ *   recv[s], recv_ids[s]: where the stream from rank s lands (capacity recv[s].n_cap records,
+ *                         recv[s].cap bytes; recv_ids[s] >= that many entries); recv[s].n is set.
+ *                         recv[rank] / recv_ids[rank] are unused: the own stream is applied in
+ *                         place from send[rank].
+ * Runs on the context's second stream after everything enqueued on the main stream (the diffs
+ * that produced send[]); it overlaps the gdsm_diff calls that follow, and a later gdsm_diff into
+ * one of the send streams waits for it (as gdsm_apply_async). Malformed records and out-of-range
+ * page indices are reported by the next gdsm_sync. */
+int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* comm, const gdsm_runs* send,
+                  const uint32_t* const* send_ids, gdsm_runs* recv, uint32_t* const* recv_ids,
+                  int target, uint32_t flags);
 
 const char* gdsm_version(void);
 /* Process-wide kernel-variant knobs for measurement, e.g. ("diff_variant", 0..4). */

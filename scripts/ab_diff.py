@@ -26,6 +26,7 @@ else:
 runs = ga.Runs(ctx, n, cap=n * 1024)
 total = None
 res = {v: [] for v in VALUES}
+full = {}
 for r in range(ROUNDS):
     for v in VALUES:
         assert gdsm.lib().gdsm_tune(KEY.encode(), v) == 0
@@ -37,7 +38,8 @@ for r in range(ROUNDS):
         p = ctx.prof_read()
         ctx.prof_enable(False)
         res[v].append(p["diff"][0] / p["diff"][1])
-        if KEY != "diff_variant" or v in (0, 1, 2, 5):
+        full.setdefault(v, []).append(sum(p[k][0] for k in ("diff", "scan", "pack")) / REPS)
+        if KEY != "diff_variant" or v in (0, 1, 2, 5, 7, 8, 9, 10, 11, 12):
             t = runs.total()
             assert total is None or t == total, (v, t, total)
             total = t
@@ -45,5 +47,5 @@ gdsm.lib().gdsm_tune(KEY.encode(), 0)
 for v in VALUES:
     ms = res[v]
     gbs = (n * 8192 + (total or 0)) / (statistics.median(ms) * 1e-3) / 1e9
-    print(f"{KEY}={v}: median {statistics.median(ms):.4f} ms  min {min(ms):.4f} ms  -> {gbs:.0f} GB/s",
-          flush=True)
+    print(f"{KEY}={v}: median {statistics.median(ms):.4f} ms  min {min(ms):.4f} ms  -> {gbs:.0f} GB/s"
+          f"  (diff+scan+pack per call: {statistics.median(full[v]):.4f} ms)", flush=True)

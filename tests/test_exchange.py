@@ -28,14 +28,22 @@ def _worker(rank, world, port, n, mode, ppm, q):
     try:
         seed = 31
         twin, cur = oracle.gen_pages(n, seed=seed, mode=mode, ppm=ppm, first_page=rank, stride=world)
-        ro, data = oracle.diff_pages(twin, cur)
         b = exchange.dest_bounds(rank, world, n)
-        off, rdata, sent_remote, received = exchange.exchange_stream(
-            torch.from_numpy(ro.astype(np.int64)), torch.from_numpy(data), b, world)
+        sids = exchange.send_ids(rank, world, n)
+        send = []
+        for d in range(world):  # one stream per destination, as the GPU shard diffs them
+            ro, data = oracle.diff_pages(twin, cur, ids=np.arange(b[d], b[d + 1], dtype=np.uint32))
+            send.append((ro, sids[d], data))
+        got = exchange.GlooTransport().exchange(send)
         _, _, rep = oracle.gen_pages(n, seed=seed, mode=mode, ppm=ppm, first_page=rank * n, replica=True)
-        rc = oracle.apply(rep, off.numpy().astype(np.uint64), rdata.numpy(), ids=exchange.recv_ids(world, n))
+        rc = 0
+        for ro, ids, data in got:  # the home applies every source's stream
+            rc |= oracle.apply(rep, ro, data, ids=ids)
         _, want = oracle.gen_pages(n, seed=seed, mode=mode, ppm=ppm, first_page=rank * n)
-        q.put((rank, rc, bool(np.array_equal(rep, want)), sent_remote, received, int(ro[-1])))
+        sent_remote = sum(int(s[0][-1]) for d, s in enumerate(send) if d != rank)
+        total = sum(int(s[0][-1]) for s in send)
+        received = sum(int(g[0][-1]) for s, g in enumerate(got) if s != rank)
+        q.put((rank, rc, bool(np.array_equal(rep, want)), sent_remote, received, total))
     finally:
         dist.destroy_process_group()
 
@@ -55,7 +63,7 @@ def test_exchange_gloo(world, mode, ppm):
         assert p.exitcode == 0
     for rank, rc, ok, sent_remote, received, total in res:
         assert rc == 0 and ok, (rank, rc)
-        assert 0 < sent_remote < total
+        assert 0 < sent_remote < total and received > 0
 
 
 def test_dest_bounds_partition():
@@ -70,5 +78,15 @@ def test_dest_bounds_partition():
                 assert np.all(pages // n == d)
                 seen[pages] += 1
         assert np.all(seen == 1)
-        ids = exchange.recv_ids(world, n)
-        assert sorted(ids.tolist()) == list(range(n))
+        # every home index is received exactly once, from its writer
+        got = np.concatenate([exchange.send_ids(r, world, n)[d] + d * n
+                              for r in range(world) for d in range(world)])
+        assert sorted(got.tolist()) == list(range(world * n))
+        assert all(len(x) == 0 or x.max() < n for r in range(world)
+                   for x in exchange.send_ids(r, world, n))
+
+
+def test_budget_covers_and_is_aligned():
+    for b in (0, 1, 4, 1000, 123456, 1 << 30):
+        x = exchange.budget(b)
+        assert x >= b + 4096 and x % 256 == 0

@@ -1,15 +1,12 @@
-"""The multi-GPU step machinery on one real GPU: a 1-rank RCCL (torch 'nccl') group drives
-gallocy_amd.exchange.Shard — device tensors aliasing libgdsm buffers, the context stream as
-torch's current stream, all_to_all_single, gdsm_apply_raw — and the home REPLICA must end equal
-to CURRENT. (N > 1 runs in the driver's multi-GPU bench; tests/test_exchange.py covers 2-4 ranks
-of the same code over gloo.)"""
+"""The multi-GPU release machinery on one real GPU: libgdsm's own RCCL communicator
+(gdsm_comm_*) and gdsm_exchange through the C ABI on one rank, exchange.Shard's pipelined
+per-destination releases, and bench.py's N > 1 step rehearsed with several ranks on cuda:0 over
+gloo (RCCL cannot put two ranks on one GPU). N > 1 RCCL runs in the driver's multi-GPU bench;
+tests/test_exchange.py covers 2-4 ranks of the same protocol over gloo on CPU."""
 import os
 import socket
 
 import pytest
-import torch
-import torch.distributed as dist
-
 import gallocy_amd as ga
 from gallocy_amd import exchange
 
@@ -24,61 +21,76 @@ def _port():
     return p
 
 
-def test_shard_step_single_rank_rccl():
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    try:
-        n = 1 << 14
-        with ga.Context(n) as ctx:
-            ctx.gen_pages(seed=5, mode=ga.GEN_CLUSTERED, ppm=100000, first_global=0, stride=1,
-                          arenas=("twin", "current"))
-            ctx.gen_pages(seed=5, mode=ga.GEN_CLUSTERED, ppm=100000, first_global=0, stride=1,
-                          arenas=("replica",))
-            runs = ga.Runs(ctx, n, cap=n * 1024)
-            shard = exchange.Shard(ctx, runs, 0, 1, n)
-            shard.gen_args = (5, ga.GEN_CLUSTERED, 100000)
-            for _ in range(2):
-                ctx.diff(out=runs)
-                shard.exchange_and_apply()
-            ctx.sync()
-            torch.cuda.synchronize()
-            assert shard.received == runs.total() > 0
-            assert shard.verify()
-    finally:
-        dist.destroy_process_group()
+def test_exchange_c_abi_single_rank_rccl():
+    """gdsm_comm_* + gdsm_exchange through the C ABI on one RCCL rank: the exact-size path (device
+    all-to-all of (records, bytes), host read, all-reduce of the capacity verdict) and the
+    fixed-budget path both land the stream in the home REPLICA, which must equal CURRENT."""
+    import ctypes as C
+
+    import numpy as np
+
+    from gallocy_amd._lib import GdsmRuns
+    L = ga.gdsm.lib()
+    n = 1 << 14
+    with ga.Context(n) as ctx:
+        comm = exchange.Comm(ctx, 0, 1)
+        try:
+            nr = C.c_int(0)
+            me = C.c_int(-1)
+            assert L.gdsm_comm_size(comm.handle, C.byref(nr), C.byref(me)) == 0
+            assert (nr.value, me.value) == (1, 0)
+            for fixed in (0, exchange.XCHG_FIXED):
+                ctx.gen_pages(seed=5 + fixed, mode=ga.GEN_CLUSTERED, ppm=100000)
+                ids = ctx.ids(np.arange(n, dtype=np.uint32))
+                runs = ctx.diff(ids, n=n, cap=n * 1024)
+                send = (GdsmRuns * 1)(runs.s)
+                recv = (GdsmRuns * 1)(GdsmRuns())
+                sid = (C.c_void_p * 1)(ids.ptr)
+                rid = (C.c_void_p * 1)(None)
+                assert L.gdsm_exchange(ctx.handle, comm.handle, send, sid, recv, rid, ga.REPLICA,
+                                       fixed) == 0
+                ctx.sync()
+                assert np.array_equal(ctx.download("replica"), ctx.download("current"))
+                # a later diff into the same stream is ordered after the exchange that read it
+                ctx.diff(ids, n=n, out=runs)
+                ctx.sync()
+                runs.free()
+        finally:
+            comm.close()
 
 
-def test_shard_pipelined_run_single_rank_rccl():
-    """Shard.run: diff k+1 on the context stream overlaps exchange + apply k on the comm
-    stream, two run buffers alternating; the replica must still end equal to CURRENT."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    try:
-        n = 1 << 14
-        with ga.Context(n) as ctx:
-            ctx.gen_pages(seed=6, mode=ga.GEN_UNIFORM, ppm=10000, first_global=0, stride=1,
-                          arenas=("twin", "current"))
-            ctx.gen_pages(seed=6, mode=ga.GEN_UNIFORM, ppm=10000, first_global=0, stride=1,
-                          arenas=("replica",))
-            runs = [ga.Runs(ctx, n, cap=n * 256) for _ in range(2)]
-            shard = exchange.Shard(ctx, runs, 0, 1, n)
-            shard.gen_args = (6, ga.GEN_UNIFORM, 10000)
+@pytest.mark.parametrize("mode,ppm", [(0, 10000), (1, 100000)])
+def test_shard_pipelined_single_rank_rccl(mode, ppm):
+    """exchange.Shard on one RCCL rank: release 0 with exact sizes, calibrate() fixes the byte
+    budgets, then pipelined releases (diff k+1 on the main stream overlaps exchange + apply k on
+    the second stream, two send sets alternating) with no host synchronisation; the home REPLICA
+    must equal CURRENT."""
+    n = 1 << 14
+    with ga.Context(n) as ctx:
+        ctx.gen_pages(seed=6, mode=mode, ppm=ppm, first_global=0, stride=1,
+                      arenas=("twin", "current"))
+        ctx.gen_pages(seed=6, mode=mode, ppm=ppm, first_global=0, stride=1, arenas=("replica",))
+        shard = exchange.Shard(ctx, 0, 1, n, 1024)
+        try:
+            shard.run(1, pipelined=False)
+            shard.calibrate()
+            assert shard.flags == exchange.XCHG_FIXED and shard.received > 0
+            ctx.prof_enable(True)
             shard.run(5)
             shard.drain()
-            ctx.sync()
-            assert shard.received == runs[0].total() == runs[1].total() > 0
-            assert shard.verify()
-    finally:
-        dist.destroy_process_group()
+            prof = ctx.prof_read()
+            assert prof["diff"][1] == 5 and prof["apply"][1] == 5
+            assert shard.verify(6, mode, ppm)
+        finally:
+            shard.close()
 
 
 @pytest.mark.parametrize("ranks,overlap", [(2, "on"), (3, "off")])
 def test_bench_multi_rank_rehearsal_gloo(ranks, overlap):
     """bench.py's N > 1 step end to end with `ranks` processes sharing cuda:0 and exchanging over
-    gloo (GDSM_BENCH_BACKEND=gloo, a rehearsal of the RCCL path: same Shard pipeline, barriers,
-    max-over-ranks timing): every rank's home REPLICA must equal CURRENT afterwards."""
+    gloo (GDSM_BENCH_BACKEND=gloo, a rehearsal of the RCCL path: the same per-destination diffs,
+    Shard, barriers, max-over-ranks timing; the strong-scaling default at a small total): every
+    rank's home REPLICA must equal CURRENT afterwards."""
     import json
     import subprocess
     import sys
@@ -88,7 +100,8 @@ def test_bench_multi_rank_rehearsal_gloo(ranks, overlap):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={ranks}", "--master-addr", "127.0.0.1", "--master-port",
            str(_port()), str(root / "bench.py"), "--gpus", str(ranks), "--steps", "3",
-           "--warmup", "1", "--pages", str(ranks * 16384), "--no-cpu", "--overlap", overlap]
+           "--warmup", "1", "--total-pages", str(ranks * ranks * 8192), "--no-cpu", "--overlap",
+           overlap]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -97,3 +110,4 @@ def test_bench_multi_rank_rehearsal_gloo(ranks, overlap):
     assert d["n_gpus"] == ranks and d["replica_equals_current"] is True
     assert d["exchange"]["received_bytes_per_step"] > 0
     assert d["pipelined"] is (overlap == "on")
+    assert d["scaling"] == "strong" and d["config"]["total_pages"] == ranks * ranks * 8192
