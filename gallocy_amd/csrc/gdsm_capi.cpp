@@ -121,8 +121,7 @@ int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* id
     GDSM_TRY(hipMemcpyAsync(ids_dev, ctx->track_dev + 2 * n * GDSM_PAGE_SZ, n * sizeof(uint32_t),
                             hipMemcpyDeviceToDevice, ctx->stream));
   }
-  const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
-  rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk ? chunk : 1));
+  rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
   if (rc) return rc;
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->track_dev, ctx->track_dev + n * GDSM_PAGE_SZ, nullptr, n,
@@ -274,8 +273,7 @@ int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events) {
   if (g.rc) return g.rc;
   int rc = 0;
   if (diff_pages) {
-    const uint64_t chunk = diff_pages < gdsm::kDiffChunk ? diff_pages : gdsm::kDiffChunk;
-    rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk));
+    rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(diff_pages));
   }
   if (!rc && coh_events)
     rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(coh_events));
@@ -451,8 +449,7 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
   }
   auto busy = ctx->runs_busy.find(out->rec_off);
   if (busy != ctx->runs_busy.end()) GDSM_TRY(hipStreamWaitEvent(ctx->stream, busy->second, 0));
-  const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
-  int rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(chunk ? chunk : 1));
+  int rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
   if (!rc) rc = safe_ids(ctx, ids, n, 0, &ids);
   if (rc) return rc;
   out->n = n;
@@ -505,10 +502,7 @@ int gdsm_apply_async(gdsm_ctx* ctx, int target, const uint32_t* ids, const gdsm_
   return 0;
 }
 
-uint64_t gdsm_diff_workspace_bytes(uint64_t n) {
-  const uint64_t chunk = n < gdsm::kDiffChunk ? n : gdsm::kDiffChunk;
-  return gdsm::diff_workspace_bytes(chunk ? chunk : 1);
-}
+uint64_t gdsm_diff_workspace_bytes(uint64_t n) { return gdsm::diff_workspace_bytes(n); }
 
 int gdsm_diff_raw(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                   uint64_t* rec_off, uint8_t* data, uint64_t cap, void* workspace,
@@ -564,9 +558,9 @@ int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n
   if (g.rc) return g.rc;
   int rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
   if (rc) return rc;
-  GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, events, n_events, totals_dev,
-                                  ctx->coh_ws, ctx->coh_ws_bytes, ctx->err, ctx->stream,
-                                  ctx->P()));
+  GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, ctx->n_nodes, events, n_events,
+                                  totals_dev, ctx->coh_ws, ctx->coh_ws_bytes, ctx->err,
+                                  ctx->stream, ctx->P()));
   return 0;
 }
 

@@ -39,6 +39,8 @@ namespace gdsm {
 constexpr uint32_t kConst = 1u << 31;
 constexpr uint32_t kCohK = 8;                   // events per thread
 constexpr uint32_t kCohBlock = 256 * kCohK;     // events per block
+constexpr uint32_t kSamp = kCohBlock / 64;       // pass A: sampling stride over a block
+static_assert(kSamp <= 64, "pass A samples the block with one wave");
 constexpr uint32_t kCohGroup = 1024;            // blocks per scan group
 constexpr uint32_t kNoHead = 0xFFFFFFFFu;
 constexpr uint64_t kNoHead64 = ~0ull;
@@ -182,7 +184,8 @@ __global__ __launch_bounds__(256) void coh_tail_kernel(const uint64_t* __restric
   } else if (const uint64_t wm = __ballot(valid && (e & 1u))) {
     // 2) no head in the tail but a write in it: the aggregate only depends on the events from
     //    the tail's last write on. The block's last head (if any) is the first event of the
-    //    tail's page: found by sampling every 32nd event, then the 32 events before the hit.
+    //    tail's page: found by sampling every kSamp-th event, then the kSamp events before the
+    //    hit.
     const uint32_t lw = 63u - (uint32_t)__clzll(wm);
     acc = wave_reduce_compose((valid && lane >= lw) ? ev_transform(e) : 0u);
     const uint64_t P = ev_page(lane_bcast64(e, 63));
@@ -190,16 +193,17 @@ __global__ __launch_bounds__(256) void coh_tail_kernel(const uint64_t* __restric
     if (hi - lo <= 64) {
       // the whole block is the tail and holds no head
     } else {
-      const uint64_t sidx = lo + (uint64_t)lane * 32;
+      const uint64_t sidx = lo + (uint64_t)lane * kSamp;
       const bool in = sidx < wlo;
       const uint64_t sm = __ballot(in && ev_page(ev[sidx]) == P);
-      const uint32_t j0 = sm ? (uint32_t)__builtin_ctzll(sm) : (uint32_t)((wlo - lo + 31) / 32);
+      const uint32_t j0 =
+          sm ? (uint32_t)__builtin_ctzll(sm) : (uint32_t)((wlo - lo + kSamp - 1) / kSamp);
       if (j0 == 0) {  // the block starts inside P's segment
         if (lo == 0 || ev_page(ev[lo - 1]) != P) h = lo;
       } else {
-        const uint64_t w0 = lo + (uint64_t)(j0 - 1) * 32 + 1;  // after the last sample below P
+        const uint64_t w0 = lo + (uint64_t)(j0 - 1) * kSamp + 1;  // after the last sample below P
         const uint64_t ix = w0 + lane;
-        const uint64_t hm2 = __ballot(lane < 32 && ix <= wlo && ev_page(ev[ix]) == P);
+        const uint64_t hm2 = __ballot(lane < kSamp && ix <= wlo && ev_page(ev[ix]) == P);
         h = w0 + (uint64_t)__builtin_ctzll(hm2);  // hm2 != 0: ev[wlo] has page P
       }
     }
@@ -351,7 +355,8 @@ __device__ __forceinline__ void coh_block(uint64_t* __restrict__ pt, uint64_t n_
                                           uint32_t cnt, uint64_t before, bool has_after,
                                           uint64_t after, uint32_t lh, uint64_t lhp, uint32_t cin,
                                           uint32_t* __restrict__ partial, uint32_t* wtot,
-                                          uint64_t* bnd, uint32_t (*red)[10], uint32_t& bad) {
+                                          uint64_t* bnd, uint32_t (*red)[10], uint32_t& bad,
+                                          uint32_t n_nodes) {
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t first = t * kCohK;
   uint32_t* pst = reinterpret_cast<uint32_t*>(pt);  // state words at even indices
@@ -388,6 +393,7 @@ __device__ __forceinline__ void coh_block(uint64_t* __restrict__ pt, uint64_t n_
       }
       if (hp && pg < pp) bad = 1;
       if (pg >= n_pages) bad = 1;
+      if (((uint32_t)(e[k] >> 1) & 7u) >= n_nodes) bad = 1;
       const bool last_in_blk = (x + 1 == cnt);
       const bool hn = last_in_blk ? has_after : true;
       const uint64_t pn = ev_page((k + 1 < kCohK && !last_in_blk) ? e[k + 1 < kCohK ? k + 1 : k]
@@ -506,7 +512,7 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
     uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
     uint64_t nb, const uint32_t* __restrict__ carry, const uint32_t* __restrict__ last_head,
     const uint64_t* __restrict__ head_pt, uint32_t* __restrict__ partial,
-    uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ err, uint32_t n_nodes) {
   __shared__ uint32_t wtot[4];
   __shared__ uint64_t bnd[8];
   __shared__ uint32_t red[4][10];
@@ -531,10 +537,10 @@ __global__ __launch_bounds__(256) void coh_apply_kernel(
 
     if (cnt == kCohBlock)
       coh_block<true>(pt, n_pages, e, b, b0, cnt, before, has_after, after, lh, lhp, cin,
-                      partial, wtot, bnd, red, bad);
+                      partial, wtot, bnd, red, bad, n_nodes);
     else
       coh_block<false>(pt, n_pages, e, b, b0, cnt, before, has_after, after, lh, lhp, cin,
-                       partial, wtot, bnd, red, bad);
+                       partial, wtot, bnd, red, bad, n_nodes);
 #pragma unroll
     for (uint32_t k = 0; k < kCohK; ++k) e[k] = en[k];
   }
@@ -580,7 +586,8 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
                                          const uint64_t (&e)[kCohK], uint64_t b0, uint32_t cnt,
                                          uint32_t lh, uint64_t lhp, uint32_t cin,
                                          uint32_t* __restrict__ slot, uint64_t* __restrict__ wd,
-                                         uint32_t* __restrict__ hpg, CohAcc& A, uint32_t& bad) {
+                                         uint32_t* __restrict__ hpg, CohAcc& A, uint32_t& bad,
+                                         uint32_t n_nodes) {
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t first = t * kCohK;  // block-relative index of e[0]
   uint32_t* pst = reinterpret_cast<uint32_t*>(pt);
@@ -598,11 +605,13 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
   // ---- heads, segment ends and the lane aggregate (its last CONST: a write, or a head whose
   // page-table word is fetched below), one pass over the events
   uint32_t hmask = 0, emask = 0, hib = 0, lw = 0, ra = 0, lastc = 0;  // lastc: 0 none, 1 write, 2 head
+  uint32_t nodes = 0;  // nodes named by the lane's events (checked against n_nodes once)
 #pragma unroll
   for (uint32_t k = 0; k < kCohK; ++k) {
     if (kFull || k < nvalid) {
       const uint32_t x = (uint32_t)e[k], node = (x >> 1) & 7u, bit = 1u << node;
       hib |= (uint32_t)(e[k] >> 32);
+      nodes |= bit;
       const uint32_t pk = page32(e[k]);
       const uint32_t pp = k ? page32(e[k > 0 ? k - 1 : 0]) : pprev;
       if ((k == 0 && g0 == 0) || pk != pp) {
@@ -623,7 +632,8 @@ __device__ __forceinline__ void coh_wave(uint64_t* __restrict__ pt, uint64_t n_p
       if (g0 + k + 1 >= n || pn != pk) emask |= 1u << k;
     }
   }
-  if (hib >> 4) bad = 1;  // page ids are u32 (SPEC §1)
+  if (hib >> 4) bad = 1;         // page ids are u32 (SPEC §1)
+  if (nodes >> n_nodes) bad = 1;  // a node outside the page table's n_nodes
   const uint32_t hc = (uint32_t)__popc(hmask);
   const uint32_t hinc = wave_incl_sum(hc);
   const uint32_t hb0 = hinc - hc, nh = lane_bcast(hinc, 63);
@@ -759,7 +769,7 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
     uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
     uint64_t nb, const uint32_t* __restrict__ carry, const uint32_t* __restrict__ last_head,
     const uint64_t* __restrict__ head_pt, uint32_t* __restrict__ partial,
-    uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ err, uint32_t n_nodes) {
   __shared__ uint32_t slots[4];
   __shared__ uint64_t wd[4][kCohHeads];
   __shared__ uint32_t hpg[4][kCohHeads];
@@ -775,10 +785,10 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
   load_block_events<true>(ev, n, b0 + t * kCohK, e);
   if (cnt == kCohBlock)
     coh_wave<true, kMeasure>(pt, n_pages, ev, n, e, b0, cnt, last_head[b], head_pt[b], carry[b],
-                             slots, wd[wave], hpg[wave], A, bad);
+                             slots, wd[wave], hpg[wave], A, bad, n_nodes);
   else
     coh_wave<false, kMeasure>(pt, n_pages, ev, n, e, b0, cnt, last_head[b], head_pt[b], carry[b],
-                              slots, wd[wave], hpg[wave], A, bad);
+                              slots, wd[wave], hpg[wave], A, bad, n_nodes);
   // per thread: inv <= 7 x 8, xfer <= 8, faults per node <= 8, so 16-bit fields hold a wave's
   // sums: five packed wave sums, one partial row per wave
   const uint32_t lo = (uint32_t)A.nf8, hi = (uint32_t)(A.nf8 >> 32);
@@ -846,11 +856,21 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 // ---------------------------------------------------------------- launchers
 // Pass C variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = coh_apply_block_kernel
 // (default), 1 = coh_apply_kernel (block-wide scans, per-event page-table accesses; the round-1
-// kernel), 2 / 3 = MEASUREMENT ONLY: variant 0 without page-table stores / without any
-// page-table traffic (output invalid). Variant 0 needs 16-B aligned events, else 1 runs.
-static int g_coh_variant = getenv("GDSM_COH_VARIANT") ? atoi(getenv("GDSM_COH_VARIANT")) : 0;
+// kernel, also the path for events that are not 16-B aligned). Built with -DGDSM_MEASURE only:
+// 2 / 3 = variant 0 without page-table stores / without any page-table traffic (output invalid).
+#ifdef GDSM_MEASURE
+constexpr int kCohVariants = 4;
+#else
+constexpr int kCohVariants = 2;
+#endif
+static int coh_variant_from_env() {
+  const char* e = getenv("GDSM_COH_VARIANT");
+  const int v = e ? atoi(e) : 0;
+  return (v >= 0 && v < kCohVariants) ? v : 0;
+}
+static int g_coh_variant = coh_variant_from_env();
 int coh_tune(const char* key, int64_t value) {
-  if (!strcmp(key, "coh_variant") && value >= 0 && value <= 3) {
+  if (!strcmp(key, "coh_variant") && value >= 0 && value < kCohVariants) {
     g_coh_variant = (int)value;
     return 0;
   }
@@ -876,9 +896,10 @@ hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hip
   return hipGetLastError();
 }
 
-hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* events,
-                            uint64_t n_events, uint64_t* totals, uint8_t* ws, uint64_t ws_bytes,
-                            uint32_t* err, hipStream_t s, Prof* prof) {
+hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
+                            const uint64_t* events, uint64_t n_events, uint64_t* totals,
+                            uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
+                            Prof* prof) {
   hipError_t r = hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
   if (r != hipSuccess || n_events == 0) return r;
   const uint64_t nb = coh_blocks(n_events), ng = coh_groups(nb);
@@ -906,10 +927,12 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* even
     ProfScope ps(prof, 7, s);
     // Persistent grid: every workgroup walks blocks b, b + grid, ... (no inter-workgroup
     // waiting, so residency is only a speed question).
-    static int grid = 0;
+    static int grid_by_dev[64] = {};  // resident workgroups of coh_apply_kernel, per device
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int& grid = grid_by_dev[dev & 63];
     if (!grid) {
-      int dev = 0, cus = 256, per = 4;
-      (void)hipGetDevice(&dev);
+      int cus = 256, per = 4;
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, coh_apply_kernel<true>, 256, 0);
       grid = cus * (per > 0 ? per : 4);
@@ -917,17 +940,21 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* even
     const unsigned g2 = (unsigned)min((uint64_t)grid, nb);
     const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
     if (g_coh_variant != 1 && vec) {
+#ifdef GDSM_MEASURE
       auto kern = g_coh_variant == 0 ? coh_apply_block_kernel<0>
                 : g_coh_variant == 2 ? coh_apply_block_kernel<1> : coh_apply_block_kernel<2>;
+#else
+      auto kern = coh_apply_block_kernel<0>;
+#endif
       hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, pt, n_pages, events,
-                         n_events, nb, carry, lh, head_pt, partial, err);
+                         n_events, nb, carry, lh, head_pt, partial, err, n_nodes);
       rows = nb * 4;
     } else if (vec)
       hipLaunchKernelGGL(coh_apply_kernel<true>, dim3(g2), dim3(256), 0, s, pt, n_pages, events,
-                         n_events, nb, carry, lh, head_pt, partial, err);
+                         n_events, nb, carry, lh, head_pt, partial, err, n_nodes);
     else
       hipLaunchKernelGGL(coh_apply_kernel<false>, dim3(g2), dim3(256), 0, s, pt, n_pages, events,
-                         n_events, nb, carry, lh, head_pt, partial, err);
+                         n_events, nb, carry, lh, head_pt, partial, err, n_nodes);
   }
   uint64_t g = (rows + 255) / 256;
   if (g > 1024) g = 1024;

@@ -6,9 +6,6 @@
 namespace gdsm {
 
 constexpr uint32_t kPage = 4096;
-// Per-page record slot in the diff workspace: the largest record (SPEC §3: 10244 B) rounded to
-// 16 B, so every slot starts 16-byte aligned.
-constexpr uint32_t kRecSlot = 10256;
 constexpr uint32_t kMaxRuns = 2048;
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }

@@ -7,13 +7,8 @@
 
 namespace gdsm {
 
-// Diff geometry: one 256-thread workgroup (4 waves) diffs kDiffPagesPerBlock pages.
-constexpr uint32_t kDiffPagesPerBlock = 64;
-constexpr uint32_t kDiffPagesPerWave = kDiffPagesPerBlock / 4;
-// Largest chunk of pages one diff pass handles with its workspace (the API loops over chunks).
-constexpr uint64_t kDiffChunk = 1ull << 20;
-
-uint64_t diff_workspace_bytes(uint64_t n_chunk);
+// Workspace of one diff of n list entries (ticket counter + one look-back granule per unit).
+uint64_t diff_workspace_bytes(uint64_t n);
 // Kernel variant knobs (see gdsm_tune); returns -1 for an unknown key.
 int tune(const char* key, int64_t value);
 int coh_tune(const char* key, int64_t value);
@@ -23,7 +18,7 @@ hipError_t launch_gen_pages(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint6
                             uint32_t ppm, hipStream_t s);
 hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        hipStream_t s, Prof* prof = nullptr);
-// Full diff of n pages (chunked internally): rec_off[n+1], data[cap].
+// Full diff of n pages in one pass: rec_off[n+1], data[cap].
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr);
@@ -43,9 +38,11 @@ hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, u
 uint64_t coh_workspace_bytes(uint64_t n_events);
 // Page table: one u64 per page, state | faults << 32.
 hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hipStream_t s);
-hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, const uint64_t* events,
-                            uint64_t n_events, uint64_t* totals, uint8_t* ws, uint64_t ws_bytes,
-                            uint32_t* err, hipStream_t s, Prof* prof = nullptr);
+// Events naming a page >= n_pages or a node >= n_nodes reject the batch (err |= 2).
+hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
+                            const uint64_t* events, uint64_t n_events, uint64_t* totals,
+                            uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
+                            Prof* prof = nullptr);
 hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,
                              uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,
                              hipStream_t s);

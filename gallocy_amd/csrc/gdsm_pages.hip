@@ -4,19 +4,13 @@
 // (resources/NUTSHELL.md:59-69); the only diff in the reference is the NW alignment
 // gallocy/utils/diff.cpp:73-167, see legacy_diff.cpp.
 //
-// Diff pipeline (all HBM-bound, no MFMA):
-//   1. diff_compact_kernel one wave per page (16 pages per wave, the next page's loads in
-//                          flight): 4 x 16 B coalesced loads of twin and current per lane,
-//                          16-bit byte-diff mask per 16-B chunk, dirty chunks compacted by
-//                          ballot into LDS, run starts/ends from the neighbour entry's edge bit,
-//                          ranks by wave prefix sums over the compacted lanes; records are built
-//                          in LDS and stored (nontemporal) to the wave's region of the
-//                          workspace, sizes to sizes[], the workgroup's sum to block_sum[].
-//                          (diff_pages_kernel: the earlier whole-page-scan kernels, variants.)
-//   2. scan_blocks_kernel  one workgroup: exclusive scan of block_sum -> block_off.
-//   3. pack_kernel         per workgroup: page offsets inside the block -> rec_off, then
-//                          copies each record from its slot to its packed place.
-// No workgroup waits on another, so nothing can hang on dispatch order.
+// Diff (HBM-bound, no MFMA): diff_single_kernel, one pass. A wave diffs a unit of 16 or 32
+// consecutive list entries (the next page's loads in flight): 4 x 16 B coalesced loads of twin and
+// current per lane, 16-bit byte-diff mask per 16-B chunk, dirty chunks compacted by ballot into
+// LDS, run starts/ends from the neighbour entry's edge bit, ranks by wave prefix sums; the record
+// image is built in the wave's LDS buffer. Its offset in the stream comes from a decoupled
+// look-back over the other waves' published totals, then the records are stored once, in place.
+// No wave waits for a ticket that a wave not yet running holds.
 #include "gdsm_common.h"
 #include "gdsm_launch.h"
 
@@ -172,10 +166,6 @@ __device__ __forceinline__ void load_page(const uint8_t* __restrict__ twin,
   }
 }
 
-// Diffs one page held in registers (chunk (k, lane) = bytes [(64k + lane) * 16, +16), page
-// order = (k, lane)); writes its record to `out` and returns the record size (wave-uniform).
-constexpr uint32_t kDiffStage = 2048;  // per-wave LDS record stage (bytes)
-
 // v_perm_b32 selectors compacting the bytes of a dword whose bit is set in a 4-bit mask to its
 // low bytes, in order; selector 0x0C yields a zero byte.
 __device__ __forceinline__ uint32_t compact_sel(uint32_t nib) {
@@ -241,14 +231,6 @@ __device__ __forceinline__ void emit_compact(uint32_t ch, uint32_t s, uint32_t e
   if (nw > 4) atomicOr(d + 4, (uint32_t)w2);
 }
 
-// a[k] for k = 2*b1 + b0 as two levels of selects on the bits of k (a select chain on k == i
-// gets rewritten into an indexed private array, i.e. scratch memory).
-__device__ __forceinline__ uint32_t sel4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                         bool b0, bool b1) {
-  const uint32_t lo = b0 ? a1 : a0, hi = b0 ? a3 : a2;
-  return b1 ? hi : lo;
-}
-
 // Run structure of one page held in registers (chunk (k, lane) = bytes [(64k + lane) * 16, +16),
 // page order = (k, lane)): per chunk the byte-diff mask m, run-start bits s, run-end bits e, the
 // exclusive ranks excl (runs ending before the chunk in the low 16 bits, changed bytes before it
@@ -310,161 +292,6 @@ __device__ __forceinline__ void emit_bytes(const PageRuns& P, const uint4 (&c)[4
     emit_chunk(k * 64 + lane, P.s[k], P.e[k], P.m[k], P.ps[k], P.excl[k], c[k], hdr, pay);
 }
 
-// Compacted emission of a whole record into an LDS image of n16 16-B words: zero it, write the
-// run count, then every lane emits its dirty chunks (one loop trip per dirty chunk of the lane,
-// all four k at once). The caller orders the image before any read (wave_lds_sync).
-__device__ __forceinline__ void emit_image(const PageRuns& P, const uint4 (&c)[4], uint32_t lane,
-                                           uint32_t* __restrict__ img, uint32_t n16,
-                                           const uint32_t* __restrict__ sel_tab) {
-  uint4* z = reinterpret_cast<uint4*>(img);
-  for (uint32_t q = lane; q < n16; q += 64) z[q] = make_uint4(0, 0, 0, 0);
-  wave_lds_sync();
-  if (lane == 0) img[0] = P.NR;
-  const uint32_t pay_base = 4u + 4u * P.NR;
-  uint32_t dm = (P.m[0] ? 1u : 0u) | (P.m[1] ? 2u : 0u) | (P.m[2] ? 4u : 0u) | (P.m[3] ? 8u : 0u);
-  while (dm) {
-    const uint32_t k = (uint32_t)__builtin_ctz(dm);
-    dm &= dm - 1;
-    const bool b0 = k & 1u, b1 = k & 2u;
-#define GDSM_SEL4(a) sel4(a[0], a[1], a[2], a[3], b0, b1)
-    const uint4 cc = make_uint4(sel4(c[0].x, c[1].x, c[2].x, c[3].x, b0, b1),
-                                sel4(c[0].y, c[1].y, c[2].y, c[3].y, b0, b1),
-                                sel4(c[0].z, c[1].z, c[2].z, c[3].z, b0, b1),
-                                sel4(c[0].w, c[1].w, c[2].w, c[3].w, b0, b1));
-    emit_compact(k * 64u + lane, GDSM_SEL4(P.s), GDSM_SEL4(P.e), GDSM_SEL4(P.m),
-                 GDSM_SEL4(P.ps), GDSM_SEL4(P.excl), cc, img, pay_base, sel_tab);
-#undef GDSM_SEL4
-  }
-}
-
-// Copies n16 16-B words from LDS to global memory (one wave, coalesced 16-B stores;
-// kNT = nontemporal stores).
-template <bool kNT = false>
-__device__ __forceinline__ void flush_lds(const uint32_t* __restrict__ src, uint32_t n16,
-                                          uint8_t* __restrict__ dst, uint32_t lane) {
-  wave_lds_sync();
-  const u32x4* s = reinterpret_cast<const u32x4*>(src);
-  u32x4* d = reinterpret_cast<u32x4*>(dst);
-  for (uint32_t q = lane; q < n16; q += 64) {
-    if (kNT)
-      __builtin_nontemporal_store(s[q], d + q);
-    else
-      d[q] = s[q];
-  }
-  wave_lds_sync();
-}
-
-// One workgroup = 4 waves = kDiffPagesPerBlock consecutive pages; wave w takes the 16 pages
-// [16w, 16w + 16) of the block in order and appends their records, each rounded up to 16 B, to
-// its own region of the workspace (16 slots = the worst case), which the pack kernel then reads
-// as near-contiguous memory.
-// kVar (launcher variants 1-4):
-//   0  records compacted in registers, OR-ed into a per-wave LDS accumulation buffer of
-//      kDiffAcc bytes and written out only when it fills and after the wave's last page: the
-//      stores are whole, contiguous lines
-//   2  byte-loop emission (emit_bytes) into the LDS stage, written out per record
-//   3  MEASUREMENT ONLY: full run scan, records not written (sizes only) -- output is invalid
-//   4  MEASUREMENT ONLY: loads + a change count per page -- the read roofline of this kernel
-constexpr uint32_t kDiffAcc = 4096;  // per-wave LDS accumulation buffer (bytes)
-
-template <int kVar>
-__device__ __forceinline__ void diff_pages_body(
-    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
-    const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
-  static_assert(kVar == 0 || kVar == 2 || kVar == 3 || kVar == 4, "diff variant");
-  constexpr uint32_t kBuf = kVar == 0 ? kDiffAcc : kDiffStage;
-  __shared__ uint32_t wsum[4];
-  __shared__ uint32_t sel_tab[16];
-  __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kBuf / 4];
-  if (threadIdx.x < 16) sel_tab[threadIdx.x] = compact_sel(threadIdx.x);
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* buf = buf_all[wave];
-  const uint64_t w0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock + wave * kDiffPagesPerWave;
-  uint8_t* region = ws + w0 * kRecSlot;
-  uint32_t acc = 0;      // record bytes of the wave's pages so far
-  uint32_t acc16 = 0;    // region bytes of the wave's pages so far (records rounded to 16 B)
-  uint32_t flushed = 0;  // region bytes already stored (variant 0); buffer = [flushed, acc16)
-  uint32_t my_size = 0;  // lane j: size of the wave's page j
-  const uint32_t cnt = (uint32_t)min((uint64_t)kDiffPagesPerWave, n > w0 ? n - w0 : 0);
-  for (uint32_t j = 0; j < cnt; ++j) {
-    const uint64_t i = w0 + j;  // index within chunk
-    uint4 t[4], c[4];
-    load_page(twin, cur, ids ? ids[first + i] : first + i, lane, t, c);
-    uint32_t size;
-    if constexpr (kVar == 4) {
-      uint32_t d = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        d |= (t[k].x ^ c[k].x) | (t[k].y ^ c[k].y) | (t[k].z ^ c[k].z) | (t[k].w ^ c[k].w);
-      size = wave_sum(d ? 1u : 0u);
-    } else {
-      PageRuns P;
-      scan_page(t, c, lane, P);
-      size = record_size(P);
-      const uint32_t n16 = (size + 15u) >> 4;
-      if constexpr (kVar == 3) {  // keep the emission inputs alive, store nothing
-        uint32_t h = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) h ^= P.s[k] ^ P.e[k] ^ P.ps[k] ^ P.excl[k] ^ c[k].x;
-        size += (wave_sum(h) == 0x9E3779B9u) ? 4u : 0u;
-      } else if (size != 0) {
-        if (16u * n16 > kBuf) {
-          // larger than the buffer: emitted straight to its place, byte by byte
-          if (kVar == 0 && acc16 > flushed) {
-            flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
-            flushed = acc16;
-          }
-          emit_bytes(P, c, lane, region + acc16);
-          if (kVar == 0) flushed = acc16 + 16u * n16;
-        } else if constexpr (kVar == 0) {
-          if (acc16 - flushed + 16u * n16 > kBuf) {
-            flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
-            flushed = acc16;
-          }
-          emit_image(P, c, lane, buf + (acc16 - flushed) / 4, n16, sel_tab);
-        } else {
-          emit_bytes(P, c, lane, reinterpret_cast<uint8_t*>(buf));
-          flush_lds(buf, n16, region + acc16, lane);
-        }
-      }
-    }
-    if (lane == j) my_size = size;
-    acc += size;
-    acc16 += (size + 15u) & ~15u;
-  }
-  if (kVar == 0 && acc16 > flushed) flush_lds(buf, (acc16 - flushed) >> 4, region + flushed, lane);
-  if (lane < cnt) sizes[w0 + lane] = my_size;
-  if (lane == 0) wsum[wave] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) block_sum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-}
-
-template <int kVar>
-__global__ __launch_bounds__(256) void diff_pages_kernel(
-    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
-    const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
-  diff_pages_body<kVar>(twin, cur, ids, first, n, ws, sizes, block_sum);
-}
-
-// ---- compacted diff (launcher variants 0, 5, 6): work only on the page's dirty 16-B chunks.
-// After the byte-diff masks are built, a ballot per k ranks the dirty chunks in page order and
-// each dirty lane parks (chunk << 16 | mask) and its current bytes in the wave's LDS list. Run
-// starts/ends, ranks and emission then run over the compacted lanes, so a sparse page costs one
-// pair of wave scans instead of four, and the page's registers die right after the masks (the
-// next page's loads are in flight meanwhile: kPrefetch). Records go out with nontemporal stores
-// (kStore 2): measured 0.05 ms per 1M pages faster than plain stores, and the following pack
-// and the previous step's apply write-back no longer slow the diff (scripts/ab_step.py).
-// A page with more than 64 dirty chunks (over a quarter of the page changed) is only sized here
-// (its size is flagged with kSlowPage in sizes[] and it takes no room in the wave's region); the
-// pack kernel, which knows its final offset, emits it straight from the arenas (emit_bytes).
-constexpr uint32_t kSlowPage = 0x80000000u;
-// Per-wave LDS record buffer (bytes): holds the largest record of a page with <= 64 dirty chunks
-// (4 + 4 * 512 runs + 1024 payload bytes = 3076, rounded to 16 B).
-constexpr uint32_t kCAcc = 3088;
-
 // Size of the record of a page whose byte-diff masks m[k] (chunk (k, lane)) are in registers
 // (the run ends need the next chunk's first bit: DPP from lane + 1, wrapping across k).
 __device__ __forceinline__ uint32_t record_size_masks(const uint32_t (&m)[4], uint32_t lane) {
@@ -479,107 +306,6 @@ __device__ __forceinline__ uint32_t record_size_masks(const uint32_t (&m)[4], ui
   const uint32_t tot = wave_sum(v);
   const uint32_t NR = tot & 0xFFFFu, NP = tot >> 16;
   return NR ? 4u + 4u * NR + ((NP + 3u) & ~3u) : 0u;
-}
-
-template <bool kPrefetch, int kStore>
-__device__ __forceinline__ void diff_compact_body(
-    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
-    const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
-  __shared__ uint32_t wsum[4];
-  __shared__ uint32_t sel_tab[16];
-  __shared__ uint32_t ent_all[4][64];
-  __shared__ uint4 dat_all[4][64];
-  __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kCAcc / 4];
-  if (threadIdx.x < 16) sel_tab[threadIdx.x] = compact_sel(threadIdx.x);
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* ent = ent_all[wave];
-  uint4* dat = dat_all[wave];
-  uint32_t* buf = buf_all[wave];
-  const uint64_t w0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock + wave * kDiffPagesPerWave;
-  uint8_t* region = ws + w0 * kRecSlot;
-  uint32_t acc = 0;      // record bytes of the wave's pages so far
-  uint32_t acc16 = 0;    // region bytes used so far (records rounded to 16 B; slow pages: none)
-  uint32_t flushed = 0;  // region bytes already stored; the LDS buffer holds [flushed, acc16)
-  uint32_t my_size = 0;  // lane j: size (| kSlowPage) of the wave's page j
-  const uint32_t cnt = (uint32_t)min((uint64_t)kDiffPagesPerWave, n > w0 ? n - w0 : 0);
-  uint4 t[4], c[4];
-  if (kPrefetch && cnt) load_page(twin, cur, ids ? ids[first + w0] : first + w0, lane, t, c);
-  for (uint32_t j = 0; j < cnt; ++j) {
-    if (!kPrefetch) load_page(twin, cur, ids ? ids[first + w0 + j] : first + w0 + j, lane, t, c);
-    uint32_t m[4], D = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      m[k] = diffmask16(t[k], c[k]);
-      const uint64_t B = __ballot(m[k] != 0u);
-      const uint32_t rank = D + __builtin_amdgcn_mbcnt_hi(
-                                    (uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
-      if (m[k] && rank < 64u) {
-        ent[rank] = ((uint32_t)(k * 64 + lane) << 16) | m[k];
-        dat[rank] = c[k];
-      }
-      D += (uint32_t)__popcll(B);
-    }
-    if (kPrefetch && j + 1 < cnt)
-      load_page(twin, cur, ids ? ids[first + w0 + j + 1] : first + w0 + j + 1, lane, t, c);
-    uint32_t size = 0, flag = 0;
-    if (D > 64u) {
-      size = record_size_masks(m, lane);
-      flag = kSlowPage;
-    } else if (D) {
-      wave_lds_sync();
-      const bool valid = lane < D;
-      const uint32_t E = valid ? ent[lane] : 0u;
-      const uint32_t Ep = from_prev_lane(E), En = from_next_lane(E);
-      const uint32_t g = E >> 16, mm = E & 0xFFFFu;
-      const uint32_t up = (Ep != 0u && (Ep >> 16) + 1u == g) ? (Ep >> 15) & 1u : 0u;
-      const uint32_t dn = (En != 0u && (En >> 16) == g + 1u) ? En & 1u : 0u;
-      const uint32_t s = mm & ~((mm << 1) | up) & 0xFFFFu;
-      const uint32_t e = mm & ~((mm >> 1) | (dn << 15)) & 0xFFFFu;
-      const uint32_t v = (uint32_t)__popc(e) | ((uint32_t)__popc(mm) << 16);
-      const uint32_t inc = wave_incl_sum(v);
-      const uint32_t tot = lane_bcast(inc, 63);
-      const uint32_t ls = s ? g * 16u + 32u - (uint32_t)__builtin_clz(s) : 0u;
-      const uint32_t ps = from_prev_lane(wave_incl_max(ls));
-      const uint32_t NR = tot & 0xFFFFu, NP = tot >> 16;
-      size = 4u + 4u * NR + ((NP + 3u) & ~3u);
-      const uint32_t rec16 = (size + 15u) & ~15u;
-      if (acc16 - flushed + rec16 > kCAcc) {
-        if (kStore != 1) flush_lds<kStore == 2>(buf, (acc16 - flushed) >> 4, region + flushed, lane);
-        flushed = acc16;
-      }
-      uint32_t* img = buf + (acc16 - flushed) / 4u;
-      uint4* z = reinterpret_cast<uint4*>(img);
-      for (uint32_t q = lane; q < rec16 >> 4; q += 64) z[q] = make_uint4(0, 0, 0, 0);
-      const uint4 cc = valid ? dat[lane] : make_uint4(0, 0, 0, 0);
-      wave_lds_sync();
-      if (lane == 0) img[0] = NR;
-      if (valid) emit_compact(g, s, e, mm, ps, inc - v, cc, img, 4u + 4u * NR, sel_tab);
-      wave_lds_sync();
-      acc16 += rec16;
-    }
-    if (lane == j) my_size = size | flag;
-    acc += size;
-  }
-  if (acc16 > flushed) {
-    if (kStore != 1) flush_lds<kStore == 2>(buf, (acc16 - flushed) >> 4, region + flushed, lane);
-    else if (wave_sum(buf[lane]) == 0x9E3779B9u) sizes[0] = 0;  // keep the LDS work alive
-  }
-  if (lane < cnt) sizes[w0 + lane] = my_size;
-  if (lane == 0) wsum[wave] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) block_sum[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-}
-
-// kStore: 0 = plain record stores, 1 = MEASUREMENT ONLY: no record stores, 2 = nontemporal.
-// kWaves: occupancy target handed to the register allocator (waves per SIMD).
-template <bool kPrefetch, int kStore, int kWaves = 4>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_compact_kernel(
-    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
-    const uint32_t* __restrict__ ids, uint64_t first, uint64_t n, uint8_t* __restrict__ ws,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ block_sum) {
-  diff_compact_body<kPrefetch, kStore>(twin, cur, ids, first, n, ws, sizes, block_sum);
 }
 
 // ---- single-pass diff (default): every record is written straight to its final place in the
@@ -597,8 +323,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
 // from LDS to the stream with coalesced dword stores (nontemporal), and re-reads its late pages
 // from the arenas to emit them byte-wise in place. No wave ever waits for a ticket that a
 // non-running wave holds, so the look-back cannot deadlock whatever the dispatch order.
-constexpr uint32_t kSpU = 16;          // list entries per unit (one wave)
-constexpr uint32_t kSpBuf = 8192;      // per-wave LDS record buffer (bytes)
 constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStVal = (1ull << 62) - 1;
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
@@ -765,152 +489,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     PageRuns P;
     scan_page(t, c, lane, P);
     emit_bytes(P, c, lane, data + excl + tab[j]);
-  }
-}
-
-// One workgroup: block_off[b] = base + sum(block_sum[0..b)), base = rec_off[first].
-// Thread t owns blocks [16t, 16t + 16) (four 16-B loads), sums them, the 1024 thread sums are
-// scanned by DPP inside each wave and through LDS across the 16 waves, then every thread writes
-// its 16 offsets. Block sums are < 2^32 each, offsets are u64. nb <= 16384 (kDiffChunk / 64).
-__global__ __launch_bounds__(1024) void scan_blocks_kernel(const uint32_t* __restrict__ block_sum,
-                                                           uint64_t nb,
-                                                           const uint64_t* __restrict__ base_ptr,
-                                                           uint64_t* __restrict__ block_off) {
-  __shared__ uint64_t wtot[16];
-  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint64_t b0 = (uint64_t)t * 16;
-  uint32_t v[16];
-  const bool vec = (reinterpret_cast<uintptr_t>(block_sum) & 15) == 0;
-  if (vec && b0 + 16 <= nb) {
-    const uint4* src = reinterpret_cast<const uint4*>(block_sum + b0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 x = src[q];
-      v[4 * q] = x.x;
-      v[4 * q + 1] = x.y;
-      v[4 * q + 2] = x.z;
-      v[4 * q + 3] = x.w;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = (b0 + q < nb) ? block_sum[b0 + q] : 0u;
-  }
-  uint64_t s = 0;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) s += v[q];
-  // A 32-bit wave scan suffices: a wave covers 64 x 16 blocks of <= 64 records of <= 10244 B,
-  // i.e. < 6.8e8 B.
-  const uint32_t inc = wave_incl_sum((uint32_t)s);
-  if (lane == 63) wtot[wave] = inc;
-  __syncthreads();
-  uint64_t pre = base_ptr ? *base_ptr : 0;
-  for (uint32_t w = 0; w < wave; ++w) pre += wtot[w];
-  uint64_t run = pre + inc - (uint32_t)s;
-  if (b0 + 16 <= nb) {
-    uint64_t o[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      o[q] = run;
-      run += v[q];
-    }
-    ulonglong2* dst = reinterpret_cast<ulonglong2*>(block_off + b0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dst[q] = make_ulonglong2(o[2 * q], o[2 * q + 1]);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      if (b0 + q < nb) {
-        block_off[b0 + q] = run;
-        run += v[q];
-      }
-  }
-}
-
-// Per workgroup (64 pages): page offsets inside the block -> rec_off; then every thread copies
-// output dwords of the block's packed range, finding each dword's record by binary search over
-// the 65 block-relative offsets in LDS (all loads independent, stores contiguous). A record's
-// source is its wave region (diff kernels) at the 16-B rounded prefix `src` of its row. Pages
-// flagged kSlowPage (compacted diff: > 64 dirty chunks) have no region copy: one wave re-reads
-// the page and emits its record straight into the packed stream.
-__global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ ws,
-                                                   const uint32_t* __restrict__ sizes,
-                                                   const uint64_t* __restrict__ block_off,
-                                                   uint64_t first, uint64_t n,
-                                                   uint64_t* __restrict__ rec_off,
-                                                   uint8_t* __restrict__ data, uint64_t cap,
-                                                   const uint8_t* __restrict__ twin,
-                                                   const uint8_t* __restrict__ cur,
-                                                   const uint32_t* __restrict__ ids) {
-  __shared__ uint32_t off[kDiffPagesPerBlock + 1];
-  __shared__ uint32_t src[kDiffPagesPerBlock];
-  __shared__ uint64_t slow_mask;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t b0 = (uint64_t)blockIdx.x * kDiffPagesPerBlock;
-  const uint64_t base = block_off[blockIdx.x];
-  if (wave == 0) {
-    static_assert(kDiffPagesPerWave == 16, "one DPP row per wave region");
-    const uint64_t i = b0 + lane;
-    const uint32_t raw = (i < n) ? sizes[i] : 0u;
-    const bool slow = (raw & kSlowPage) != 0u;
-    const uint32_t sz = raw & ~kSlowPage;
-    const uint32_t inc = wave_incl_sum(sz);
-    const uint32_t s16 = slow ? 0u : (sz + 15u) & ~15u;
-    src[lane] = row_incl_sum(s16) - s16;
-    off[lane] = inc - sz;
-    if (lane == 63) off[64] = inc;
-    const uint64_t sm = __ballot(slow);
-    if (lane == 0) slow_mask = sm;
-    if (i < n) rec_off[first + i + 1] = base + inc;
-    if (first == 0 && blockIdx.x == 0 && lane == 0) rec_off[0] = 0;
-  }
-  __syncthreads();
-  const uint64_t sm = slow_mask;
-  // Only records that end inside the capacity are copied.
-  uint32_t limit = off[64];
-  if (base + limit > cap) {
-    limit = 0;
-    for (uint32_t r = 0; r < kDiffPagesPerBlock; ++r)
-      if (base + off[r + 1] <= cap) limit = off[r + 1];
-  }
-  // kPackU dwords per thread per pass, every load issued before the first store: a typical
-  // block (64 records of ~66 B) is one pass, i.e. one memory round trip instead of four.
-  constexpr uint32_t kPackU = 8;
-  uint32_t* dst = reinterpret_cast<uint32_t*>(data + base);
-  const uint32_t ndw = limit / 4;
-  for (uint32_t g0 = threadIdx.x; g0 < ndw; g0 += 256 * kPackU) {
-    uint32_t v[kPackU];
-    uint32_t live = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < kPackU; ++u) {
-      const uint32_t g = g0 + u * 256;
-      v[u] = 0;
-      if (g < ndw) {
-        const uint32_t byte = g * 4;
-        uint32_t r = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1)
-          if (off[r + step] <= byte) r += step;
-        if (!((sm >> r) & 1u)) {
-          v[u] = *reinterpret_cast<const uint32_t*>(
-              ws + (b0 + (r & ~(kDiffPagesPerWave - 1))) * kRecSlot + src[r] + (byte - off[r]));
-          live |= 1u << u;
-        }
-      }
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kPackU; ++u)
-      if ((live >> u) & 1u) dst[g0 + u * 256] = v[u];
-  }
-  for (uint64_t rem = sm; rem;) {  // wave-uniform
-    const uint32_t r = (uint32_t)__builtin_ctzll(rem);
-    rem &= rem - 1;
-    if ((r & 3u) != wave || base + off[r + 1] > cap) continue;
-    const uint64_t i = first + b0 + r;
-    uint4 t[4], c[4];
-    load_page(twin, cur, ids ? ids[i] : i, lane, t, c);
-    PageRuns P;
-    scan_page(t, c, lane, P);
-    emit_bytes(P, c, lane, data + base + off[r]);
   }
 }
 
@@ -1124,43 +702,33 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
 }
 
 // ------------------------------------------------------------------------- launchers
-// Diff kernel variant, gdsm_tune("diff_variant", v) or GDSM_DIFF_VARIANT=v (in-process A/B,
-// scripts/ab_diff.py):
-//   0  compacted, next page's loads in flight, nontemporal record stores, 5 waves/SIMD (default)
-//   1  per-chunk scans over the whole page, records OR-ed into a per-wave LDS buffer
-//   2  as 1 with byte-loop emission
-//   3  MEASUREMENT ONLY: variant 1's full run scan, records not written (output invalid)
-//   4  MEASUREMENT ONLY: loads + a change count per page (the read roofline of this kernel)
-//   5  compacted, one page at a time, plain stores, 8 waves/SIMD
-//   6  MEASUREMENT ONLY: variant 0 without the record stores
-//   7  variant 0 with plain (temporal) record stores
+// Diff geometry, gdsm_tune("diff_variant", v) or GDSM_DIFF_VARIANT=v; every variant writes the
+// same canonical stream (tests/test_gpu_pages.py checks each):
+//   0  automatic (default): 32 pages per wave when the caller's stream capacity allows at most
+//      384 B per page (sparse writes: config 2's ~66 B records; fewer look-backs), else 16
+//   1  16 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
+//   2  32 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
+// Measurement-only kernels (invalid output) are not part of the library.
 static int g_diff_variant = -1;
 static int diff_variant() {
   if (g_diff_variant < 0) {
     const char* e = getenv("GDSM_DIFF_VARIANT");
-    g_diff_variant = e ? atoi(e) : 0;
-    if (g_diff_variant < 0 || g_diff_variant > 12) g_diff_variant = 0;
+    const int v = e ? atoi(e) : 0;
+    g_diff_variant = (v >= 0 && v <= 2) ? v : 0;
   }
   return g_diff_variant;
 }
-// Apply kernel variant: 0 = normal; 1 = MEASUREMENT ONLY, no replica stores; 2 = nt stores.
-static int g_apply_variant = 0;
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "apply_variant") && value >= 0 && value <= 2) {
-    g_apply_variant = (int)value;
-    return 0;
-  }
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 12) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 2) {
     g_diff_variant = (int)value;
     return 0;
   }
   return coh_tune(key, value);
 }
 
-uint64_t diff_workspace_bytes(uint64_t n_chunk) {
-  const uint64_t nb = (n_chunk + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
-  return n_chunk * kRecSlot + n_chunk * 4 + nb * 4 + nb * 8 + 64;
-}
+// Single-pass diff workspace: the ticket counter and one status granule per 16-page unit (the
+// smaller unit, so any geometry fits).
+uint64_t diff_workspace_bytes(uint64_t n) { return 8 * (1 + (n + 15) / 16) + 64; }
 
 static inline unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap) {
   uint64_t g = (work + per_block - 1) / per_block;
@@ -1207,72 +775,18 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
-  if (diff_variant() == 0) {
-    // single pass: ws = ticket counter + one status granule per unit, zeroed per launch
-    const uint64_t nunits = (n + kSpU - 1) / kSpU;
-    if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
-    if (e != hipSuccess) return e;
-    ProfScope ps(prof, 0, s);
-    hipLaunchKernelGGL((diff_single_kernel<kSpU, kSpBuf, 4>), dim3((unsigned)((nunits + 3) / 4)),
-                       dim3(256), 0, s, twin, cur, ids, n, rec_off, data, cap,
-                       reinterpret_cast<uint64_t*>(ws));
-    return hipGetLastError();
-  }
-  if (diff_variant() >= 9) {  // single-pass geometry A/B: (pages per wave, LDS bytes, waves/SIMD)
-    typedef void (*K)(const uint8_t*, const uint8_t*, const uint32_t*, uint64_t, uint64_t*,
-                      uint8_t*, uint64_t, uint64_t*);
-    static const K kk[] = {diff_single_kernel<8, 6144, 5>, diff_single_kernel<16, 6144, 5>,
-                           diff_single_kernel<8, 4096, 6>, diff_single_kernel<32, 8192, 4>};
-    static const uint32_t uu[] = {8, 16, 8, 32};
-    const int v = diff_variant() - 9;
-    const uint64_t nunits = (n + uu[v] - 1) / uu[v];
-    if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
-    if (e != hipSuccess) return e;
-    ProfScope ps(prof, 0, s);
-    hipLaunchKernelGGL(kk[v], dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids,
-                       n, rec_off, data, cap, reinterpret_cast<uint64_t*>(ws));
-    return hipGetLastError();
-  }
-  // Largest chunk whose workspace fits.
-  uint64_t chunk = n < kDiffChunk ? n : kDiffChunk;
-  while (chunk > kDiffPagesPerBlock && diff_workspace_bytes(chunk) > ws_bytes) chunk >>= 1;
-  if (diff_workspace_bytes(chunk) > ws_bytes) return hipErrorInvalidValue;
-  const uint64_t nbmax = (chunk + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
-  uint8_t* slots = ws;
-  uint32_t* sizes = reinterpret_cast<uint32_t*>(ws + chunk * kRecSlot);
-  uint32_t* block_sum = sizes + chunk;
-  uint64_t* block_off =
-      reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(block_sum + nbmax) + 15) & ~15ull);
-  for (uint64_t first = 0; first < n; first += chunk) {
-    const uint64_t m = (n - first < chunk) ? n - first : chunk;
-    const uint64_t nb = (m + kDiffPagesPerBlock - 1) / kDiffPagesPerBlock;
-    {
-      ProfScope ps(prof, 0, s);
-      // gdsm_tune("diff_variant", v): see diff_variant() above
-      static void (*const kVariants[])(const uint8_t*, const uint8_t*, const uint32_t*, uint64_t,
-                                       uint64_t, uint8_t*, uint32_t*, uint32_t*) = {
-          diff_compact_kernel<true, 2, 5>, diff_pages_kernel<0>,
-          diff_pages_kernel<2>,            diff_pages_kernel<3>,
-          diff_pages_kernel<4>,            diff_compact_kernel<false, 0, 4>,
-          diff_compact_kernel<true, 1, 5>, diff_compact_kernel<true, 0, 5>,
-          diff_compact_kernel<true, 2, 5>};
-      auto kern = kVariants[diff_variant()];
-      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, twin, cur, ids, first, m,
-                         slots, sizes, block_sum);
-    }
-    {
-      ProfScope ps(prof, 1, s);
-      hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, s, block_sum, nb,
-                         first ? rec_off + first : nullptr, block_off);
-    }
-    {
-      ProfScope ps(prof, 2, s);
-      hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nb), dim3(256), 0, s, slots, sizes,
-                         block_off, first, m, rec_off, data, cap, twin, cur, ids);
-    }
-  }
+  int v = diff_variant();
+  if (v == 0) v = (cap <= 384 * n) ? 2 : 1;
+  const uint32_t U = v == 2 ? 32 : 16;
+  const uint64_t nunits = (n + U - 1) / U;
+  if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
+  // ticket counter + status granules, zeroed per launch (outside the timed kernel)
+  hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
+  if (e != hipSuccess) return e;
+  ProfScope ps(prof, 0, s);
+  auto kern = v == 2 ? diff_single_kernel<32, 8192, 4> : diff_single_kernel<16, 8192, 4>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, n,
+                     rec_off, data, cap, reinterpret_cast<uint64_t*>(ws));
   return hipGetLastError();
 }
 
@@ -1281,9 +795,7 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
   ProfScope ps(prof, 3, s);
-  auto kern = g_apply_variant == 1 ? apply_kernel<1> : g_apply_variant == 2 ? apply_kernel<2>
-                                                                              : apply_kernel<0>;
-  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, target, ids, n,
+  hipLaunchKernelGGL(apply_kernel<0>, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, target, ids, n,
                      rec_off, data, err);
   return hipGetLastError();
 }

@@ -235,8 +235,8 @@ void or_coh_init(uint32_t* state, uint32_t* faults, uint64_t n_pages, uint32_t n
   }
 }
 
-int or_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages, const uint64_t* events,
-                 uint64_t n_events, uint64_t* totals) {
+int or_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages, uint32_t n_nodes,
+                 const uint64_t* events, uint64_t n_events, uint64_t* totals) {
   for (int k = 0; k < 10; ++k) totals[k] = 0;
   uint64_t last_page = 0;
   for (uint64_t i = 0; i < n_events; ++i) {
@@ -244,7 +244,7 @@ int or_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages, const uint
     const uint64_t p = e >> 4;
     const uint32_t node = (uint32_t)((e >> 1) & 7u);
     const int wr = (int)(e & 1u);
-    if (p >= n_pages || (i && p < last_page)) return -22;
+    if (p >= n_pages || (i && p < last_page) || node >= n_nodes) return -22;
     last_page = p;
     uint32_t s = state[p];
     uint32_t cs = s & 0xffu, owner = (s >> 8) & 0xffu, st = (s >> 16) & 3u, dirty = (s >> 18) & 1u;

@@ -53,9 +53,10 @@ int or_nw_diff(const char* m1, size_t n1, const char* m2, size_t n2, char* out1,
 /* SPEC §5. */
 void or_coh_init(uint32_t* state, uint32_t* faults, uint64_t n_pages, uint32_t n_nodes);
 /* totals[0] = invalidations, totals[1] = transfers, totals[2..10) = node faults.
- * Returns 0, or -22 if the batch is not sorted by page or names a page/node out of range. */
-int or_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages, const uint64_t* events,
-                 uint64_t n_events, uint64_t* totals);
+ * Returns 0, or -22 if the batch is not sorted by page or names a page >= n_pages or a node
+ * >= n_nodes (the state is then partly folded). */
+int or_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages, uint32_t n_nodes,
+                 const uint64_t* events, uint64_t n_events, uint64_t* totals);
 
 /* SPEC §6 event fill from per-page counts; offsets = exclusive scan of counts (n+1). */
 void or_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page, uint64_t n,

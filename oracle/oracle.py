@@ -32,7 +32,7 @@ def lib():
         L.or_nw_diff.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p,
                                  C.c_char_p, C.POINTER(C.c_size_t)]
         L.or_coh_init.argtypes = [vp, vp, u64, C.c_uint32]
-        L.or_coherence.argtypes = [vp, vp, u64, vp, u64, vp]
+        L.or_coherence.argtypes = [vp, vp, u64, C.c_uint32, vp, u64, vp]
         L.or_gen_events.argtypes = [vp, vp, u64, u64, u64, C.c_uint32, C.c_uint32]
         _lib = L
     return _lib
@@ -88,10 +88,11 @@ def coh_init(n_pages, n_nodes=8):
     return st, fl
 
 
-def coherence(state, faults, events):
+def coherence(state, faults, events, n_nodes=8):
     ev = np.ascontiguousarray(events, np.uint64)
     tot = np.zeros(10, np.uint64)
-    rc = lib().or_coherence(_p(state), _p(faults), len(state), _p(ev) if len(ev) else None, len(ev), _p(tot))
+    rc = lib().or_coherence(_p(state), _p(faults), len(state), n_nodes,
+                            _p(ev) if len(ev) else None, len(ev), _p(tot))
     return rc, {"invalidations": int(tot[0]), "transfers": int(tot[1]),
                 "node_faults": [int(x) for x in tot[2:]]}
 

@@ -1,8 +1,8 @@
 """Per-kernel times of the config-2 step in one process (HIP events from libgdsm's profiler):
 diff alone, apply alone (re-applying the same stream is idempotent), and the serial step
-diff -> scan -> pack -> apply, so that the cost one kernel leaves to the next shows up.
+diff -> apply, so that the cost one kernel leaves to the next shows up.
 
-    python scripts/ab_step.py [apply_variant values, e.g. 0,1]"""
+    AB_MODE=clustered python scripts/ab_step.py"""
 import statistics
 import sys
 from pathlib import Path
@@ -25,7 +25,6 @@ ctx.diff(out=runs)
 ctx.apply(runs)
 ctx.sync()
 REPS = 10
-AV = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0]
 
 
 def measure(fn):
@@ -49,11 +48,7 @@ res = {}
 for r in range(3):
     for name, fn in [("diff", lambda: ctx.diff(out=runs)), ("step", step)]:
         res.setdefault(name, []).append(measure(fn))
-    for v in AV:
-        assert gdsm.lib().gdsm_tune(b"apply_variant", v) == 0
-        res.setdefault(f"apply{v}", []).append(measure(lambda: ctx.apply(runs)))
-        res.setdefault(f"step_apply{v}", []).append(measure(step))
-    gdsm.lib().gdsm_tune(b"apply_variant", 0)
+    res.setdefault("apply", []).append(measure(lambda: ctx.apply(runs)))
 for name, lst in res.items():
     keys = lst[0].keys()
     print(name, {k: statistics.median(d[k] for d in lst) for k in keys}, flush=True)

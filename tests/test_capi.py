@@ -93,10 +93,12 @@ def test_no_gpu_is_reported_not_crashed():
 
 
 def test_workspace_sizing():
+    """gdsm_diff_workspace_bytes(n) for the single-pass diff."""
     from gallocy_amd import _lib
     lib = _lib.load()
-    assert lib.gdsm_diff_workspace_bytes(1) >= 10244
-    assert lib.gdsm_diff_workspace_bytes(1 << 24) == lib.gdsm_diff_workspace_bytes(1 << 20)
+    # single-pass diff: a ticket counter and one 8-B look-back granule per 16 pages
+    assert lib.gdsm_diff_workspace_bytes(1) >= 16
+    assert lib.gdsm_diff_workspace_bytes(1 << 24) == 8 * (1 + (1 << 20)) + 64
 
 
 CALLER = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "legacy_caller"
@@ -112,3 +114,16 @@ def test_legacy_caller_on_gallocy_internal_heap():
     r = subprocess.run([str(CALLER)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("ok ")
+
+
+def test_tune_rejects_measurement_only_variants():
+    """Kernels that do not produce valid output are not selectable in the product library
+    (they exist only in a -DGDSM_MEASURE build); the valid variants are."""
+    from gallocy_amd import _lib
+    L = _lib.load()
+    for key, bad in ((b"coh_variant", 2), (b"coh_variant", 3), (b"diff_variant", 3),
+                     (b"apply_variant", 1), (b"no_such_knob", 0)):
+        assert L.gdsm_tune(key, bad) == -22, (key, bad)
+    for key, ok in ((b"diff_variant", 1), (b"diff_variant", 2), (b"coh_variant", 1)):
+        assert L.gdsm_tune(key, ok) == 0
+    assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0

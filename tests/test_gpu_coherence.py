@@ -1,5 +1,7 @@
 """GPU parity of the batched page-coherence state machine (docs/SPEC.md §5) against the C oracle
 fold, through the C-ABI. Bit-exact: page-table words, per-page faults and the batch totals."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -17,7 +19,7 @@ def _run_both(n_pages, batches, n_nodes=8):
         st, fl = oracle.coh_init(n_pages, n_nodes)
         for ev in batches:
             tot = c.coherence_batch(ev)
-            rc, otot = oracle.coherence(st, fl, ev)
+            rc, otot = oracle.coherence(st, fl, ev, n_nodes=n_nodes)
             assert rc == 0
             assert tot == otot
         gst, gfl = c.coh_download()
@@ -100,6 +102,58 @@ def test_unsorted_batch_is_rejected():
         assert ei.value.errno == 22
         with pytest.raises(GdsmError):
             c.coherence_batch(np.array([99 << 4], np.uint64))  # page out of range
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_node_outside_the_table_is_rejected(variant):
+    """gdsm_coherence_batch rejects an event naming a node >= the n_nodes of gdsm_coh_init, like
+    the oracle (both pass-C kernels)."""
+    L = ga.gdsm.lib()
+    assert L.gdsm_tune(b"coh_variant", variant) == 0
+    try:
+        with ga.Context(16, arenas=()) as c:
+            c.coh_init(3)
+            with pytest.raises(GdsmError) as ei:
+                c.coherence_batch(np.array([(1 << 4) | (3 << 1), (2 << 4) | (7 << 1) | 1],
+                                           np.uint64))
+            assert ei.value.errno == 22
+            c.coh_init(3)
+            c.coherence_batch(np.array([(1 << 4) | (2 << 1)], np.uint64))
+    finally:
+        L.gdsm_tune(b"coh_variant", 0)
+
+
+@pytest.mark.parametrize("unaligned", [False, True])
+def test_variant1_and_unaligned_events_match_oracle(unaligned):
+    """Pass-C variant 1 (coh_apply_kernel, the persistent block-scan kernel) and the path taken for
+    event arrays that are not 16-B aligned (coh_apply_kernel<false>) are bit-exact too."""
+    L = ga.gdsm.lib()
+    n = 5000
+    counts = zipf_counts(n, 90000, seed=4)
+    host = oracle.gen_events(counts, seed=9, n_nodes=8, write_pct=25)
+    if not unaligned:
+        assert L.gdsm_tune(b"coh_variant", 1) == 0
+    try:
+        with ga.Context(n, arenas=()) as c:
+            c.coh_init(8)
+            buf = c.buffer(8 * (len(host) + 1))
+            if unaligned:  # one u64 in: 8-B aligned, not 16-B aligned
+                padded = np.concatenate([np.zeros(1, np.uint64), host])
+                buf.upload(padded)
+                ptr = buf.ptr + 8
+            else:
+                buf.upload(host)
+                ptr = buf.ptr
+            tot = (C.c_uint64 * 10)()
+            assert L.gdsm_coherence_batch(c.handle, ptr, len(host), tot) == 0
+            st, fl = oracle.coh_init(n, 8)
+            rc, otot = oracle.coherence(st, fl, host)
+            assert rc == 0
+            assert list(tot) == [otot["invalidations"], otot["transfers"], *otot["node_faults"]]
+            gst, gfl = c.coh_download()
+            assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+    finally:
+        L.gdsm_tune(b"coh_variant", 0)
 
 
 def test_out_of_range_page_writes_nothing():

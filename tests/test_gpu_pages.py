@@ -151,19 +151,22 @@ def test_out_of_range_page_ids_touch_no_listed_page_and_fail():
         c.sync()  # the error word was cleared
 
 
-def test_chunked_diff_small_workspace():
-    """The diff loops over chunks when its workspace is small (raw C-ABI entry point)."""
+def test_raw_diff_workspace_contract():
+    """gdsm_diff_raw with the workspace gdsm_diff_workspace_bytes(n) names works; a smaller one is
+    rejected with -EINVAL before anything runs."""
     n = 1000
     t, cur = oracle.gen_pages(n, seed=12, mode=0, ppm=40000)
     L = _lib.load()
     with ga.Context(n) as c:
         c.upload("twin", t)
         c.upload("current", cur)
-        ws_bytes = L.gdsm_diff_workspace_bytes(128)
+        ws_bytes = L.gdsm_diff_workspace_bytes(n)
         ws = c.buffer(ws_bytes)
         ro_buf = c.buffer((n + 1) * 8)
         cap = n * 2048
         data_buf = c.buffer(cap)
+        assert L.gdsm_diff_raw(c.arena_ptr("twin"), c.arena_ptr("current"), None, n, ro_buf.ptr,
+                               data_buf.ptr, cap, ws.ptr, 64, c.stream) == -22
         rc = L.gdsm_diff_raw(c.arena_ptr("twin"), c.arena_ptr("current"), None, n, ro_buf.ptr,
                              data_buf.ptr, cap, ws.ptr, ws_bytes, c.stream)
         assert rc == 0
@@ -490,11 +493,25 @@ def _mixed_density_pages(rng, n):
     return tw, cu
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 5])
+def _lds_overflow_pages(rng, n):
+    """Pages with <= 64 dirty 16-B chunks but large records (alternating bytes in 60 chunks:
+    2404-B records), so a wave's 8 KiB LDS buffer fills after three of them and the rest of the
+    unit is emitted from the arenas after the look-back."""
+    tw = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    cu = tw.copy()
+    for i in range(n):
+        if i % 5 == 4:
+            continue
+        for ch in rng.choice(256, 60, replace=False):
+            cu[i, ch * 16:ch * 16 + 16:2] ^= 0x3C
+    return tw, cu
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_diff_variants_bit_exact(variant, golden):
-    """Every output-producing diff kernel variant (gdsm_tune "diff_variant") is bit-exact on
-    edge pages, random byte densities (incl. records larger than the LDS stage) and clustered
-    writes."""
+    """Every diff geometry (gdsm_tune "diff_variant": automatic, 16 or 32 pages per wave) is
+    bit-exact on edge pages, random byte densities (pages past the 64-dirty-chunk fast path),
+    records that overflow the wave's LDS buffer, and clustered and uniform synthetic writes."""
     L = _lib.load()
     assert L.gdsm_tune(b"diff_variant", variant) == 0
     try:
@@ -510,6 +527,7 @@ def test_diff_variants_bit_exact(variant, golden):
         cases.append(oracle.gen_pages(200, seed=9, mode=1, ppm=100000))
         cases.append(oracle.gen_pages(200, seed=9, mode=0, ppm=10000))
         cases.append(_mixed_density_pages(rng, 300))
+        cases.append(_lds_overflow_pages(rng, 200))
         for tw, cu in cases:
             with ga.Context(len(tw)) as c:
                 c.upload("twin", tw)

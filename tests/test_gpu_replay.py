@@ -22,7 +22,7 @@ def test_mmult_replay_end_to_end(ndim, nodes):
         st, fl = oracle.coh_init(R.Z, nodes)
         acc = np.zeros(10, np.int64)
         for r in range(R.T.rounds):
-            rc, t = oracle.coherence(st, fl, R.T.round_events(r))
+            rc, t = oracle.coherence(st, fl, R.T.round_events(r), n_nodes=nodes)
             assert rc == 0
             acc += [t["invalidations"], t["transfers"], *t["node_faults"]]
         assert R.totals.tolist() == acc.tolist()

@@ -220,3 +220,14 @@ def test_c1_windows_pinned_by_reference_diff(golden):
     for i in range(0, 256, 32):
         o1, o2 = oracle.nw_diff(tw[i].tobytes(), cw[i].tobytes())
         assert [zlib.crc32(o1), zlib.crc32(o2)] == g["crc"][i].tolist()
+
+
+def test_coherence_rejects_node_outside_the_table():
+    """A page table initialised for n nodes rejects an event naming node >= n (include/gdsm.h
+    gdsm_coherence_batch: -EINVAL)."""
+    st, fl = oracle.coh_init(8, 3)
+    rc, _ = oracle.coherence(st, fl, np.array([(1 << 4) | (3 << 1)], np.uint64), n_nodes=3)
+    assert rc == -22
+    st, fl = oracle.coh_init(8, 3)
+    rc, _ = oracle.coherence(st, fl, np.array([(1 << 4) | (2 << 1)], np.uint64), n_nodes=3)
+    assert rc == 0

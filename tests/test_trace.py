@@ -54,7 +54,7 @@ def test_trace_shape_and_oracle_fold(nodes):
     n_w = sum(len(T.row_sets(i)[1]) for i in range(64))
     assert len(writes) == n_w
     st, fl = oracle.coh_init(L.n_pages, nodes)
-    rc, tot = oracle.coherence(st, fl, ev)
+    rc, tot = oracle.coherence(st, fl, ev, n_nodes=nodes)
     assert rc == 0
     if nodes == 1:
         assert tot["invalidations"] == 0 and tot["transfers"] == 0
@@ -69,10 +69,10 @@ def test_round_batches_equal_whole_trace():
     st1, fl1 = oracle.coh_init(L.n_pages, 4)
     acc = np.zeros(10, np.int64)
     for r in range(T.rounds):
-        rc, t = oracle.coherence(st1, fl1, T.round_events(r))
+        rc, t = oracle.coherence(st1, fl1, T.round_events(r), n_nodes=4)
         assert rc == 0
         acc += [t["invalidations"], t["transfers"], *t["node_faults"]]
     st2, fl2 = oracle.coh_init(L.n_pages, 4)
-    rc, t = oracle.coherence(st2, fl2, T.all_events())
+    rc, t = oracle.coherence(st2, fl2, T.all_events(), n_nodes=4)
     assert np.array_equal(st1, st2) and np.array_equal(fl1, fl2)
     assert acc.tolist() == [t["invalidations"], t["transfers"], *t["node_faults"]]
