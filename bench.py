@@ -160,7 +160,7 @@ def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
     return out
 
 
-DIFF_KERNEL = "gdsm::diff_compact_kernel"
+DIFF_KERNEL = "gdsm::diff_single_kernel"
 
 
 def read_traffic(pages: int, mode: str, ppm: int):

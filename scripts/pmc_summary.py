@@ -39,10 +39,9 @@ if len(sys.argv) > 6:
             out["main_kernel_bytes_per_launch"] = d["hbm_bytes_per_launch"]
     out["workload"] = json.loads(sys.argv[6])
 else:
-    # the diff kernel the bench runs (compacted kernel by default; the older whole-page kernels
-    # appear when GDSM_DIFF_VARIANT selects them)
+    # the diff kernel the bench runs
     for k, d in out["kernels"].items():
-        if k.startswith("gdsm::diff_compact_kernel") or k.startswith("gdsm::diff_pages_kernel"):
+        if k.startswith("gdsm::diff_single_kernel"):
             out["diff_kernel"] = k
             out["diff_kernel_bytes_per_launch"] = d["hbm_bytes_per_launch"]
 json.dump(out, open(sys.argv[3], "w"), indent=1)
