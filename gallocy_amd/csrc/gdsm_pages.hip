@@ -795,7 +795,8 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
   ProfScope ps(prof, 3, s);
-  hipLaunchKernelGGL(apply_kernel<0>, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, target, ids, n,
+  // one 64-record task per wave, 4 waves per workgroup: no workgroup launched without work
+  hipLaunchKernelGGL(apply_kernel<0>, dim3(grid_for(n, 256, 65536)), dim3(256), 0, s, target, ids, n,
                      rec_off, data, err);
   return hipGetLastError();
 }

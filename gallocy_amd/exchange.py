@@ -124,7 +124,7 @@ class Shard:
     `n` arena pages per rank (TWIN/CURRENT: the pages this rank writes; REPLICA: its home block).
     Two sets of per-destination send streams alternate, so diff k+1 (main stream) overlaps the
     exchange and home-side apply of release k (the context's second stream); a diff into set b
-    waits for the exchange that last read it (libgdsm orders that itself).
+    waits on the device for the exchange that last read it (libgdsm orders that itself).
 
     transport "rccl": gdsm_exchange (RCCL inside libgdsm). After `calibrate()`, releases use
     GDSM_XCHG_FIXED byte budgets: no host synchronisation at all per release.
@@ -147,8 +147,10 @@ class Shard:
             for d, r in enumerate(st):
                 r.s.n = self.counts[d]
         rmax = max(self.counts) + 1  # records from any source: n/G or n/G + 1
-        self.recv = [gdsm.Runs(ctx, rmax, cap=max(4096, rmax * cap_per_page)) for _ in range(world)]
-        self.rids = [ctx.buffer(4 * rmax) for _ in range(world)]
+        # receive streams per source (the own stream is applied in place: a stub)
+        self.recv = [gdsm.Runs(ctx, rmax, cap=max(4096, rmax * cap_per_page)) if s != rank
+                     else gdsm.Runs(ctx, 1, cap=16) for s in range(world)]
+        self.rids = [ctx.buffer(4 * rmax if s != rank else 4) for s in range(world)]
         self.transport = transport
         self.comm = Comm(ctx, rank, world, group) if transport == "rccl" else None
         self.gloo = GlooTransport(group) if transport == "gloo" else None
@@ -205,22 +207,17 @@ class Shard:
         self.exchange(k)
 
     def run(self, steps: int, pipelined: bool = True):
-        """`steps` releases. Pipelined: diff k+1 is enqueued before exchange k, so with RCCL the
-        transfer and the home-side apply of k overlap the diff of k+1."""
-        if steps <= 0:
-            return
-        if not pipelined or self.comm is None:
-            for k in range(steps):
-                self.step(self.k + k)
-                if not pipelined:
-                    self.ctx.sync()
-            self.k += steps
-            return
-        self.diff(self.k)
+        """`steps` releases, enqueued in order diff k -> exchange k -> diff k+1 -> ... Pipelined:
+        the two send sets alternate, so diff k+1 (main stream) runs while exchange + home-side
+        apply k run on the second stream (gdsm_exchange waits only for what the main stream
+        holds when it is called: diff k). Serial: one send set, so diff k+1 waits on the device
+        for the exchange that read it. Neither synchronises the host (RCCL transport)."""
         for k in range(steps):
-            if k + 1 < steps:
-                self.diff(self.k + k + 1)
-            self.exchange(self.k + k)
+            j = self.k + k if pipelined else 0
+            self.diff(j)
+            self.exchange(j)
+            if self.comm is None:
+                self.ctx.sync()
         self.k += steps
 
     def calibrate(self):
