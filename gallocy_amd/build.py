@@ -100,6 +100,12 @@ def build_sanitized(verbose: bool = False) -> Path:
     return lib
 
 
+def build_test_drivers(verbose: bool = False) -> None:
+    """Compiled C++ callers of libgdsm.so used by the tests (tests/cpp/, output in _build/)."""
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "cpp")], check=True,
+                   stdout=None if verbose else subprocess.DEVNULL)
+
+
 def build_oracle(verbose: bool = False) -> None:
     """Test oracle (oracle/liboracle.so) and, when the reference tree exists, oracle/_ref."""
     targets = ["oracle"]
@@ -114,5 +120,6 @@ if __name__ == "__main__":
         print(build_sanitized(verbose=True))
         sys.exit(0)
     build_lib(force="--force" in sys.argv, verbose=True)
+    build_test_drivers(verbose=True)
     build_oracle(verbose=True)
     print(LIB)
