@@ -268,12 +268,64 @@ def run_coherence(args):
     ctx.close()
 
 
+def run_mmult_ranks(args, rank: int, world: int):
+    """BASELINE configs[4] at N > 1: one process (GPU) per DSM node of the trace
+    (gallocy_amd.replay.MmultRankReplay): page-table shards at the homes, per-round diffs shipped
+    to the home GPUs with gdsm_exchange (RCCL). Strong scaling: the same NDIM = 1000 product."""
+    import torch
+    import torch.distributed as dist
+
+    from gallocy_amd.replay import MmultRankReplay
+    backend = os.environ.get("GDSM_BENCH_BACKEND", "nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo")
+    R = MmultRankReplay(rank, world, ndim=args.ndim, seed=args.seed, device=local,
+                        transport="gloo" if backend == "gloo" else "rccl")
+    dist.barrier()
+    dt = R.run()
+    ok = torch.tensor([1 if np.array_equal(R.home_block(), R.final_block()) else 0],
+                      dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    tot = torch.tensor(R.totals.tolist(), dtype=torch.int64)
+    dist.all_reduce(tot)
+    ev = torch.tensor([R.events_total, R.pages_diffed], dtype=torch.int64)
+    dist.all_reduce(ev)
+    if rank == 0:
+        res = {"metric": "mmult trace replay rounds/sec", "value": round(R.T.rounds / dt, 1),
+               "unit": "rounds/s", "n_gpus": world, "steps": R.T.rounds, "warmup": 0,
+               "ms_per_step": round(dt / R.T.rounds * 1e3, 4), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "u8/u64",
+               "data": "test_mmult trace from the reference heap layout (gallocy_amd/trace.py)",
+               "config": {"workload": f"NDIM={args.ndim}, {world} DSM nodes = {world} GPUs, "
+                                      f"{R.Z} zone pages, page-table shards + RCCL diff exchange",
+                          "rows": args.ndim, "events": int(ev[0]), "pages_diffed": int(ev[1]),
+                          **({"backend": "gloo (REHEARSAL, not a measurement)"}
+                             if backend == "gloo" else {})},
+               "seconds_total": round(dt, 4), "rows_per_s": round(args.ndim / dt, 1),
+               "home_copy_equals_product": bool(ok.item()),
+               "totals": {"invalidations": int(tot[0]), "transfers": int(tot[1]),
+                          "node_faults": [int(x) for x in tot[2:]]}}
+        print(json.dumps(res), flush=True)
+    R.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def run_mmult(args):
     """BASELINE configs[4]: the test_mmult trace (reference heap layout, NDIM=1000) replayed end
-    to end: per round one coherence batch + twin/write/diff/apply of every row written."""
+    to end: per round one coherence batch + twin/write/diff/apply of every row written. One GPU
+    simulates --nodes nodes; under torch.distributed.run every rank is one node on its own GPU
+    (run_mmult_ranks)."""
     import torch
 
     from gallocy_amd.replay import MmultReplay
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        return run_mmult_ranks(args, int(os.environ.get("RANK", "0")), world)
     torch.cuda.set_device(0)
     R = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed)
     dt = R.run()

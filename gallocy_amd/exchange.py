@@ -118,6 +118,47 @@ class Comm:
             self.handle = None
 
 
+def exchange_runs(ctx: gdsm.Context, comm: Comm, send: list, send_ids: list, recv: list,
+                  recv_ids: list, flags: int = 0, target=gdsm.REPLICA):
+    """gdsm_exchange over lists of G Runs / device id pointers; updates recv[s].n."""
+    G = comm.world
+    s_arr = (GdsmRuns * G)(*[r.s for r in send])
+    r_arr = (GdsmRuns * G)(*[r.s for r in recv])
+    sid = (C.c_void_p * G)(*send_ids)
+    rid = (C.c_void_p * G)(*recv_ids)
+    check(gdsm.lib().gdsm_exchange(ctx.handle, comm.handle, s_arr, sid, r_arr, rid, target, flags),
+          "gdsm_exchange")
+    for s in range(G):
+        recv[s].s.n = r_arr[s].n
+
+
+def exchange_gloo(ctx: gdsm.Context, gloo: GlooTransport, send: list, send_ids: list,
+                  counts: list, rank: int):
+    """The same release over GlooTransport with host staging (one-GPU multi-rank rehearsal):
+    every source's stream is applied to ctx's REPLICA. Returns (sent_remote, received) bytes."""
+    parts = []
+    for d, r in enumerate(send):
+        if counts[d]:
+            h = r.to_host()
+            ids = send_ids[d].download(np.uint32, counts[d])
+        else:
+            h = gdsm.HostRuns(np.zeros(1, np.uint64), np.zeros(0, np.uint8))
+            ids = np.zeros(0, np.uint32)
+        parts.append((h.rec_off, ids, h.data))
+    got = gloo.exchange(parts)
+    for ro, ids, data in got:
+        if len(ids) == 0:
+            continue
+        runs = gdsm.Runs.from_host(ctx, gdsm.HostRuns(ro, data))
+        d_ids = ctx.ids(ids)
+        ctx.apply(runs, "replica", d_ids)
+        ctx.sync()
+        runs.free()
+        d_ids.free()
+    sent_remote = sum(int(p[0][-1]) for d, p in enumerate(parts) if d != rank)
+    return sent_remote, sum(int(g[0][-1]) for g in got)
+
+
 class Shard:
     """One rank's release pipeline: per-destination diffs -> exchange -> apply at the homes.
 
@@ -169,38 +210,14 @@ class Shard:
     def exchange(self, k: int):
         st = self.send[k % len(self.send)]
         if self.comm is not None:
-            G = self.world
-            send = (GdsmRuns * G)(*[r.s for r in st])
-            recv = (GdsmRuns * G)(*[r.s for r in self.recv])
-            sid = (C.c_void_p * G)(*[b.ptr for b in self.sids])
-            rid = (C.c_void_p * G)(*[b.ptr for b in self.rids])
-            check(self.L.gdsm_exchange(self.ctx.handle, self.comm.handle, send, sid, recv, rid,
-                                       gdsm.REPLICA, self.flags), "gdsm_exchange")
-            for s in range(G):  # gdsm_exchange sets recv[s].n
-                self.recv[s].s.n = recv[s].n
+            exchange_runs(self.ctx, self.comm, st, [b.ptr for b in self.sids], self.recv,
+                          [b.ptr for b in self.rids], self.flags)
         else:
             self._exchange_gloo(st)
 
     def _exchange_gloo(self, st):
-        parts = []
-        for d, r in enumerate(st):
-            h = r.to_host() if self.counts[d] else gdsm.HostRuns(np.zeros(1, np.uint64),
-                                                                  np.zeros(0, np.uint8))
-            ids = (self.sids[d].download(np.uint32, self.counts[d]) if self.counts[d]
-                   else np.zeros(0, np.uint32))
-            parts.append((h.rec_off, ids, h.data))
-        got = self.gloo.exchange(parts)
-        self.received = sum(int(g[0][-1]) for g in got)
-        self.sent_remote = sum(int(p[0][-1]) for d, p in enumerate(parts) if d != self.rank)
-        for s, (ro, ids, data) in enumerate(got):
-            if len(ids) == 0:
-                continue
-            runs = gdsm.Runs.from_host(self.ctx, gdsm.HostRuns(ro, data))
-            d_ids = self.ctx.ids(ids)
-            self.ctx.apply(runs, "replica", d_ids)
-            self.ctx.sync()
-            runs.free()
-            d_ids.free()
+        self.sent_remote, self.received = exchange_gloo(self.ctx, self.gloo, st, self.sids,
+                                                        self.counts, self.rank)
 
     def step(self, k: int):
         self.diff(k)

@@ -128,3 +128,180 @@ class MmultReplay:
         self._runs.free()
         self.data.close()
         self.pt.close()
+
+
+class MmultRankReplay:
+    """Config 5 with one process (one GPU) per DSM node: rank t of P = node t of the trace.
+
+    Pages are homed in contiguous blocks, home(p) = p // ceil(Z / P), which is also the home the
+    page table is initialised with (SPEC §5). Per round, on every rank:
+      1. coherence: the round's events on the pages homed here, in the trace's order, folded into
+         this rank's page-table shard (local page p - base);
+      2. twin, then the node's own row writes c[i][*] in its view of the zone (CURRENT);
+      3. release: the written pages are diffed into one stream per home rank and shipped with
+         gdsm_exchange (RCCL), each home applying what it receives to its REPLICA (indexed by
+         global page: the home block is REPLICA[base, base + per)).
+    At the end every home block equals the zone after the multiplication, and the page-table
+    shards together equal the sequential fold of the whole trace (tests/test_gpu_replay.py).
+    transport "gloo": the exchange goes through host memory (GlooTransport), so several ranks
+    can rehearse on one GPU; not a measurement."""
+
+    def __init__(self, rank: int, world: int, ndim: int = 1000, seed: int = 0, device: int = 0,
+                 transport: str = "rccl", group=None):
+        from . import exchange
+        self.rank, self.P = rank, world
+        self.L = mmult_layout(ndim)
+        self.T = MmultTrace(self.L, world, seed)
+        self.Z = self.L.n_pages
+        self.per = -(-self.Z // world)
+        self.base = min(self.Z, rank * self.per)
+        self.nh = max(0, min(self.Z, self.base + self.per) - self.base)
+        L, Z = self.L, self.Z
+        self.image = zone_image(L)
+        home = lambda p: p // self.per  # noqa: E731
+        # ---- host preparation (not part of the replay time)
+        self.rounds = []
+        rowvals = np.stack([c_row_values(L, i) for i in range(L.ndim)]).view(np.uint8)
+        max_per_dest, max_ev = 1, 1
+
+        def written(rows):
+            return np.unique(np.concatenate(
+                [np.arange(int(L.c_rows[i]) // PAGE_SZ,
+                           (int(L.c_rows[i]) + 8 * L.ndim - 1) // PAGE_SZ + 1) for _, i in rows])
+                             ) if rows else np.zeros(0, np.int64)
+        for r in range(self.T.rounds):
+            all_rows = self.T.round_rows(r)
+            for t in range(world):  # receive streams are sized for the largest sender
+                wp = written([x for x in all_rows if x[0] == t])
+                if len(wp):
+                    max_per_dest = max(max_per_dest, int(np.bincount(home(wp)).max()))
+            rows = [(t, i) for t, i in all_rows if t == rank]
+            pages = written(rows)
+            by_dest = [pages[home(pages) == d].astype(np.uint32) for d in range(world)]
+            ev = self.T.round_events(r)
+            pg = (ev >> 4).astype(np.int64)
+            mine = (pg >= self.base) & (pg < self.base + self.nh)
+            ev = (((pg[mine] - self.base).astype(np.uint64) << 4) | (ev[mine] & 15)).astype(np.uint64)
+            self.rounds.append((rows, pages.astype(np.uint32), by_dest, ev))
+            max_per_dest = max([max_per_dest] + [len(x) for x in by_dest])
+            max_ev = max(max_ev, len(ev))
+        # ---- device state
+        self.data = gdsm.Context(Z, device=device)
+        self.pt = gdsm.Context(max(1, self.nh), device=device, arenas=())
+        pages_img = self.image.reshape(Z, PAGE_SZ)
+        for a in ("current", "twin", "replica"):
+            self.data.upload(a, pages_img)
+        self.pt.coh_init(world)
+        if self.nh:  # every page of this shard is homed here (SPEC §5 initial state)
+            st = np.full(self.nh, (1 << rank) | (rank << 8) | (2 << 16), np.uint32)
+            self.pt.coh_upload(st, np.zeros(self.nh, np.uint32))
+        self.d_rows = self.data.buffer(rowvals.nbytes).upload(rowvals)
+        self.row_bytes = 8 * L.ndim
+        # per round: written pages (twin list) and per-destination lists, in one device buffer
+        flat, self.offs = [], []
+        pos = 0
+        for rows, pages, by_dest, ev in self.rounds:
+            o = [pos]
+            flat.append(pages)
+            pos += len(pages)
+            for x in by_dest:
+                o.append(pos)
+                flat.append(x)
+                pos += len(x)
+            self.offs.append(o)
+        allids = np.concatenate(flat).astype(np.uint32) if pos else np.zeros(1, np.uint32)
+        self.d_ids = self.data.ids(allids)
+        evs = [e for *_, e in self.rounds]
+        self.ev_off = np.concatenate([[0], np.cumsum([len(e) for e in evs])]).astype(np.int64)
+        allev = np.concatenate(evs).astype(np.uint64) if self.ev_off[-1] else np.zeros(1, np.uint64)
+        self.d_ev = self.pt.buffer(max(8, allev.nbytes)).upload(allev)
+        self.d_tot = self.pt.buffer(8 * 10 * max(1, self.T.rounds))
+        cap = max_per_dest * 10244
+        self.send = [gdsm.Runs(self.data, max_per_dest, cap=cap) for _ in range(world)]
+        self.recv = [gdsm.Runs(self.data, max_per_dest, cap=cap) if s != rank
+                     else gdsm.Runs(self.data, 1, cap=16) for s in range(world)]
+        self.rids = [self.data.buffer(4 * max_per_dest) for _ in range(world)]
+        gdsm.check(gdsm.lib().gdsm_reserve(self.data.handle, max_per_dest, 0), "reserve")
+        gdsm.check(gdsm.lib().gdsm_reserve(self.pt.handle, 0, max_ev), "reserve")
+        self.transport = transport
+        self.comm = exchange.Comm(self.data, rank, world, group) if transport == "rccl" else None
+        self.gloo = exchange.GlooTransport(group) if transport == "gloo" else None
+        self.events_total = int(self.ev_off[-1])
+        self.pages_diffed = sum(len(p) for _, p, _, _ in self.rounds)
+        self.totals = None
+
+    def round(self, r: int):
+        from . import exchange
+        lib = gdsm.lib()
+        rows, pages, by_dest, ev = self.rounds[r]
+        e0, e1 = int(self.ev_off[r]), int(self.ev_off[r + 1])
+        if e1 > e0:                                                                      # 1
+            gdsm.check(lib.gdsm_coherence_batch_async(self.pt.handle, self.d_ev.ptr + 8 * e0,
+                                                      e1 - e0, self.d_tot.ptr + 80 * r), "coherence")
+        o = self.offs[r]
+        if len(pages):
+            self.data.twin(self.d_ids.ptr + 4 * o[0], n=len(pages))                         # 2
+            base = self.data.arena_ptr("current")
+            for _, i in rows:
+                gdsm.check(lib.gdsm_memcpy_d2d(self.data.handle, base + int(self.L.c_rows[i]),
+                                               self.d_rows.ptr + i * self.row_bytes,
+                                               self.row_bytes), "row write")
+        counts = [len(x) for x in by_dest]
+        sids = [self.d_ids.ptr + 4 * o[1 + d] for d in range(self.P)]
+        for d in range(self.P):                                                          # 3
+            self.data.diff(sids[d], n=counts[d], out=self.send[d])  # n = 0: rec_off[0] = 0
+        if self.comm is not None:
+            exchange.exchange_runs(self.data, self.comm, self.send, sids, self.recv,
+                                   [b.ptr for b in self.rids])
+        else:
+            self.data.sync()
+            exchange.exchange_gloo(self.data, self.gloo, self.send,
+                                   [_Ptr(self.data, p) for p in sids], counts, self.rank)
+
+    def run(self) -> float:
+        self.data.sync()
+        self.pt.sync()
+        t0 = time.perf_counter()
+        for r in range(self.T.rounds):
+            self.round(r)
+        self.data.sync()
+        self.pt.sync()
+        dt = time.perf_counter() - t0
+        self.totals = self.d_tot.download(np.uint64, 10 * self.T.rounds).reshape(-1, 10).sum(0).astype(np.int64)
+        return dt
+
+    def home_block(self) -> np.ndarray:
+        """REPLICA pages [base, base + per) (this rank's home block)."""
+        if not self.nh:
+            return np.zeros(0, np.uint8)
+        return self.data.download("replica", self.base, self.nh).reshape(-1)
+
+    def final_block(self) -> np.ndarray:
+        z = self.image.copy()
+        f64 = z.view("<f8")
+        n = self.L.ndim
+        for i in range(n):
+            o = int(self.L.c_rows[i]) // 8
+            f64[o:o + n] = c_row_values(self.L, i)
+        return z[self.base * PAGE_SZ:(self.base + self.nh) * PAGE_SZ]
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+        for r in self.send + self.recv:
+            r.free()
+        self.data.close()
+        self.pt.close()
+
+
+class _Ptr:
+    """A device pointer that downloads like a DeviceBuffer (exchange_gloo reads id lists)."""
+
+    def __init__(self, ctx, ptr):
+        self.ctx, self.ptr = ctx, ptr
+
+    def download(self, dtype, count):
+        out = np.empty(count, dtype=dtype)
+        gdsm.check(gdsm.lib().gdsm_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr,
+                                              out.nbytes), "d2h")
+        return out
