@@ -1,12 +1,17 @@
 #!/bin/bash
-# rocprofv3 PMC passes (one per counter group) over coherence pass C variants 0 and 1.
+# rocprofv3 PMC passes (one per counter group) over coherence pass-C variants (COH_PMC_VARIANTS).
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/cohpmc
 mkdir -p $OUT
-for v in ${COH_PMC_VARIANTS:-0 4}; do
-  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --kernel-trace -d $OUT/a$v -o a --output-format csv -- python3 scripts/coh_pmc.py 268435456 uniform $v > $OUT/a$v.log 2>&1 || exit 1
-  timeout -s KILL 90 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE --kernel-trace -d $OUT/b$v -o b --output-format csv -- python3 scripts/coh_pmc.py 268435456 uniform $v > $OUT/b$v.log 2>&1 || exit 1
+A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_IFETCH SQ_WAVE_CYCLES"
+B="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SALU SQ_BUSY_CYCLES SQ_LEVEL_WAVES SQ_INSTS_SMEM"
+C="SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+for v in ${COH_PMC_VARIANTS:-0 2}; do
+  for p in a b c; do
+    case $p in a) CT=$A;; b) CT=$B;; c) CT=$C;; esac
+    timeout -s KILL 90 rocprofv3 --pmc $CT --kernel-trace -d $OUT/$p$v -o $p --output-format csv -- python3 scripts/coh_pmc.py 268435456 uniform $v > $OUT/$p$v.log 2>&1 || exit 1
+  done
 done
 python3 - <<'PY'
 import csv, glob, collections
@@ -15,5 +20,5 @@ for f in sorted(glob.glob("gpurun_out/cohpmc/*/*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         if "coh_apply" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    print(f, {k: sum(v) / len(v) for k, v in acc.items()})
+    print(f.split("/")[2], {k: round(sum(v) / len(v) / 524288, 1) for k, v in sorted(acc.items())})
 PY

@@ -104,7 +104,7 @@ def test_unsorted_batch_is_rejected():
             c.coherence_batch(np.array([99 << 4], np.uint64))  # page out of range
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_node_outside_the_table_is_rejected(variant):
     """gdsm_coherence_batch rejects an event naming a node >= the n_nodes of gdsm_coh_init, like
     the oracle (both pass-C kernels)."""
@@ -152,6 +152,35 @@ def test_variant1_and_unaligned_events_match_oracle(unaligned):
             assert list(tot) == [otot["invalidations"], otot["transfers"], *otot["node_faults"]]
             gst, gfl = c.coh_download()
             assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+    finally:
+        L.gdsm_tune(b"coh_variant", 0)
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_arbitrary_page_table_states(variant):
+    """Uploaded page-table words in any SPEC §5 state (INVALID, SHARED, EXCLUSIVE, the unused
+    state 3, owners >= 8, dirty or not, large fault counts): every pass-C kernel folds them
+    exactly like the oracle, over Zipf batches with hot pages and single-event pages."""
+    L = ga.gdsm.lib()
+    n = 6000
+    rng = np.random.default_rng(77 + variant)
+    assert L.gdsm_tune(b"coh_variant", variant) == 0
+    try:
+        with ga.Context(n, arenas=()) as c:
+            c.coh_init(8)
+            st = rng.integers(0, 1 << 19, n).astype(np.uint32)
+            fl = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+            c.coh_upload(st, fl)
+            for b in range(3):
+                counts = zipf_counts(n, 70000, s=0.9, seed=200 + b)
+                counts[rng.integers(0, n, 5)] = rng.integers(2000, 9000, 5)
+                ev = oracle.gen_events(counts, seed=300 + b, n_nodes=8, write_pct=(5, 30, 70)[b])
+                tot = c.coherence_batch(ev)
+                rc, otot = oracle.coherence(st, fl, ev)
+                assert rc == 0 and tot == otot
+                gst, gfl = c.coh_download()
+                assert np.array_equal(gst, st), np.flatnonzero(gst != st)[:10]
+                assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
     finally:
         L.gdsm_tune(b"coh_variant", 0)
 
