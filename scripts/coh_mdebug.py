@@ -13,7 +13,7 @@ import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-variant = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+variant = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 trials = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
 assert gdsm.lib().gdsm_tune(b"coh_variant", variant) == 0
 best = None

@@ -1,5 +1,5 @@
 """Debug aid (needs a -DGDSM_COH_STAMPS build loaded with GDSM_LIB): average per-wave phase
-durations of the hit-mask pass C (s_memtime ticks) on a config-4 batch."""
+durations of pass C (s_memtime ticks) on a config-4 batch."""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -17,7 +17,7 @@ pages = 16 << 20
 L = gdsm.lib()
 ctx = ga.Context(pages, arenas=())
 ev = ctx.gen_events(event_counts(pages, n_ev, dist, seed=2026), seed=2026, n_nodes=8, write_pct=20)
-assert L.gdsm_tune(b"coh_variant", int(sys.argv[3]) if len(sys.argv) > 3 else 2) == 0
+assert L.gdsm_tune(b"coh_variant", int(sys.argv[3]) if len(sys.argv) > 3 else 0) == 0
 for _ in range(2):
     ctx.coh_init(8)
     ctx.coherence_batch(ev)

@@ -104,85 +104,76 @@ def test_unsorted_batch_is_rejected():
             c.coherence_batch(np.array([99 << 4], np.uint64))  # page out of range
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_node_outside_the_table_is_rejected(variant):
+def test_node_outside_the_table_is_rejected():
     """gdsm_coherence_batch rejects an event naming a node >= the n_nodes of gdsm_coh_init, like
-    the oracle (both pass-C kernels)."""
-    L = ga.gdsm.lib()
-    assert L.gdsm_tune(b"coh_variant", variant) == 0
-    try:
-        with ga.Context(16, arenas=()) as c:
-            c.coh_init(3)
-            with pytest.raises(GdsmError) as ei:
-                c.coherence_batch(np.array([(1 << 4) | (3 << 1), (2 << 4) | (7 << 1) | 1],
-                                           np.uint64))
-            assert ei.value.errno == 22
-            c.coh_init(3)
-            c.coherence_batch(np.array([(1 << 4) | (2 << 1)], np.uint64))
-    finally:
-        L.gdsm_tune(b"coh_variant", 0)
+    the oracle."""
+    with ga.Context(16, arenas=()) as c:
+        c.coh_init(3)
+        with pytest.raises(GdsmError) as ei:
+            c.coherence_batch(np.array([(1 << 4) | (3 << 1), (2 << 4) | (7 << 1) | 1], np.uint64))
+        assert ei.value.errno == 22
+        c.coh_init(3)
+        c.coherence_batch(np.array([(1 << 4) | (2 << 1)], np.uint64))
+
+
+def _batch_from(c, host, unaligned):
+    """Device copy of a host event batch: 16-B aligned, or one u64 in (8-B aligned only), which
+    takes the scalar-load instance of pass C."""
+    buf = c.buffer(8 * (len(host) + 1))
+    if unaligned:
+        buf.upload(np.concatenate([np.zeros(1, np.uint64), host]))
+        return buf, buf.ptr + 8
+    buf.upload(host)
+    return buf, buf.ptr
 
 
 @pytest.mark.parametrize("unaligned", [False, True])
-def test_variant1_and_unaligned_events_match_oracle(unaligned):
-    """Pass-C variant 1 (coh_apply_kernel, the persistent block-scan kernel) and the path taken for
-    event arrays that are not 16-B aligned (coh_apply_kernel<false>) are bit-exact too."""
+def test_unaligned_events_match_oracle(unaligned):
+    """Event arrays that are not 16-B aligned (pass C with scalar loads) are bit-exact too."""
     L = ga.gdsm.lib()
     n = 5000
     counts = zipf_counts(n, 90000, seed=4)
     host = oracle.gen_events(counts, seed=9, n_nodes=8, write_pct=25)
-    if not unaligned:
-        assert L.gdsm_tune(b"coh_variant", 1) == 0
-    try:
-        with ga.Context(n, arenas=()) as c:
-            c.coh_init(8)
-            buf = c.buffer(8 * (len(host) + 1))
-            if unaligned:  # one u64 in: 8-B aligned, not 16-B aligned
-                padded = np.concatenate([np.zeros(1, np.uint64), host])
-                buf.upload(padded)
-                ptr = buf.ptr + 8
-            else:
-                buf.upload(host)
-                ptr = buf.ptr
+    with ga.Context(n, arenas=()) as c:
+        c.coh_init(8)
+        _, ptr = _batch_from(c, host, unaligned)
+        tot = (C.c_uint64 * 10)()
+        assert L.gdsm_coherence_batch(c.handle, ptr, len(host), tot) == 0
+        st, fl = oracle.coh_init(n, 8)
+        rc, otot = oracle.coherence(st, fl, host)
+        assert rc == 0
+        assert list(tot) == [otot["invalidations"], otot["transfers"], *otot["node_faults"]]
+        gst, gfl = c.coh_download()
+        assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+
+
+@pytest.mark.parametrize("unaligned", [False, True])
+def test_arbitrary_page_table_states(unaligned):
+    """Uploaded page-table words in any SPEC §5 state (INVALID, SHARED, EXCLUSIVE, the unused
+    state 3, owners >= 8, dirty or not, fault counts up to 2^32 - 1): pass C folds them exactly
+    like the oracle, over Zipf batches with hot pages and single-event pages. (The round-1
+    block-scan kernel, retired in round 2, lost bit 31 of large fault counts here.)"""
+    L = ga.gdsm.lib()
+    n = 6000
+    rng = np.random.default_rng(77 + unaligned)
+    with ga.Context(n, arenas=()) as c:
+        c.coh_init(8)
+        st = rng.integers(0, 1 << 19, n).astype(np.uint32)
+        fl = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+        c.coh_upload(st, fl)
+        for b in range(3):
+            counts = zipf_counts(n, 70000, s=0.9, seed=200 + b)
+            counts[rng.integers(0, n, 5)] = rng.integers(2000, 9000, 5)
+            ev = oracle.gen_events(counts, seed=300 + b, n_nodes=8, write_pct=(5, 30, 70)[b])
+            _, ptr = _batch_from(c, ev, unaligned)
             tot = (C.c_uint64 * 10)()
-            assert L.gdsm_coherence_batch(c.handle, ptr, len(host), tot) == 0
-            st, fl = oracle.coh_init(n, 8)
-            rc, otot = oracle.coherence(st, fl, host)
+            assert L.gdsm_coherence_batch(c.handle, ptr, len(ev), tot) == 0
+            rc, otot = oracle.coherence(st, fl, ev)
             assert rc == 0
             assert list(tot) == [otot["invalidations"], otot["transfers"], *otot["node_faults"]]
             gst, gfl = c.coh_download()
-            assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
-    finally:
-        L.gdsm_tune(b"coh_variant", 0)
-
-
-@pytest.mark.parametrize("variant", [0, 2])
-def test_arbitrary_page_table_states(variant):
-    """Uploaded page-table words in any SPEC §5 state (INVALID, SHARED, EXCLUSIVE, the unused
-    state 3, owners >= 8, dirty or not, large fault counts): every pass-C kernel folds them
-    exactly like the oracle, over Zipf batches with hot pages and single-event pages."""
-    L = ga.gdsm.lib()
-    n = 6000
-    rng = np.random.default_rng(77 + variant)
-    assert L.gdsm_tune(b"coh_variant", variant) == 0
-    try:
-        with ga.Context(n, arenas=()) as c:
-            c.coh_init(8)
-            st = rng.integers(0, 1 << 19, n).astype(np.uint32)
-            fl = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-            c.coh_upload(st, fl)
-            for b in range(3):
-                counts = zipf_counts(n, 70000, s=0.9, seed=200 + b)
-                counts[rng.integers(0, n, 5)] = rng.integers(2000, 9000, 5)
-                ev = oracle.gen_events(counts, seed=300 + b, n_nodes=8, write_pct=(5, 30, 70)[b])
-                tot = c.coherence_batch(ev)
-                rc, otot = oracle.coherence(st, fl, ev)
-                assert rc == 0 and tot == otot
-                gst, gfl = c.coh_download()
-                assert np.array_equal(gst, st), np.flatnonzero(gst != st)[:10]
-                assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
-    finally:
-        L.gdsm_tune(b"coh_variant", 0)
+            assert np.array_equal(gst, st), np.flatnonzero(gst != st)[:10]
+            assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
 
 
 def test_out_of_range_page_writes_nothing():
