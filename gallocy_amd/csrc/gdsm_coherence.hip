@@ -615,370 +615,6 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
-// ---------------------------------------------------------------- C'': hit-mask pass C
-// The same block / carry inputs, restated so that an event costs a handful of VALU operations,
-// in a persistent kernel that loads the next block's events while it walks the current one:
-//  * the state a page's next event meets is kept as a 16-bit HIT MASK, bit 2n = "a read by n
-//    hits" (n in the copyset), bit 2n+1 = "a write by n hits" (EXCLUSIVE and owned by n). An
-//    event's low nibble is (n << 1) | rw, i.e. exactly its bit index, so one v_bfe_u32 with the
-//    event's low dword as offset tests it (the mask is duplicated into both halves, so bit 4 of
-//    the dword, page bit 0, does not matter). A read miss adds bit 2n and clears every
-//    write-hit bit (EXCLUSIVE -> SHARED); a write leaves bits 2n and 2n+1 only.
-//  * owner (<< 1) lives in the low 16 bits of a second register compared with v_cmp_ne_u16;
-//    above them a write marks "written since the head" and a head carries its state bits;
-//  * lane aggregates are scanned as M-words (hit mask | owner << 16 | state, dirty << 24 |
-//    EXCLUSIVE-intact << 27 | CONST << 31; READ(R) = read bits) with the same composition rule;
-//  * booleans stay lane masks (SALU); heads load {mask, owner} from the wave's LDS slot list,
-//    filled by consecutive lanes from the page table; a segment end parks {mask, owner | flags |
-//    faults << 20} in its head's slot, or, for a segment opened in an earlier lane, in the lane's
-//    own record until the walk is over (lanes walk their events in step, so that head's slot
-//    may not have been read yet);
-//    closed segments are stored by consecutive lanes at the end as whole 8-B words.
-constexpr uint32_t kRdBits = 0x55555555u;  // read-hit bits, both halves
-constexpr uint32_t kXb = 1u << 27;         // M-word: EXCLUSIVE not yet broken by a read miss
-constexpr uint32_t kAw = 1u << 16;         // owner register: written since the head
-constexpr uint32_t kRm = 1u << 30;         // end record: a read missed since the head
-
-__device__ __forceinline__ uint32_t spread8(uint32_t cs) {
-  uint32_t s = cs & 0xFFu;
-  s = (s | (s << 4)) & 0x0F0Fu;
-  s = (s | (s << 2)) & 0x3333u;
-  s = (s | (s << 1)) & 0x5555u;
-  return s;
-}
-__device__ __forceinline__ uint32_t compact16(uint32_t m) {
-  m &= 0x5555u;
-  m = (m | (m >> 1)) & 0x3333u;
-  m = (m | (m >> 2)) & 0x0F0Fu;
-  m = (m | (m >> 4)) & 0x00FFu;
-  return m;
-}
-// SPEC §5 state word -> CONST M-word.
-__device__ __forceinline__ uint32_t mword_of_state(uint32_t w) {
-  const uint32_t owner = (w >> 8) & 0xFFu, st = (w >> 16) & 3u;
-  const uint32_t wb = (st == 2u && owner < 8u) ? (2u << (2u * owner)) : 0u;
-  return spread8(w) | wb | (owner << 16) | (((w >> 16) & 7u) << 24) | (st == 2u ? kXb : 0u) |
-         kConst;
-}
-// a, then b (M-words): a READ b adds its readers; one outside a's copyset breaks EXCLUSIVE.
-__device__ __forceinline__ uint32_t mcompose(uint32_t a, uint32_t b) {
-  const uint32_t keep = (b & ~a & 0x5555u) ? ~(0xAAAAu | kXb) : ~0u;
-  return (b & kConst) ? b : ((a | b) & keep);
-}
-__device__ __forceinline__ uint32_t wave_incl_mcompose_dpp(uint32_t v) {
-  v = mcompose(dpp0<0x111>(v), v);
-  v = mcompose(dpp0<0x112>(v), v);
-  v = mcompose(dpp0<0x114>(v), v);
-  v = mcompose(dpp0<0x118>(v), v);
-  v = mcompose(dpp0<0x142, 0xA>(v), v);
-  v = mcompose(dpp0<0x143, 0xC>(v), v);
-  return v;
-}
-// Walk registers of a head slot from an M-word: {duplicated hit mask, owner << 1 | (state,
-// dirty) << 17}. The state bits say EXCLUSIVE only while the M-word's kXb holds.
-__device__ __forceinline__ uint2 slot_of_mword(uint32_t m) {
-  const uint32_t st = (m >> 24) & 3u;
-  const uint32_t ste = (st == 2u && !(m & kXb)) ? 1u : st;
-  return make_uint2((m & 0xFFFFu) * 0x10001u,
-                    ((m >> 15) & 0x1FEu) | ((ste | ((m >> 24) & 4u)) << 17));
-}
-// Walk registers of a head from its page-table state word.
-__device__ __forceinline__ uint2 slot_of_state(uint32_t w) {
-  const uint32_t owner = (w >> 8) & 0xFFu, st = (w >> 16) & 3u;
-  const uint32_t m16 = spread8(w) | ((st == 2u && owner < 8u) ? (2u << (2u * owner)) : 0u);
-  return make_uint2(m16 * 0x10001u, (owner << 1) | (((w >> 16) & 7u) << 17));
-}
-// M-word of a head slot (heads are loaded with kXb = EXCLUSIVE).
-__device__ __forceinline__ uint32_t mword_of_slot(uint2 s) {
-  const uint32_t sd = (s.y >> 17) & 7u;
-  return (s.x & 0xFFFFu) | ((s.y & 0x1FEu) << 15) | (sd << 24) | ((sd & 3u) == 2u ? kXb : 0u) |
-         kConst;
-}
-// Page-table state word of a closed segment from its end record.
-__device__ __forceinline__ uint32_t state_of_record(uint2 r) {
-  const uint32_t cs = compact16(r.x), owner = (r.y >> 1) & 0xFFu;
-  uint32_t st, dirty;
-  if (r.y & kAw) {
-    st = (r.x & 0xAAAAu) ? 2u : 1u;
-    dirty = 1u;
-  } else {
-    const uint32_t s0 = (r.y >> 17) & 3u;
-    st = (s0 == 2u && (r.y & kRm)) ? 1u : s0;
-    dirty = (r.y >> 19) & 1u;
-  }
-  return cs | (owner << 8) | (st << 16) | (dirty << 18);
-}
-
-
-template <bool kFull, bool kVec>
-__device__ __forceinline__ void coh_wave_p(uint64_t* __restrict__ pt, uint64_t n_pages,
-                                           const uint64_t* __restrict__ ev, uint64_t n,
-                                           const uint64_t (&e)[kCohK], uint64_t eb, uint64_t ea,
-                                           uint64_t b0, uint32_t cnt,
-                                           uint32_t lh, uint64_t lhp, uint32_t cin,
-                                           uint32_t* __restrict__ wagg, uint2* __restrict__ slot,
-                                           uint32_t* __restrict__ hpg, uint32_t& inv_acc,
-                                           uint32_t& xfer_acc, uint32_t (&nf_acc)[4], uint32_t& bad,
-                                           uint32_t n_nodes, uint64_t (&en)[kCohK], uint64_t& ebn,
-                                           uint64_t& ean, uint64_t i0n, bool more) {
-  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint32_t first = t * kCohK;  // block-relative index of e[0]
-  uint32_t* pst = reinterpret_cast<uint32_t*>(pt);
-  uint32_t* pfl = pst + 1;
-  const uint64_t g0 = b0 + first;
-  bool V[kCohK];
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k) V[k] = kFull || first + k < cnt;
-
-  COH_STAMP(1);
-  // ---- P1: pages, heads, ends, write flags, node bits; validation
-  uint32_t lo[kCohK], pg[kCohK];
-  uint32_t hib = 0, mx = 0;
-  // per event (recomputed where used, to keep registers for occupancy): 2n | the "written" marker
-  // (a write's owner register), and the read-hit bit of n in both halves
-  auto n2 = [&](uint32_t k) { return (lo[k] & 0xEu) | kAw; };
-  auto rb = [&](uint32_t k) { return 0x10001u << (lo[k] & 0xEu); };
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k) {
-    lo[k] = (uint32_t)e[k];
-    pg[k] = (uint32_t)(e[k] >> 4);
-    hib |= (uint32_t)(e[k] >> 32);
-    mx = max(mx, V[k] ? (lo[k] & 0xEu) : 0u);
-  }
-  if (hib >> 4) bad = 1;                  // page ids are u32 (SPEC §1)
-  if ((mx >> 1) >= n_nodes) bad = 1;      // a node outside the page table's n_nodes
-  // neighbours: DPP inside the wave; the wave's edge events were loaded with the events (lanes 0
-  // and 63), so nothing waits on a second round trip
-  uint32_t pprev = from_prev_lane(pg[kCohK - 1]);
-  uint32_t pnext = from_next_lane(pg[0]);
-  if (lane == 0) pprev = (uint32_t)(eb >> 4);
-  if (lane == 63) pnext = (uint32_t)(ea >> 4);
-  bool H[kCohK], WR[kCohK], E7;
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k) {
-    const uint32_t pp = k ? pg[k > 0 ? k - 1 : 0] : pprev;
-    const bool origin = (k == 0) && g0 == 0;
-    H[k] = V[k] && (origin || pg[k] != pp);
-    if (V[k] && !origin && pg[k] < pp) bad = 1;
-    WR[k] = V[k] && (lo[k] & 1u);
-  }
-  // end at the lane's 8th event: the next page differs or the batch ends
-  E7 = V[kCohK - 1] && (g0 + kCohK >= n || pg[kCohK - 1] != pnext);
-  // E[k] = H[k+1] for k < 7, except at the batch's last event (partial blocks)
-  bool E[kCohK];
-#pragma unroll
-  for (uint32_t k = 0; k + 1 < kCohK; ++k) E[k] = V[k] && (H[k + 1] || !V[k + 1]);
-  E[kCohK - 1] = E7;
-  // (!V[k+1] with V[k]: event k is the block's last; in a partial block that is the batch end)
-
-  COH_STAMP(2);
-  // ---- P2: head ranks and the head list (slot s = rank + d; d = 1 when the wave opens inside a
-  // segment, whose end then parks in slot 0)
-  uint32_t hc = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k) hc += H[k] ? 1u : 0u;
-  const uint32_t hinc = wave_incl_sum(hc);
-  const uint32_t hb0 = hinc - hc, nh = lane_bcast(hinc, 63);
-  const uint32_t d = (__ballot(H[0]) & 1ull) ? 0u : 1u;
-  const uint32_t pfirst = lane_bcast(pg[0], 0);
-  uint32_t hr = hb0 + d;
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k)
-    if (H[k]) hpg[hr++] = pg[k];
-  // the block's last head (pass A snapshot) is this wave's last head when it lies here
-  const uint32_t snap = (lh != kNoHead && (lh >> 9) == wave) ? nh - 1 + d : kNoHead;
-  wave_lds_sync();
-  uint32_t fo0 = 0;  // old fault count of head `lane` (P6 stores its word from the same lane)
-  for (uint32_t r = lane; r < nh; r += 64) {
-    const uint32_t s = r + d, p = hpg[s];
-    uint64_t w = 0;
-    if (p >= n_pages)
-      bad = 1;
-    else
-      w = (s == snap) ? lhp : pt[p];
-    if (r < 64) fo0 = (uint32_t)(w >> 32);
-    slot[s] = slot_of_state((uint32_t)w);
-  }
-  wave_lds_sync();
-
-  COH_STAMP(3);
-  // ---- P3: lane aggregate (the last CONST: a head's slot or a write; then the reads after it)
-  uint32_t Ra = 0, lwn2 = 0;
-  bool A = true, LH = false;
-#pragma unroll
-  for (int k = kCohK - 1; k >= 0; --k) {
-    if (A && V[k] && !WR[k]) Ra |= rb(k);
-    if (A && WR[k]) lwn2 = n2(k);
-    if (A && H[k] && !WR[k]) LH = true;
-    A = A && !(H[k] || WR[k]);
-  }
-  uint32_t agg = Ra & 0xFFFFu;
-  if (!A) {
-    const uint32_t w2 = lwn2 & 0xEu;
-    const uint32_t cw = LH ? mword_of_slot(slot[hinc - 1 + d])
-                           : ((3u << w2) | (w2 << 15) | (6u << 24) | kXb | kConst);
-    agg = mcompose(cw, agg);
-  }
-  const uint32_t inc = wave_incl_mcompose_dpp(agg);
-  if (lane == 63) wagg[wave] = inc;
-  __syncthreads();
-  COH_STAMP(4);
-  uint32_t carry = (cin & kConst) ? mword_of_state(cin) : spread8(cin);
-  for (uint32_t w = 0; w < wave; ++w) carry = mcompose(carry, wagg[w]);
-  const uint32_t cur = mcompose(carry, from_prev_lane(inc));
-  if (!(cur & kConst) && !H[0] && V[0]) bad = 1;
-
-  // ---- the next block's events, in flight while this block is walked and written back
-  if (more) {
-    load_block_events<kVec>(ev, n, i0n, en);
-    ebn = (lane == 0 && i0n > 0 && i0n <= n) ? ev[i0n - 1] : 0ull;
-    ean = (lane == 63 && i0n + kCohK < n) ? ev[i0n + kCohK] : 0ull;
-  }
-
-  COH_STAMP(5);
-  // ---- P4: walk. The chain from one event's mask to the next stays in VGPRs: hit and write are
-  // sign-extended bit fields (0 or ~0), selections are bit-field inserts.
-  const uint2 s0 = slot_of_mword(cur);
-  uint32_t M = s0.x, O2 = s0.y, run = 0, inv2 = 0, xfer = 0, nf4 = 0, rmv = 0;
-  bool NH = true, IE = false;
-  hr = hb0 + d;
-#pragma unroll
-  for (uint32_t k = 0; k < kCohK; ++k) {
-    if (kFull || V[k]) {
-      if (H[k]) {
-        const uint2 hs = slot[hr++];
-        M = hs.x;
-        O2 = hs.y;
-        run = 0;
-        rmv = 0;
-      }
-      NH = NH && !H[k];
-      const uint32_t hm = (uint32_t)__builtin_amdgcn_sbfe((int)M, lo[k], 1u);   // ~0: hit
-      const uint32_t wm = (uint32_t)__builtin_amdgcn_sbfe((int)lo[k], 0u, 1u);  // ~0: write
-      const uint32_t wfm = wm & ~hm & kRdBits;  // a write that faults: the copyset bits
-      inv2 += (uint32_t)__popc(M & ~rb(k) & wfm);  // both halves: 2 x |copyset \ {n}|
-      xfer += ((uint16_t)O2 != (uint16_t)n2(k)) ? (wfm & 1u) : 0u;
-      const uint32_t fv = hm + 1u;  // 1: the event faults
-      nf4 += fv << ((n2(k) << 1) & 31u);
-      run += fv;
-      rmv |= ~wm & ~hm;  // a read missed
-      const uint32_t Mr = (M & (hm | kRdBits)) | rb(k);
-      M = (wm & (rb(k) | (rb(k) << 1))) | (~wm & Mr);
-      O2 = (wm & n2(k)) | (~wm & O2);
-      if (E[k]) {
-        // the end of a segment opened in an earlier lane parks in the lane's own record: its
-        // head slot may not be read yet (lanes walk their events in step)
-        const uint32_t at = NH ? kCohHeads + lane : hr - 1;
-        slot[at] = make_uint2(M, O2 + (run << 20) + (rmv & kRm));
-        IE = IE || NH;
-      }
-    }
-  }
-  const uint32_t inv = inv2 >> 1;
-  wave_lds_sync();
-
-  COH_STAMP(6);
-  // ---- P5: fault counts of segments crossing lanes (segmented over the wave)
-  const uint32_t sex = from_prev_lane(wave_incl_segsum_dpp((hc ? kConst : 0u) | run)) & ~kConst;
-  if (IE) {  // the lane's first end closes a segment opened in an earlier lane
-    uint2 rcd = slot[kCohHeads + lane];
-    rcd.y += sex << 20;
-    if (hb0 > 0) {
-      slot[hb0 + d - 1] = rcd;  // its head is in this wave (every head slot has been read)
-    } else if (pfirst < n_pages) {
-      // the wave's first segment, opened before it: its head's wave added the rest
-      pst[2 * (uint64_t)pfirst] = state_of_record(rcd);
-      const uint32_t c = (rcd.y >> 20) & 0x3FFu;
-      if (c) atomicAdd(&pfl[2 * (uint64_t)pfirst], c);
-    }
-  }
-  const bool open_end = lane_bcast(V[kCohK - 1] && !E[kCohK - 1] ? 1u : 0u, 63) != 0u;
-  if (lane == 63 && open_end) {  // the last segment continues past this wave
-    const uint32_t c = run + (NH ? sex : 0u);
-    if (c && pg[kCohK - 1] < n_pages) atomicAdd(&pfl[2 * (uint64_t)pg[kCohK - 1]], c);
-  }
-  wave_lds_sync();
-  // ---- P6: closed segments (every head but an open last one): one whole 8-B page-table word
-  // each, by consecutive lanes (whole 32-B sectors: a half-word store would make the memory
-  // read-modify-write every sector). The same lane loaded head r < 64 and kept its old fault
-  // count; later heads (waves of many short segments) re-read theirs: no other wave touches a
-  // page whose segment starts and ends here.
-  const uint32_t nclosed = (open_end && nh > 0) ? nh - 1 : nh;  // nh = 0: one open segment
-  for (uint32_t r = lane; r < nclosed; r += 64) {
-    const uint32_t s = r + d, p = hpg[s];
-    if (p < n_pages) {
-      const uint2 rcd = slot[s];
-      const uint32_t fo = r < 64 ? fo0 : (s == snap ? (uint32_t)(lhp >> 32) : pfl[2 * (uint64_t)p]);
-      pt[p] = (uint64_t)state_of_record(rcd) |
-              ((uint64_t)(fo + ((rcd.y >> 20) & 0x3FFu)) << 32);
-    }
-  }
-
-  COH_STAMP(7);
-  // ---- totals: per lane, node faults widened from nibbles to 16-bit fields (nodes 0|4, 2|6,
-  // 1|5, 3|7); wave sums once per workgroup at the end
-  inv_acc += inv;
-  xfer_acc += xfer;
-  const uint32_t ev4 = nf4 & 0x0F0F0F0Fu, od4 = (nf4 >> 4) & 0x0F0F0F0Fu;
-  nf_acc[0] += ev4 & 0x00FF00FFu;
-  nf_acc[1] += (ev4 >> 8) & 0x00FF00FFu;
-  nf_acc[2] += od4 & 0x00FF00FFu;
-  nf_acc[3] += (od4 >> 8) & 0x00FF00FFu;
-}
-
-// Persistent pass C over blocks [b_lo, b_hi): a workgroup walks blocks b_lo + blockIdx.x,
-// + gridDim.x, ... and keeps its totals in registers (one partial row per wave at the end, row
-// index row_base + blockIdx.x). Node-fault fields are 16 bits per lane: at most 8 per block, so
-// a workgroup may take up to 8191 blocks (the launcher sizes the grid for that).
-#ifndef GDSM_COH_PWPE
-#define GDSM_COH_PWPE 5
-#endif
-template <bool kFull, bool kVec>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GDSM_COH_PWPE))) void coh_apply_p_kernel(
-    uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
-    uint64_t b_lo, uint64_t b_hi, const uint32_t* __restrict__ carry,
-    const uint32_t* __restrict__ last_head, const uint64_t* __restrict__ head_pt,
-    uint32_t* __restrict__ partial, uint64_t row_base, uint32_t* __restrict__ err,
-    uint32_t n_nodes) {
-  __shared__ uint32_t wagg[2][4];  // by block parity: a wave may run one block ahead
-  __shared__ uint2 slot[4][kCohHeads + 64];  // head slots, then one end record per lane
-  __shared__ uint32_t hpg[4][kCohHeads];
-  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  uint32_t bad = 0, inv = 0, xfer = 0;
-  uint32_t nf[4] = {0, 0, 0, 0};
-  uint64_t e[kCohK], eb = 0, ea = 0;
-  uint64_t b = b_lo + blockIdx.x;
-  if (b < b_hi) {
-    const uint64_t i0 = b * kCohBlock + t * kCohK;
-    load_block_events<kVec>(ev, n, i0, e);
-    eb = (lane == 0 && i0 > 0 && i0 <= n) ? ev[i0 - 1] : 0ull;
-    ea = (lane == 63 && i0 + kCohK < n) ? ev[i0 + kCohK] : 0ull;
-  }
-  for (uint32_t par = 0; b < b_hi; b += gridDim.x, par ^= 1u) {
-    COH_STAMP(0);
-    const uint64_t b0 = b * kCohBlock, bn = b + gridDim.x;
-    const uint32_t cnt = (uint32_t)min((uint64_t)kCohBlock, n - b0);
-    uint64_t en[kCohK], ebn = 0, ean = 0;
-    coh_wave_p<kFull, kVec>(pt, n_pages, ev, n, e, eb, ea, b0, cnt, last_head[b], head_pt[b],
-                            carry[b], wagg[par], slot[wave], hpg[wave], inv, xfer, nf, bad,
-                            n_nodes, en, ebn, ean, bn * kCohBlock + t * kCohK, bn < b_hi);
-#pragma unroll
-    for (uint32_t k = 0; k < kCohK; ++k) e[k] = en[k];
-    eb = ebn;
-    ea = ean;
-  }
-  const uint32_t v[10] = {inv, xfer, nf[0] & 0xFFFFu, nf[2] & 0xFFFFu, nf[1] & 0xFFFFu,
-                          nf[3] & 0xFFFFu, nf[0] >> 16, nf[2] >> 16, nf[1] >> 16, nf[3] >> 16};
-  uint32_t mine = 0;
-#pragma unroll
-  for (int q = 0; q < 10; ++q) {
-    const uint32_t sm = wave_sum(v[q]);
-    if (lane == (uint32_t)q) mine = sm;
-  }
-  if (lane < 10) partial[((row_base + blockIdx.x) * 4 + wave) * 10 + lane] = mine;
-  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
-}
-
 // ---------------------------------------------------------------- D: totals
 __global__ __launch_bounds__(256) void coh_reduce_kernel(const uint32_t* __restrict__ partial,
                                                          uint64_t nb,
@@ -1032,9 +668,9 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 // (output invalid). (Rounds 1-2 also carried the round-1 block-scan kernel and a hit-mask
 // restatement; both were slower and are in the history.)
 #ifdef GDSM_MEASURE
-constexpr int kCohVariants = 4;
+constexpr int kCohVariants = 3;
 #else
-constexpr int kCohVariants = 2;
+constexpr int kCohVariants = 1;
 #endif
 static int coh_variant_from_env() {
   const char* e = getenv("GDSM_COH_VARIANT");
@@ -1095,48 +731,21 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
     hipLaunchKernelGGL(coh_rescan_kernel, dim3((unsigned)ng), dim3(256), 0, s, agg, nb, groups,
                        carry);
   }
-  uint64_t rows = nb * 4;  // partial rows of totals: one per wave of pass C
   {
     ProfScope ps(prof, 7, s);
     const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
-    if (g_coh_variant == 1) {
-      const uint64_t nfull = n_events / kCohBlock;
-      static int grid_by_dev[64] = {};  // resident workgroups of the persistent kernel, per device
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      int& g = grid_by_dev[dev & 63];
-      if (!g) {
-        int cus = 256, per = 5;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, coh_apply_p_kernel<true, true>,
-                                                            256, 0);
-        g = cus * (per > 0 ? per : 5);
-      }
-      uint64_t grid = min((uint64_t)g, nfull);
-      grid = max(grid, (nfull + 7999) / 8000);  // 16-bit node-fault fields: <= 8191 blocks each
-      auto kfull = vec ? coh_apply_p_kernel<true, true> : coh_apply_p_kernel<true, false>;
-      auto ktail = vec ? coh_apply_p_kernel<false, true> : coh_apply_p_kernel<false, false>;
-      if (nfull)
-        hipLaunchKernelGGL(kfull, dim3((unsigned)grid), dim3(256), 0, s, pt, n_pages, events,
-                           n_events, (uint64_t)0, nfull, carry, lh, head_pt, partial, (uint64_t)0,
-                           err, n_nodes);
-      if (nb > nfull)
-        hipLaunchKernelGGL(ktail, dim3(1), dim3(256), 0, s, pt, n_pages, events, n_events, nfull,
-                           nb, carry, lh, head_pt, partial, grid, err, n_nodes);
-      rows = (grid + (nb > nfull ? 1 : 0)) * 4;
-    } else {
 #ifdef GDSM_MEASURE
-      auto kern = !vec                 ? coh_apply_block_kernel<0, false>
-                  : g_coh_variant == 2 ? coh_apply_block_kernel<1, true>
-                  : g_coh_variant == 3 ? coh_apply_block_kernel<2, true>
-                                       : coh_apply_block_kernel<0, true>;
+    auto kern = !vec                 ? coh_apply_block_kernel<0, false>
+                : g_coh_variant == 1 ? coh_apply_block_kernel<1, true>
+                : g_coh_variant == 2 ? coh_apply_block_kernel<2, true>
+                                     : coh_apply_block_kernel<0, true>;
 #else
-      auto kern = vec ? coh_apply_block_kernel<0, true> : coh_apply_block_kernel<0, false>;
+    auto kern = vec ? coh_apply_block_kernel<0, true> : coh_apply_block_kernel<0, false>;
 #endif
-      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, pt, n_pages, events, n_events,
-                         nb, carry, lh, head_pt, partial, err, n_nodes);
-    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, s, pt, n_pages, events, n_events,
+                       nb, carry, lh, head_pt, partial, err, n_nodes);
   }
+  const uint64_t rows = nb * 4;  // partial rows of totals: one per wave of pass C
   uint64_t g = (rows + 255) / 256;
   if (g > 1024) g = 1024;
   {
