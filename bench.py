@@ -88,56 +88,25 @@ def payload_bytes(rec_off: np.ndarray, data: np.ndarray) -> int:
     return int((w[first_hdr + within] >> 16).astype(np.int64).sum())
 
 
-def _cpu_leg(oracle, n: int, mode: int, ppm: int, seed: int, first_page: int, seconds: float,
-             t_start: float, out: list):
-    """One thread of the CPU baseline: diff+apply passes over its own n-page sample until
-    `seconds` after t_start. The oracle is a ctypes CDLL, so the GIL is released in its calls."""
-    twin, cur = oracle.gen_pages(n, seed=seed, mode=mode, ppm=ppm, first_page=first_page)
-    rep = twin.copy()
-    ro, _ = oracle.diff_pages(twin, cur)  # warm-up, sizes the stream
-    cap, reps = int(ro[-1]), 0
-    while time.perf_counter() < t_start:
-        time.sleep(0.001)
-    t0 = time.perf_counter()
-    while True:
-        ro, data = oracle.diff_pages(twin, cur, cap=cap)
-        oracle.apply(rep, ro, data)
-        reps += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    out.append((reps * n, time.perf_counter() - t0, np.array_equal(rep, cur)))
-
-
 def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
-    """The C oracle (oracle/liboracle.so) on a bounded sample of the workload: one thread, then
-    all of this process's CPU share (single-core and all-core)."""
-    import threading
+    """The C oracle (oracle/liboracle.so, -O3, OpenMP, timed in C) on a bounded sample of the
+    workload: one thread, then all of this process's CPU share (single-core and
+    all-core), each thread repeating diff + apply passes over its own sample."""
     from oracle import oracle
-    n = 32768
-    one: list = []
-    _cpu_leg(oracle, n, mode, ppm, seed, 0, seconds / 2, time.perf_counter(), one)
-    pages1, dt1, ok1 = one[0]
+    n1, nper = 32768, 16384
+    pages1, dt1, ok1 = oracle.bench_diff_apply(n1, mode, ppm, seed, seconds / 2, 1)
     assert ok1
     # The box exports OMP_NUM_THREADS = its CPU share; os.cpu_count() is the whole machine.
     nt = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     nt = max(1, min(nt, len(os.sched_getaffinity(0)), 16))
-    nper = n // 2
-    res: list = []
-    start = time.perf_counter() + 0.5 + 0.05 * nt  # every thread's sample is built by then
-    ths = [threading.Thread(target=_cpu_leg,
-                            args=(oracle, nper, mode, ppm, seed, i * nper, seconds / 2, start, res))
-           for i in range(nt)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    assert len(res) == nt and all(r[2] for r in res)
-    alln = sum(r[0] for r in res) / max(r[1] for r in res)
-    out = {"value": round(alln, 1), "unit": "pages/s", "cores": nt, "kind": "port",
-           "sample": f"{nt} threads x {nper} pages each, repeated diff+apply passes of the same "
-                     f"workload (seed {seed}) for {seconds / 2:.1f} s, oracle/gdsm_oracle.c",
+    pages, dt, ok = oracle.bench_diff_apply(nper, mode, ppm, seed, seconds / 2, nt)
+    assert ok
+    out = {"value": round(pages / dt, 1), "unit": "pages/s", "cores": nt, "kind": "port",
+           "sample": f"{nt} OpenMP threads x {nper} pages each (thread t: pages [t*{nper}, "
+                     f"(t+1)*{nper}) of the workload, seed {seed}), repeated diff+apply passes "
+                     f"for {seconds / 2:.1f} s, oracle/gdsm_oracle.c -O3, timed in C",
            "single_thread": {"value": round(pages1 / dt1, 1), "cores": 1,
-                             "sample": f"{n} pages x {pages1 // n} passes, {dt1:.1f} s"}}
+                             "sample": f"{n1} pages x {pages1 // n1} passes, {dt1:.1f} s"}}
     drv = oracle.REF_DRIVER
     if drv.exists():
         try:

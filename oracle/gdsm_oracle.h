@@ -62,6 +62,13 @@ int or_coherence(uint32_t* state, uint32_t* faults, uint64_t n_pages, uint32_t n
 void or_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page, uint64_t n,
                    uint64_t seed, uint32_t n_nodes, uint32_t write_pct);
 
+/* bench.py's CPU baseline only (gdsm_oracle_bench.c): `threads` OpenMP threads, thread t on
+ * pages [t*n, (t+1)*n) of the SPEC §6 workload, repeat diff + apply passes for `seconds`.
+ * *pages = pages processed by all threads, *elapsed = the slowest thread's seconds, *ok = every
+ * replica equals its current arena. Returns 0, -12 (allocation) or -22. */
+int or_bench_diff_apply(uint64_t n, int mode, uint32_t ppm, uint64_t seed, double seconds,
+                        int threads, uint64_t* pages, double* elapsed, int* ok);
+
 #ifdef __cplusplus
 }
 #endif

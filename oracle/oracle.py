@@ -34,6 +34,9 @@ def lib():
         L.or_coh_init.argtypes = [vp, vp, u64, C.c_uint32]
         L.or_coherence.argtypes = [vp, vp, u64, C.c_uint32, vp, u64, vp]
         L.or_gen_events.argtypes = [vp, vp, u64, u64, u64, C.c_uint32, C.c_uint32]
+        L.or_bench_diff_apply.argtypes = [u64, C.c_int, C.c_uint32, u64, C.c_double, C.c_int,
+                                          C.POINTER(u64), C.POINTER(C.c_double),
+                                          C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -128,3 +131,14 @@ def ref_nw_batch(cases):
         out.append((raw[i:i + L], raw[i + L:i + 2 * L]))
         i += 2 * L
     return out
+
+
+def bench_diff_apply(n, mode, ppm, seed, seconds, threads):
+    """bench.py's CPU baseline: `threads` OpenMP threads, each repeating diff + apply passes
+    over its own n-page sample for `seconds` (timed in C). Returns (pages, seconds, replicas ok)."""
+    pages, dt, ok = C.c_uint64(), C.c_double(), C.c_int()
+    rc = lib().or_bench_diff_apply(n, mode, ppm, seed, seconds, threads, C.byref(pages),
+                                   C.byref(dt), C.byref(ok))
+    if rc:
+        raise OSError(-rc, "or_bench_diff_apply")
+    return pages.value, dt.value, bool(ok.value)
