@@ -52,6 +52,11 @@ SIGNATURES = {
     "gdsm_memcpy_h2d": (C.c_int, [vp, vp, vp, C.c_uint64]),
     "gdsm_memcpy_d2h": (C.c_int, [vp, vp, vp, C.c_uint64]),
     "gdsm_memcpy_d2d": (C.c_int, [vp, vp, vp, C.c_uint64]),
+    "gdsm_capture_begin": (C.c_int, [vp]),
+    "gdsm_capture_join": (C.c_int, [vp, vp]),
+    "gdsm_capture_end": (C.c_int, [vp, C.POINTER(vp)]),
+    "gdsm_graph_launch": (C.c_int, [vp, vp]),
+    "gdsm_graph_destroy": (C.c_int, [vp]),
     "gdsm_prof_enable": (C.c_int, [vp, C.c_int]),
     "gdsm_prof_read": (C.c_int, [vp, C.POINTER(C.c_double), u64p]),
     "gdsm_gen_pages": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,

@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <new>
@@ -48,8 +49,13 @@ int ensure_aux(gdsm_ctx* ctx) {
   return 0;
 }
 
+// Contexts with a graph capture open (gdsm_capture_begin): workspaces may not move under a
+// capture, since the recorded kernels keep their addresses.
+std::atomic<int> g_capturing{0};
+
 int ensure(uint8_t** buf, uint64_t* have, uint64_t need) {
   if (*have >= need) return 0;
+  if (g_capturing.load()) return -EBUSY;  // size workspaces with gdsm_reserve before capturing
   if (*buf) (void)hipFree(*buf);
   *buf = nullptr;
   *have = 0;
@@ -237,10 +243,103 @@ void* gdsm_stream(gdsm_ctx* ctx) {
 
 int gdsm_sync(gdsm_ctx* ctx) {
   if (!ctx) return -EINVAL;
+  if (ctx->capturing) return -EBUSY;  // a recording stream cannot be waited for
   CtxGuard g(ctx);
   if (g.rc) return g.rc;
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   return check_and_clear_err(ctx);
+}
+
+// ---- HIP graphs ---------------------------------------------------------------------------
+struct gdsm_graph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  int device = 0;
+};
+
+int gdsm_capture_begin(gdsm_ctx* ctx) {
+  if (!ctx || ctx->capturing) return -EINVAL;
+  CtxGuard g(ctx);  // pending async applies join the main stream before the capture opens
+  if (g.rc) return g.rc;
+  GDSM_TRY(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+  ctx->capturing = true;
+  ++g_capturing;
+  return 0;
+}
+
+int gdsm_capture_join(gdsm_ctx* ctx, gdsm_ctx* other) {
+  if (!ctx || !other || !ctx->capturing || other == ctx || other->capturing ||
+      other->device != ctx->device || other->aux_pending)
+    return -EINVAL;
+  DeviceGuard g(ctx->device);
+  hipEvent_t e = nullptr;
+  GDSM_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (hipEventRecord(e, ctx->stream) != hipSuccess ||
+      hipStreamWaitEvent(other->stream, e, 0) != hipSuccess) {
+    (void)hipEventDestroy(e);
+    return -EIO;
+  }
+  ctx->capture_events.push_back(e);
+  ctx->capture_joined.push_back(other);
+  other->capturing = true;
+  return 0;
+}
+
+int gdsm_capture_end(gdsm_ctx* ctx, gdsm_graph** out) {
+  if (!ctx || !out || !ctx->capturing) return -EINVAL;
+  DeviceGuard g(ctx->device);
+  int rc = 0;
+  for (gdsm_ctx* o : ctx->capture_joined) {  // the joined streams rejoin before the capture ends
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(e, o->stream) != hipSuccess ||
+        hipStreamWaitEvent(ctx->stream, e, 0) != hipSuccess)
+      rc = -EIO;
+    if (e) ctx->capture_events.push_back(e);
+    o->capturing = false;
+  }
+  hipGraph_t graph = nullptr;
+  const hipError_t ee = hipStreamEndCapture(ctx->stream, &graph);
+  ctx->capturing = false;
+  --g_capturing;
+  for (hipEvent_t e : ctx->capture_events) (void)hipEventDestroy(e);
+  ctx->capture_events.clear();
+  ctx->capture_joined.clear();
+  if (ee != hipSuccess || !graph || rc) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc ? rc : map_err(ee) ? map_err(ee) : -EIO;
+  }
+  gdsm_graph* gg = new (std::nothrow) gdsm_graph;
+  if (!gg) {
+    (void)hipGraphDestroy(graph);
+    return -ENOMEM;
+  }
+  gg->graph = graph;
+  gg->device = ctx->device;
+  if (hipGraphInstantiate(&gg->exec, graph, nullptr, nullptr, 0) != hipSuccess) {
+    (void)hipGraphDestroy(graph);
+    delete gg;
+    return -EIO;
+  }
+  *out = gg;
+  return 0;
+}
+
+int gdsm_graph_launch(gdsm_ctx* ctx, const gdsm_graph* gg) {
+  if (!ctx || !gg || ctx->capturing || gg->device != ctx->device) return -EINVAL;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  GDSM_TRY(hipGraphLaunch(gg->exec, ctx->stream));
+  return 0;
+}
+
+int gdsm_graph_destroy(gdsm_graph* gg) {
+  if (!gg) return -EINVAL;
+  DeviceGuard g(gg->device);
+  if (gg->exec) (void)hipGraphExecDestroy(gg->exec);
+  if (gg->graph) (void)hipGraphDestroy(gg->graph);
+  delete gg;
+  return 0;
 }
 
 static int page_copy(gdsm_ctx* ctx, int which, uint64_t first, uint64_t n, void* host, bool up) {
@@ -274,6 +373,12 @@ int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events) {
   int rc = 0;
   if (diff_pages) {
     rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(diff_pages));
+    // checked copies of the id lists of diff / twin / apply on the main stream
+    if (!rc) {
+      uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[0]);
+      rc = ensure(&buf, &ctx->ids_safe_bytes[0], 4 * diff_pages);
+      ctx->ids_safe[0] = reinterpret_cast<uint32_t*>(buf);
+    }
   }
   if (!rc && coh_events)
     rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(coh_events));

@@ -6,6 +6,7 @@
 
 #include <map>
 #include <set>
+#include <vector>
 
 #include "gdsm.h"
 #include "gdsm_prof.h"
@@ -52,6 +53,10 @@ struct gdsm_ctx {
   // apply's list is never overwritten by a call on the main stream
   uint32_t* ids_safe[2] = {nullptr, nullptr};
   uint64_t ids_safe_bytes[2] = {0, 0};
+  // graph capture (gdsm_capture_*): open on this context's stream (or joined into another's)
+  bool capturing = false;
+  std::vector<gdsm_ctx*> capture_joined;
+  std::vector<hipEvent_t> capture_events;
 };
 
 namespace gdsm {

@@ -493,14 +493,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
 }
 
 // ------------------------------------------------------------------------- apply (SPEC §4)
-// A wave takes 64 consecutive records. It stages as many of them as fit in an 8 KiB LDS window
-// with coalesced loads (one global round trip for the whole window), then handles them one by
-// one out of LDS: the run list becomes the page's 4096-bit dirty mask by toggling a bit at each
-// run start and end and taking a prefix-XOR (lane l owns bytes [64l, 64l+64)); the payload index
-// of a byte is the popcount of the dirty bits before it. The replica is only STORED to (16-B
-// stores for whole chunks, dword stores for whole dwords, byte stores otherwise), never read, so
-// no wave ever waits on a replica load. A record larger than the window is read from global.
-constexpr uint32_t kApplyWin = 8192;  // bytes of records staged per wave
+// A wave takes 64 (short lists: 4) consecutive records. It stages as many of them as fit in an LDS
+// window (kApplyWin*) with coalesced loads, one global round trip per window, then
+// applies them four at a time, one record per 16-lane DPP row (apply_rows: validate every header,
+// then spread the (run, 16-B chunk) pairs over the row). The replica is only STORED to (16-B
+// stores for whole chunks, 8-B / dword stores for whole words, byte stores otherwise), never
+// read. A record larger than the window is read from global by row 0.
+// Bytes of records staged per wave: 8 KiB for long lists (LDS for occupancy), 12 KiB for short
+// ones (every well-formed record fits, so dense records never take the global path).
+constexpr uint32_t kApplyWinLong = 8192, kApplyWinShort = 12288;
+static_assert(kApplyWinShort >= 10244, "every well-formed record (GDSM_MAX_RECORD) fits");
 
 // Stores the payload bytes selected by `mask` (16 bits, chunk of 16 B at dst) from pay[pp..].
 // Replica store; kNT = nontemporal (streaming) cache policy.
@@ -612,6 +614,18 @@ __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32
     const uint32_t cinc = row_incl_sum(nch);
     const uint32_t cex = cinc - nch;
     const uint32_t T = row_last(cinc);
+    if (__ballot(nch > 2u) == 0) {
+      // short runs (<= 2 chunks each, e.g. word-sized edits): every lane stores its own run, no
+      // cross-lane lookup (a 4-step bpermute search per 16 pairs dominated many-run records);
+      // longer runs keep the spread below, whose 16 lanes store consecutive chunks
+      for (uint32_t c = 0; c < nch; ++c) {
+        if (kMode != 1)
+          store_run_chunk<kMode == 2>(page, ((off >> 4) + c) << 4, off, end, rec8, pp);
+        else
+          sink += off ^ end ^ (uint32_t)rec8[pp];
+      }
+      continue;
+    }
     const uint32_t tmax = lane_bcast(wave_incl_max(T), 63);
     for (uint32_t g = lr; g < ((tmax + 15u) & ~15u); g += 16) {
       uint32_t i = 0;
@@ -635,21 +649,21 @@ __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32
   return !bad;
 }
 
-template <int kMode>
+template <int kMode, uint32_t kApplyWin>
 __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target,
                                                     const uint32_t* __restrict__ ids, uint64_t n,
                                                     const uint64_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ data,
-                                                    uint32_t* __restrict__ err) {
+                                                    uint32_t* __restrict__ err, uint32_t per_task) {
   __shared__ __attribute__((aligned(16))) uint32_t win_all[4][kApplyWin / 4];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, row = lane >> 4;
   uint32_t* win = win_all[wave];
-  const uint64_t ntask = (n + 63) / 64;
+  const uint64_t ntask = (n + per_task - 1) / per_task;
   uint32_t bad = 0, sink = 0;
   for (uint64_t task = (uint64_t)blockIdx.x * 4 + wave; task < ntask;
        task += (uint64_t)gridDim.x * 4) {
-    const uint64_t a = task * 64;
-    const uint32_t cnt = (uint32_t)min((uint64_t)64, n - a);
+    const uint64_t a = task * per_task;
+    const uint32_t cnt = (uint32_t)min((uint64_t)per_task, n - a);
     const uint64_t my_off = rec_off[a + min(lane, cnt)];  // lane l: start of record a+l
     const uint64_t end_off = rec_off[a + cnt];
     uint32_t j = 0;
@@ -704,31 +718,39 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
 // ------------------------------------------------------------------------- launchers
 // Diff geometry, gdsm_tune("diff_variant", v) or GDSM_DIFF_VARIANT=v; every variant writes the
 // same canonical stream (tests/test_gpu_pages.py checks each):
-//   0  automatic (default): 32 pages per wave when the caller's stream capacity allows at most
-//      384 B per page (sparse writes: config 2's ~66 B records; fewer look-backs), else 16
+//   0  automatic (default): 2 pages per wave for short lists (n <= 32768: a wave walks its
+//      pages one after the other, so a few dozen pages must not share one wave), else 32 pages
+//      per wave when the caller's stream capacity allows at most 384 B per page (sparse writes:
+//      config 2's ~66 B records; fewer look-backs), else 16
 //   1  16 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 //   2  32 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
+//   3  2 pages per wave
 // Measurement-only kernels (invalid output) are not part of the library.
 static int g_diff_variant = -1;
 static int diff_variant() {
   if (g_diff_variant < 0) {
     const char* e = getenv("GDSM_DIFF_VARIANT");
     const int v = e ? atoi(e) : 0;
-    g_diff_variant = (v >= 0 && v <= 2) ? v : 0;
+    g_diff_variant = (v >= 0 && v <= 3) ? v : 0;
   }
   return g_diff_variant;
 }
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 2) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 3) {
     g_diff_variant = (int)value;
     return 0;
   }
   return coh_tune(key, value);
 }
 
-// Single-pass diff workspace: the ticket counter and one status granule per 16-page unit (the
-// smaller unit, so any geometry fits).
-uint64_t diff_workspace_bytes(uint64_t n) { return 8 * (1 + (n + 15) / 16) + 64; }
+// Single-pass diff workspace: the ticket counter and one status granule per unit of the
+// smallest geometry that n may take (2 pages up to kDiffShort, else 16), non-decreasing in n so
+// a workspace reserved for n fits every shorter list.
+constexpr uint64_t kDiffShort = 32768;
+uint64_t diff_workspace_bytes(uint64_t n) {
+  const uint64_t u16 = (n + 15) / 16, u2 = (min(n, kDiffShort) + 1) / 2;
+  return 8 * (1 + max(u16, u2)) + 64;
+}
 
 static inline unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap) {
   uint64_t g = (work + per_block - 1) / per_block;
@@ -776,15 +798,17 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        uint64_t ws_bytes, hipStream_t s, Prof* prof) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   int v = diff_variant();
-  if (v == 0) v = (cap <= 384 * n) ? 2 : 1;
-  const uint32_t U = v == 2 ? 32 : 16;
+  if (v == 0) v = n <= kDiffShort ? 3 : (cap <= 384 * n) ? 2 : 1;
+  const uint32_t U = v == 3 ? 2 : v == 2 ? 32 : 16;
   const uint64_t nunits = (n + U - 1) / U;
   if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
   // ticket counter + status granules, zeroed per launch (outside the timed kernel)
   hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
   if (e != hipSuccess) return e;
   ProfScope ps(prof, 0, s);
-  auto kern = v == 2 ? diff_single_kernel<32, 8192, 4> : diff_single_kernel<16, 8192, 4>;
+  auto kern = v == 3   ? diff_single_kernel<2, 8192, 4>
+              : v == 2 ? diff_single_kernel<32, 8192, 4>
+                       : diff_single_kernel<16, 8192, 4>;
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, n,
                      rec_off, data, cap, reinterpret_cast<uint64_t*>(ws));
   return hipGetLastError();
@@ -795,9 +819,14 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
   ProfScope ps(prof, 3, s);
-  // one 64-record task per wave, 4 waves per workgroup: no workgroup launched without work
-  hipLaunchKernelGGL(apply_kernel<0>, dim3(grid_for(n, 256, 65536)), dim3(256), 0, s, target, ids, n,
-                     rec_off, data, err);
+  // one task per wave, 4 waves per workgroup: no workgroup launched without work. A task is 64
+  // records (one staging window serves many small records); short lists take 4 per task, so a
+  // few dense records are spread over waves instead of queueing in one
+  const bool short_list = n <= 16384;
+  const uint32_t per_task = short_list ? 4u : 64u;
+  auto kern = short_list ? apply_kernel<0, kApplyWinShort> : apply_kernel<0, kApplyWinLong>;
+  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4 * per_task, 65536)), dim3(256), 0, s, target, ids,
+                     n, rec_off, data, err, per_task);
   return hipGetLastError();
 }
 

@@ -145,6 +145,21 @@ class Runs:
             check(lib().gdsm_runs_free(self.ctx.handle, C.byref(self.s)), "gdsm_runs_free")
 
 
+class Graph:
+    """An instantiated HIP graph of recorded libgdsm calls (Context.capture_end)."""
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    def launch(self, ctx: "Context"):
+        check(lib().gdsm_graph_launch(ctx.handle, self.handle), "gdsm_graph_launch")
+
+    def destroy(self):
+        if self.handle:
+            lib().gdsm_graph_destroy(self.handle)
+            self.handle = None
+
+
 class Context:
     """One shard of pages on one GPU: TWIN / CURRENT / REPLICA arenas + the page table."""
 
@@ -190,6 +205,19 @@ class Context:
 
     def sync(self):
         check(lib().gdsm_sync(self.handle), "gdsm_sync")
+
+    # -- HIP graphs (gdsm_capture_*): record a launch-bound sequence once, replay it at once
+    def capture_begin(self, *others: "Context"):
+        """Starts recording this context's asynchronous calls (and those of `others`, joined in
+        order) into one graph; end with capture_end()."""
+        check(lib().gdsm_capture_begin(self.handle), "gdsm_capture_begin")
+        for o in others:
+            check(lib().gdsm_capture_join(self.handle, o.handle), "gdsm_capture_join")
+
+    def capture_end(self) -> "Graph":
+        g = C.c_void_p()
+        check(lib().gdsm_capture_end(self.handle, C.byref(g)), "gdsm_capture_end")
+        return Graph(g.value)
 
     PROF_STAGES = ("diff", "scan", "pack", "apply", "twin", "coh_tail", "coh_scan", "coh_apply",
                    "coh_reduce", "nw_fill", "nw_trace", "exchange")

@@ -16,7 +16,8 @@ Per round (one row per node, gallocy_amd/trace.py):
      different nodes at disjoint bytes: their records hit the same home page with disjoint
      runs, which the store-only apply handles without a read-modify-write race.
 The trace, the rows' values and the page lists are prepared on the host before the timed
-replay; a round is then only asynchronous launches on two streams (page table, page data).
+replay; a round is then only asynchronous launches on two streams (page table, page data),
+or, with run(graph=True), one HIP graph of all rounds recorded beforehand.
 At the end the home copies must equal the zone after the whole multiplication, and the page
 table / totals must equal the oracle's sequential fold of the same events.
 """
@@ -100,15 +101,38 @@ class MmultReplay:
         self.data.diff(ids, n=n, out=self._runs)                                           # 4
         self.data.apply(self._runs, "replica", home)                                       # 5
 
-    def run(self) -> float:
+    def run(self, graph: bool = False) -> float:
+        """Replays every round once; returns the seconds from the first launch to the end.
+        graph=False (default): the calls are issued eagerly on the two streams. graph=True: the
+        rounds' calls on both contexts are recorded once into one HIP graph (gdsm_capture_*,
+        untimed) and the replay is one graph launch. On MI355X the graph replay is the slower of
+        the two (0.40 vs 0.35 ms per round at NDIM = 1000): a round is ~20 dependent tiny
+        operations, bound by their device-side cost, not by the host issuing them."""
         self.data.sync()
         self.pt.sync()
-        t0 = time.perf_counter()
-        for r in range(self.T.rounds):
-            self.round(r)
-        self.data.sync()
+        self.graph_build_s = 0.0
+        if graph:
+            tb = time.perf_counter()
+            self.data.capture_begin(self.pt)
+            try:
+                for r in range(self.T.rounds):
+                    self.round(r)
+            finally:
+                g = self.data.capture_end()
+            self.graph_build_s = time.perf_counter() - tb
+            t0 = time.perf_counter()
+            g.launch(self.data)
+            self.data.sync()
+            dt = time.perf_counter() - t0
+            g.destroy()
+        else:
+            t0 = time.perf_counter()
+            for r in range(self.T.rounds):
+                self.round(r)
+            self.data.sync()
+            self.pt.sync()
+            dt = time.perf_counter() - t0
         self.pt.sync()
-        dt = time.perf_counter() - t0
         self.totals = self.d_tot.download(np.uint64, 10 * self.T.rounds).reshape(-1, 10).sum(0).astype(np.int64)
         return dt
 

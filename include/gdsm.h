@@ -55,9 +55,9 @@ enum gdsm_init_flags {
 };
 /* Per-kernel stages timed by gdsm_prof_* (HIP events on the context stream). */
 enum gdsm_prof_stage {
-  GDSM_PROF_DIFF = 0, /* diff_compact_kernel: the dominant kernel of the hot path */
-  GDSM_PROF_SCAN,
-  GDSM_PROF_PACK,
+  GDSM_PROF_DIFF = 0, /* diff_single_kernel: the dominant kernel of the hot path */
+  GDSM_PROF_SCAN,     /* unused since round 2 (the diff packs its stream itself) */
+  GDSM_PROF_PACK,     /* unused since round 2 */
   GDSM_PROF_APPLY,
   GDSM_PROF_TWIN,
   GDSM_PROF_COH_TAIL,
@@ -107,6 +107,26 @@ int gdsm_memcpy_h2d(gdsm_ctx* ctx, void* dev, const void* host, uint64_t bytes);
 int gdsm_memcpy_d2h(gdsm_ctx* ctx, void* host, const void* dev, uint64_t bytes);
 /* Asynchronous device-to-device copy on the context stream. */
 int gdsm_memcpy_d2d(gdsm_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+
+/* HIP graphs: record a launch-bound sequence once and replay it with one launch.
+ * - Between gdsm_capture_begin(ctx) and gdsm_capture_end(ctx, &g), the asynchronous calls on ctx
+ *   are recorded, not run: gdsm_twin, gdsm_diff, gdsm_apply, gdsm_memcpy_d2d,
+ *   gdsm_coherence_batch_async and the generators.
+ * - gdsm_capture_join(ctx, other) adds a second context on the same device. Its asynchronous
+ *   calls are recorded into the same graph, ordered after what ctx had recorded when it joined.
+ *   ctx's recording waits for them at gdsm_capture_end.
+ * - Size the workspaces beforehand with gdsm_reserve: a call that would grow one fails with
+ *   -EBUSY, and so does gdsm_sync on a recording context. Other calls that synchronise the host
+ *   fail too.
+ * - gdsm_graph_launch enqueues the whole graph on ctx's stream; gdsm_sync reports its
+ *   device-side failures as usual. Every recorded pointer must stay valid while the graph
+ *   lives. */
+typedef struct gdsm_graph gdsm_graph;
+int gdsm_capture_begin(gdsm_ctx* ctx);
+int gdsm_capture_join(gdsm_ctx* ctx, gdsm_ctx* other);
+int gdsm_capture_end(gdsm_ctx* ctx, gdsm_graph** out);
+int gdsm_graph_launch(gdsm_ctx* ctx, const gdsm_graph* g);
+int gdsm_graph_destroy(gdsm_graph* g);
 
 /* Per-kernel timing: when enabled, every kernel the context launches is bracketed by HIP events
  * on its stream; gdsm_prof_read synchronises and returns the summed milliseconds and launch

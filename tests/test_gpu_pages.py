@@ -507,9 +507,9 @@ def _lds_overflow_pages(rng, n):
     return tw, cu
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_diff_variants_bit_exact(variant, golden):
-    """Every diff geometry (gdsm_tune "diff_variant": automatic, 16 or 32 pages per wave) is
+    """Every diff geometry (gdsm_tune "diff_variant": automatic, 16, 32 or 2 pages per wave) is
     bit-exact on edge pages, random byte densities (pages past the 64-dirty-chunk fast path),
     records that overflow the wave's LDS buffer, and clustered and uniform synthetic writes."""
     L = _lib.load()

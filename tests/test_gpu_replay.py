@@ -10,14 +10,17 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("ndim,nodes", [(64, 1), (64, 2), (96, 4), (64, 8), (257, 3),
-                                        (1000, 1), (1000, 2), (1000, 4), (1000, 8)])
-def test_mmult_replay_end_to_end(ndim, nodes):
+@pytest.mark.parametrize("ndim,nodes,graph", [(64, 1, False), (64, 2, False), (96, 4, False),
+                                              (64, 8, False), (257, 3, False), (1000, 1, False),
+                                              (1000, 2, False), (1000, 4, False), (1000, 8, False),
+                                              (96, 4, True), (1000, 4, True)])
+def test_mmult_replay_end_to_end(ndim, nodes, graph):
     """NDIM = 1000 is BASELINE config 5's size (test/test_mmult.cpp:103-180 uses
-    NDIM up to 1021 before the reference heap aborts)."""
+    NDIM up to 1021 before the reference heap aborts). graph: every round recorded into one HIP
+    graph (gdsm_capture_*) and replayed by one launch, or issued eagerly (the default)."""
     R = MmultReplay(ndim=ndim, nodes=nodes, seed=7)
     try:
-        R.run()
+        R.run(graph=graph)
         assert np.array_equal(R.home_copy(), R.final_image())
         st, fl = oracle.coh_init(R.Z, nodes)
         acc = np.zeros(10, np.int64)
