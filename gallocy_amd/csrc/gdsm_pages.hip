@@ -687,8 +687,16 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
       }
       const uint64_t stop = (k == 64) ? end_off : lane_bcast64(my_off, k);
       const uint32_t words = (uint32_t)((stop - start) >> 2);
+      // the window is filled by LDS-DMA (global_load_lds_dword: 256 B per wave instruction, all
+      // of them in flight at once), so a wave waits one round trip per window, not one per 256 B
       const uint32_t* src = reinterpret_cast<const uint32_t*>(data + start);
-      for (uint32_t q = lane; q < words; q += 64) win[q] = src[q];
+      for (uint32_t q0 = 0; q0 < words; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        __builtin_amdgcn_global_load_lds(
+            (__attribute__((address_space(1))) void*)(src + (q < words ? q : 0)),
+            (__attribute__((address_space(3))) void*)(win + q0), 4, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed
       wave_lds_sync();
       const uint8_t* win8 = reinterpret_cast<const uint8_t*>(win);
       for (uint32_t jj = j; jj < k; jj += 4) {
