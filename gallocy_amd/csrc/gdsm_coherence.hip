@@ -197,6 +197,10 @@ __global__ __launch_bounds__(256) void coh_tail_kernel(const uint64_t* __restric
     uint64_t h = kNoHead64;  // global index of the last head
     if (hi - lo <= 64) {
       // the whole block is the tail and holds no head
+    } else if (ev_page(ev[lo]) == P) {
+      // the block starts on P too: the batch is sorted, so the whole block is P's (a hot page
+      // spanning blocks); its head, if any, is its first event
+      if (lo == 0 || ev_page(ev[lo - 1]) != P) h = lo;
     } else {
       const uint64_t sidx = lo + (uint64_t)lane * kSamp;
       const bool in = sidx < wlo;
