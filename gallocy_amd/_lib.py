@@ -67,11 +67,14 @@ SIGNATURES = {
     "gdsm_runs_alloc": (C.c_int, [vp, C.c_uint64, C.c_uint64, C.POINTER(GdsmRuns)]),
     "gdsm_runs_free": (C.c_int, [vp, C.POINTER(GdsmRuns)]),
     "gdsm_diff": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns)]),
+    "gdsm_diff_apply": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns), C.c_int]),
     "gdsm_runs_total": (C.c_int, [vp, C.POINTER(GdsmRuns), C.POINTER(C.c_uint64)]),
     "gdsm_apply": (C.c_int, [vp, C.c_int, vp, C.POINTER(GdsmRuns)]),
     "gdsm_apply_async": (C.c_int, [vp, C.c_int, vp, C.POINTER(GdsmRuns)]),
     "gdsm_diff_workspace_bytes": (C.c_uint64, [C.c_uint64]),
     "gdsm_diff_raw": (C.c_int, [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, C.c_uint64, vp]),
+    "gdsm_diff_apply_raw": (C.c_int, [vp, vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp,
+                                      C.c_uint64, vp]),
     "gdsm_apply_raw": (C.c_int, [vp, vp, C.c_uint64, vp, vp, vp, vp]),
     "gdsm_twin_raw": (C.c_int, [vp, vp, vp, C.c_uint64, vp]),
     "gdsm_coh_init": (C.c_int, [vp, C.c_uint32]),

@@ -542,14 +542,20 @@ int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs) {
   return 0;
 }
 
-int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
+static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,
+                     int target) {
   if (!ctx || !out || !out->rec_off || (!out->data && out->cap)) return -EINVAL;
   if (!ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
+  if (target >= 0 && (target > 2 || target == GDSM_TWIN || target == GDSM_CURRENT ||
+                      !ctx->arena[target]))
+    return -EINVAL;
   if (!ids && n > ctx->n_pages) return -EINVAL;
   if (out->n_cap ? n > out->n_cap : (out->owned && n > out->n)) return -EINVAL;
   DeviceGuard g(ctx->device);
-  if (ctx->aux_targets & ((1u << GDSM_TWIN) | (1u << GDSM_CURRENT))) {
-    int rc = join_aux(ctx);  // a pending apply writes an arena this diff reads
+  uint32_t touched = (1u << GDSM_TWIN) | (1u << GDSM_CURRENT);
+  if (target >= 0) touched |= 1u << target;
+  if (ctx->aux_targets & touched) {
+    int rc = join_aux(ctx);  // a pending apply writes an arena this call reads or writes
     if (rc) return rc;
   }
   auto busy = ctx->runs_busy.find(out->rec_off);
@@ -560,8 +566,18 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
-                             ctx->stream, ctx->P()));
+                             ctx->stream, ctx->P(), target >= 0 ? ctx->arena[target] : nullptr));
   return 0;
+}
+
+int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {
+  return diff_impl(ctx, ids, n, out, -1);
+}
+
+int gdsm_diff_apply(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,
+                    int target) {
+  if (target < 0) return -EINVAL;
+  return diff_impl(ctx, ids, n, out, target);
 }
 
 int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total) {
@@ -619,6 +635,16 @@ int gdsm_diff_raw(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, 
   return 0;
 }
 
+int gdsm_diff_apply_raw(const uint8_t* twin, const uint8_t* cur, uint8_t* target,
+                        const uint32_t* ids, uint64_t n, uint64_t* rec_off, uint8_t* data,
+                        uint64_t cap, void* workspace, uint64_t workspace_bytes, void* stream) {
+  if (!twin || !cur || !target || !rec_off || !workspace || (!data && cap)) return -EINVAL;
+  GDSM_TRY(gdsm::launch_diff(twin, cur, ids, n, rec_off, data, cap,
+                             static_cast<uint8_t*>(workspace), workspace_bytes,
+                             static_cast<hipStream_t>(stream), nullptr, target));
+  return 0;
+}
+
 int gdsm_apply_raw(uint8_t* target, const uint32_t* ids, uint64_t n, const uint64_t* rec_off,
                    const uint8_t* data, uint32_t* err, void* stream) {
   if (!target || !rec_off || (!data && n)) return -EINVAL;
@@ -644,6 +670,8 @@ int gdsm_twin_raw(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64
 // ---- coherence -------------------------------------------------------------------------
 int gdsm_coh_init(gdsm_ctx* ctx, uint32_t n_nodes) {
   if (!ctx || n_nodes == 0 || n_nodes > GDSM_MAX_NODES) return -EINVAL;
+  // the fold kernel reads page ids from the events' low dwords (SPEC §5: page < 2^28)
+  if (ctx->n_pages > GDSM_MAX_COH_PAGES) return -EINVAL;
   CtxGuard g(ctx);
   if (g.rc) return g.rc;
   if (!ctx->coh_pt) {

@@ -619,6 +619,434 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
+// ---------------------------------------------------------------- F: single-pass fold
+// One wave = one block of kFBlock events (kFK consecutive events per lane), no other pass before
+// it: the block's carry comes from a decoupled look-back over the other waves' published
+// aggregates (the diff kernel's protocol), so passes A and B and their head snapshots go away.
+//
+// The walk keeps, per lane, a HIT MASK instead of the state word: bit 2n = a read by node n hits
+// (n in the copyset), bit 2n+1 = a write by n hits (EXCLUSIVE, owned by n), kHE = EXCLUSIVE,
+// kHW = a write since the segment's base. The event's low nibble (node << 1 | rw) is its bit
+// index, so "does it fault" is one bit-field extract, a read miss is (H | bit) & kKr and every
+// write sets H = 3 << 2n | kHE | kHW. O = 2 * owner for transfers. The state word of a segment
+// end is rebuilt from (H, O, base) only where a segment ends.
+//
+// Ordering without head snapshots: the only page-table word this wave loads that another wave
+// may store is the one of its last head (that segment can end in a later wave). A wave whose
+// first segment started before it looks back until a predecessor that holds a head (kFHead) or
+// has published its inclusive prefix, and every wave publishes only after its loads landed, so
+// the head's wave has read the word before anyone stores it. Page ids are taken from the low
+// dword (n_pages <= 2^28; any high-dword bit rejects the batch).
+constexpr uint32_t kFK = 16;
+constexpr uint32_t kFBlock = 64 * kFK;
+constexpr uint32_t kHE = 0x10000u, kHW = 0x20000u, kPRE = 0x40000u, kHRead = 0x5555u;
+constexpr uint32_t kKr = kHRead | kHW | kPRE;  // kept by a read miss
+constexpr uint64_t kFAgg = 1ull << 62, kFIncl = 2ull << 62, kFHead = 1ull << 61;
+constexpr uint32_t kFoldCtrs = 8;                   // workgroup ticket counters
+constexpr uint64_t kFoldStatus = kFoldCtrs * 32;    // u64 index of block 0's status granule
+
+__device__ __forceinline__ uint32_t hit_seed(uint32_t w) {
+  uint32_t c = w & 0xFFu;
+  c = (c | (c << 4)) & 0x0F0Fu;
+  c = (c | (c << 2)) & 0x3333u;
+  c = (c | (c << 1)) & 0x5555u;
+  const uint32_t owner = (w >> 8) & 0xFFu;
+  const uint32_t wbit = owner < 8u ? (2u << (2u * owner)) : 0u;
+  return (((w >> 16) & 3u) == 2u) ? (c | kHE | wbit) : c;
+}
+__device__ __forceinline__ uint32_t hit_copyset(uint32_t h) {
+  uint32_t t = h & kHRead;
+  t = (t | (t >> 1)) & 0x3333u;
+  t = (t | (t >> 2)) & 0x0F0Fu;
+  return (t | (t >> 4)) & 0xFFu;
+}
+// The state word at a segment end: the base is the last writer's word when the lane wrote since
+// the segment's base B (a head's word or the lane's incoming state), then the reads since.
+__device__ __forceinline__ uint32_t seg_final(uint32_t h, uint32_t O, uint32_t B) {
+  const uint32_t own = O >> 1;
+  const uint32_t base = (h & kHW) ? ((own << 8) | (1u << own) | 0x60000u) : B;
+  const bool flip = ((base >> 16) & 3u) == 2u && !(h & kHE);
+  return (base | hit_copyset(h)) ^ (flip ? 0x30000u : 0u);
+}
+__device__ __forceinline__ uint32_t wr_word(uint32_t x) {  // CONST word of a write event
+  const uint32_t node = (x >> 1) & 7u;
+  return (node << 8) | (1u << node) | 0x60000u;
+}
+// v_s ∘ v_{s-1} ∘ … ∘ v_0 in lane 63 (higher lanes first): the scan with swapped operands.
+__device__ __forceinline__ uint32_t wave_rev_compose_dpp(uint32_t v) {
+  v = tcompose(v, dpp0<0x111>(v));
+  v = tcompose(v, dpp0<0x112>(v));
+  v = tcompose(v, dpp0<0x114>(v));
+  v = tcompose(v, dpp0<0x118>(v));
+  v = tcompose(v, dpp0<0x142, 0xA>(v));
+  v = tcompose(v, dpp0<0x143, 0xC>(v));
+  return lane_bcast(v, 63);
+}
+
+template <bool kVec, bool kFull, bool kNodes>
+__device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
+                                              const uint64_t* __restrict__ ev, uint64_t n,
+                                              uint64_t b, uint64_t* __restrict__ status,
+                                              uint32_t* __restrict__ partial,
+                                              uint32_t* __restrict__ err, uint32_t n_nodes,
+                                              uint32_t* __restrict__ tr) {
+  const uint32_t lane = lane_id();
+  const uint64_t lo = b * kFBlock;
+  const uint64_t g0 = lo + (uint64_t)lane * kFK;  // global index of this lane's first event
+  const uint32_t nv =
+      kFull ? kFK : (uint32_t)min((uint64_t)kFK, g0 < n ? n - g0 : (uint64_t)0);
+  // ---- events: low dwords (page << 4 | node << 1 | rw); every high-dword bit is an error
+  uint32_t X[kFK], hib = 0;
+  if (kVec && kFull) {
+    // coalesced 16-B loads (load q: events [128q, 128q + 128), two per lane), transposed through
+    // LDS so that each lane holds 16 consecutive events: loading them straight (128-B lane stride)
+    // touched 64 lines per load, 8 loads per line, and re-fetched lines from L2 up to 8 times
+    // (4 dwords of padding per 64 events keep the b64 writes and b128 reads conflict-free)
+#pragma unroll
+    for (uint32_t q = 0; q < kFK / 2; ++q) {
+      const uint4 v = ld_nt16(ev + lo + 128 * q + 2 * lane);
+      hib |= v.y | v.w;
+      const uint32_t e0 = 128 * q + 2 * lane;
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(tr + e0 + 4 * (e0 >> 6)) = (u32x2){v.x, v.z};
+    }
+    wave_lds_sync();
+    const uint32_t base = 16 * lane + 4 * (lane >> 2);
+#pragma unroll
+    for (uint32_t r = 0; r < kFK / 4; ++r) {
+      const uint4 w = *reinterpret_cast<const uint4*>(tr + base + 4 * r);
+      X[4 * r] = w.x;
+      X[4 * r + 1] = w.y;
+      X[4 * r + 2] = w.z;
+      X[4 * r + 3] = w.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kFK; ++k) {
+      const uint64_t e = (k < nv) ? ev[g0 + k] : 0ull;
+      X[k] = (uint32_t)e;
+      hib |= (uint32_t)(e >> 32);
+    }
+  }
+  const uint32_t xprev_w = lo > 0 ? (uint32_t)ev[lo - 1] : 0u;               // uniform
+  const bool has_next = lo + kFBlock < n;
+  const uint32_t xnext_w = has_next ? (uint32_t)ev[lo + kFBlock] : 0u;        // uniform
+  uint32_t xp = from_prev_lane(X[kFK - 1]);
+  if (lane == 0) xp = xprev_w;
+  const bool batch_first = lo == 0 && lane == 0;
+
+  // ---- heads (a new page), the first / last head events, validity
+  uint32_t hm = 0, hc = 0, xf = 0, xl = 0, nodes = 0;
+  uint32_t bad = hib ? 1u : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < kFK; ++k) {
+    if (kFull || k < nv) {
+      const uint32_t x = X[k], pv = k ? X[k ? k - 1 : 0] : xp;
+      const uint32_t pg = x >> 4, pp = pv >> 4;
+      const bool first = k == 0 && batch_first;
+      const bool head = first || pg != pp;
+      if (!first && pg < pp) bad = 1;
+      hm |= (head ? 1u : 0u) << k;
+      if (kNodes) nodes |= 1u << (x & 14u);
+      if (head) {
+        if (hc == 0) xf = x;
+        xl = x;
+        ++hc;
+      }
+    }
+  }
+  if (kNodes && (nodes & ~((1u << (2 * n_nodes)) - 1u) & kHRead)) bad = 1;
+  uint32_t xlast = X[kFK - 1];  // the lane's last valid event
+  if (!kFull) {
+#pragma unroll
+    for (uint32_t k = 0; k < kFK; ++k)
+      if (k + 1 == nv) xlast = X[k];
+  }
+  if (nv && (xlast >> 4) >= n_pages) bad = 1;
+  // does the lane's last event end its segment? (the next lane's first event is a head, or the
+  // next wave's, or the batch ends there)
+  uint32_t nh0 = from_next_lane(hm & 1u);
+  if (lane == 63) nh0 = has_next ? (((xnext_w >> 4) != (X[kFK - 1] >> 4)) ? 1u : 0u) : 1u;
+  bool last_end = nh0 != 0;
+  if (!kFull && nv > 0 && g0 + nv == n) last_end = true;
+
+  // ---- page-table words of the lane's first and last heads (one gathered load each)
+  uint64_t Wl = 0, Wf = 0;
+  {
+    const uint32_t pl = xl >> 4, pf = xf >> 4;
+    if (hc && pl < n_pages) Wl = pt[pl];
+    if (hc > 1 && pf < n_pages) Wf = pt[pf];
+  }
+  // the walk recomputes every per-event value from X: without this the compiler keeps the
+  // prologue's copies (pages, head flags of 16 events) live through the walk
+#pragma unroll
+  for (uint32_t k = 0; k < kFK; ++k) asm volatile("" : "+v"(X[k]));
+  const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
+  const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
+
+  // ---- the walk, from a PROBE state: the lane's incoming state is not known yet (it comes
+  // from the look-back below, which this walk hides). Only the events before the lane's first
+  // CONST (its first write or head) depend on it, and those are reads: the probe starts with an
+  // empty copyset and no write hits (kPRE marks "still in that prefix"), so each prefix read
+  // misses once per node and the first write (if it comes before any head) misses. Hc / Xc keep
+  // the state after the prefix and the first CONST event; both outcomes are corrected once the
+  // incoming state is known. Everything after the first CONST is exact.
+  uint32_t H = kPRE, O = 0x1FEu, B = 0, Bfo = 0, c0 = 0, T = 0, hs = 0;
+  uint32_t inv = 0, xfer = 0, F0 = 0, F1 = 0, Hc = kPRE, Xc = 0;
+  uint32_t sH = 0, sO = 0, sB = 0, sBf = 0, sN = 0, sP = 0;  // pending local segment end
+  uint32_t dH = 0, dO = 0, dT = 0, dP = 0;                   // the lane's first segment end
+  bool local = false, hasS = false, hasD = false;
+// (macros, not lambdas: captured flags end up in scratch memory)
+#define COH_FLUSH_S()                                                                        \
+  do {                                                                                       \
+    if (sP < n_pages) pt[sP] = (uint64_t)seg_final(sH, sO, sB) | ((uint64_t)(sBf + sN) << 32); \
+  } while (0)
+#define COH_END_SEG(p_)    \
+  do {                     \
+    if (!local) {          \
+      dH = H;              \
+      dO = O;              \
+      dT = T;              \
+      dP = (p_);           \
+      hasD = true;         \
+    } else {               \
+      if (hasS) COH_FLUSH_S(); \
+      sH = H;              \
+      sO = O;              \
+      sB = B;              \
+      sBf = Bfo;           \
+      sN = T - c0;         \
+      sP = (p_);           \
+      hasS = true;         \
+    }                      \
+  } while (0)
+#pragma unroll
+  for (uint32_t k = 0; k < kFK; ++k) {
+    if (kFull || k < nv) {
+      const uint32_t x = X[k];
+      {
+        const uint32_t pm = (uint32_t)((int32_t)(H << 13) >> 31);  // still in the prefix
+        Xc = (x & pm) | (Xc & ~pm);
+      }
+      if ((hm >> k) & 1u) {  // a head: the previous segment ends, this one's base is its word
+        if (k > 0) COH_END_SEG(X[k ? k - 1 : 0] >> 4);
+        if (hs + 1 == hc) {
+          H = Hl;
+          O = Ol;
+          B = Bl;
+          Bfo = Bfl;
+        } else {
+          uint64_t w = Wf;
+          if (hs != 0) {
+            const uint32_t p = x >> 4;
+            w = p < n_pages ? pt[p] : 0ull;
+          }
+          B = (uint32_t)w & 0x7FFFFu;
+          Bfo = (uint32_t)(w >> 32);
+          H = hit_seed(B);
+          O = ((B >> 8) & 0xFFu) << 1;
+        }
+        c0 = T;
+        local = true;
+        ++hs;
+      }
+      const uint32_t bi = x & 15u, xn2 = x & 14u;
+      const bool wr = bi != xn2;
+      const uint32_t hitv = __builtin_amdgcn_ubfe(H, bi, 1u);
+      const bool hit = hitv != 0;
+      const uint32_t miss = hitv ^ 1u;
+      const uint32_t m = 1u << xn2;
+      const bool wmiss = wr && !hit;
+      inv += (uint32_t)__popc(wmiss ? (H & kHRead & ~m) : 0u);
+      xfer += (wmiss && O != xn2) ? 1u : 0u;
+      const uint32_t Hr = hit ? H : ((H | m) & kKr);
+      H = wr ? ((3u << xn2) | kHE | kHW) : Hr;
+      O = wr ? xn2 : O;
+      if (k < 8)
+        F0 += miss << (2u * xn2);
+      else
+        F1 += miss << (2u * xn2);
+      T += miss;
+      {
+        const uint32_t qm = (uint32_t)((int32_t)(H << 13) >> 31);
+        Hc = (H & qm) | (Hc & ~qm);
+      }
+      // accumulate now: left alone, the compiler sinks these sums past the walk and keeps every
+      // event's intermediate values live (140+ VGPRs)
+      asm volatile("" : "+v"(inv), "+v"(xfer), "+v"(F0), "+v"(F1), "+v"(Hc), "+v"(Xc));
+    }
+  }
+  if (nv && last_end) COH_END_SEG(xlast >> 4);
+  if (hasS) COH_FLUSH_S();
+#undef COH_END_SEG
+#undef COH_FLUSH_S
+
+  // ---- lane aggregate (exact: the state after the lane's first CONST does not depend on the
+  // incoming state; without a CONST the lane is READ(its reads)), scan, publish, look back
+  const bool has_c = !(H & kPRE);
+  const uint32_t a = has_c ? (kConst | seg_final(H, O, B)) : hit_copyset(H);
+  const uint32_t inc = wave_incl_compose_dpp(a);
+  const uint32_t agg = lane_bcast(inc, 63);
+  const bool whead = __ballot(hc != 0) != 0;
+  // every load of this wave has landed before its status is visible (see above)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0)
+    __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (whead ? kFHead : 0ull) | agg,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t carry = 0;
+  if (b > 0) {
+    int64_t pos = (int64_t)b - 1;
+    for (;;) {
+      const int64_t q = pos - (int64_t)lane;
+      uint64_t st = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : kFIncl;
+      uint32_t s, spins = 0;
+      for (;;) {
+        const uint64_t pub = __ballot((st >> 62) != 0);
+        const uint64_t stop = __ballot((st >> 62) == 2 || (st & kFHead));
+        const uint32_t u = ~pub ? (uint32_t)__builtin_ctzll(~pub) : 64u;
+        s = (stop & pub) ? (uint32_t)__builtin_ctzll(stop & pub) : 64u;
+        if (s < u || u == 64) break;
+        if (++spins > (1u << 24)) {  // never expected: fail the batch rather than hang the GPU
+          bad = 1;
+          s = u;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if ((st >> 62) == 0 && q >= 0)
+          st = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t part;
+      if (s == 0)
+        part = (uint32_t)lane_bcast64(st, 0);
+      else
+        part = wave_rev_compose_dpp(lane <= s ? (uint32_t)st : 0u);
+      carry = tcompose(part, carry);
+      if (s < 64) break;
+      pos -= 64;
+    }
+    if (lane == 0)
+      __hip_atomic_store(status + b, kFIncl | (whead ? kFHead : 0ull) | tcompose(carry, agg),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const uint32_t cur = tcompose(carry, from_prev_lane(inc));
+  const bool cont = nv && !(hm & 1u);  // the lane's first event continues a segment
+  if (cont && !(cur & kConst)) bad = 1;
+
+  // ---- corrections of the probe prefix, now that the incoming state `cur` is known
+  const uint32_t P8 = hit_copyset(Hc);      // nodes read before the first CONST
+  const uint32_t cs = cur & 0xFFu;
+  const uint32_t hitP = cont ? (P8 & cs) : 0u;  // prefix reads that hit after all
+  const uint32_t s1 = tcompose(cur, P8);     // the state after the prefix (CONST)
+  const bool wfirst = cont && has_c && !(hc && Xc == xf);  // the first CONST is a write
+  int32_t dfirst = -(int32_t)__popc(hitP);   // correction of the lane's first segment count
+  uint32_t wcorr = 0;                        // node whose probe write fault did not happen
+  bool wnofault = false;
+  if (wfirst) {
+    const uint32_t w = (Xc >> 1) & 7u, wb = 1u << w;
+    const bool f = !(((s1 >> 16) & 3u) == 2u && ((s1 >> 8) & 0xFFu) == w);
+    inv = inv - (uint32_t)__popc(P8 & ~wb) + (f ? (uint32_t)__popc(s1 & 0xFFu & ~wb) : 0u);
+    xfer = xfer - 1u + ((f && ((s1 >> 8) & 0xFFu) != w) ? 1u : 0u);
+    if (!f) {
+      wnofault = true;
+      wcorr = w;
+      dfirst -= 1;
+    }
+  }
+  // the lane's first segment ends here: its state and count
+  uint32_t Df = 0, Dc = 0;
+  if (hasD) {
+    Df = wfirst ? seg_final(dH, dO, 0u) : (s1 & 0x7FFFFu);
+    Dc = (uint32_t)((int32_t)dT + dfirst);
+  }
+
+  // ---- fault counts of segments that cross lanes (counts only: old counts are 32-bit)
+  const uint32_t own = hc ? T - c0 : (uint32_t)((int32_t)T + dfirst);
+  const uint32_t sin = wave_incl_segsum_dpp((hc ? kConst : 0u) | own);
+  const uint32_t cnt_in = from_prev_lane(sin) & ~kConst;
+  const uint64_t hb = __ballot(hc != 0);
+  const uint64_t below = hb & ((1ull << lane) - 1ull);
+  const uint32_t hl = below ? 63u - (uint32_t)__clzll(below) : 0u;
+  const uint32_t oldf = (uint32_t)__shfl((int)Bfo, (int)hl, 64);
+  uint32_t* pst = reinterpret_cast<uint32_t*>(pt);
+  if (hasD && dP < n_pages) {
+    const uint32_t c = cnt_in + Dc;
+    if (below) {
+      pt[dP] = (uint64_t)Df | ((uint64_t)(oldf + c) << 32);
+    } else {  // the wave's first segment: opened before it
+      pst[2 * (uint64_t)dP] = Df;
+      if (c) atomicAdd(&pst[2 * (uint64_t)dP + 1], c);
+    }
+  }
+  if (kFull && lane == 63 && !last_end) {  // the wave's last segment continues
+    const uint32_t p = X[kFK - 1] >> 4, c = sin & ~kConst;
+    if (c && p < n_pages) atomicAdd(&pst[2 * (uint64_t)p + 1], c);
+  }
+
+  // ---- totals: one partial row per wave (16-bit fields hold a wave's sums)
+  uint32_t Fe = (F0 & 0x0F0F0F0Fu) + (F1 & 0x0F0F0F0Fu);              // nodes 0, 2, 4, 6
+  uint32_t Fo = ((F0 >> 4) & 0x0F0F0F0Fu) + ((F1 >> 4) & 0x0F0F0F0Fu);  // nodes 1, 3, 5, 7
+  {
+    const uint32_t e = hitP & 0x55u, o = (hitP >> 1) & 0x55u;
+    Fe -= (e & 1u) | ((e & 4u) << 6) | ((e & 16u) << 12) | ((e & 64u) << 18);
+    Fo -= (o & 1u) | ((o & 4u) << 6) | ((o & 16u) << 12) | ((o & 64u) << 18);
+    if (wnofault) {
+      const uint32_t one = 1u << (8u * (wcorr >> 1));
+      if (wcorr & 1u)
+        Fo -= one;
+      else
+        Fe -= one;
+    }
+  }
+  const uint32_t v[5] = {inv | (xfer << 16), (Fe & 0xFFu) | ((Fo & 0xFFu) << 16),
+                         ((Fe >> 8) & 0xFFu) | (((Fo >> 8) & 0xFFu) << 16),
+                         ((Fe >> 16) & 0xFFu) | (((Fo >> 16) & 0xFFu) << 16),
+                         (Fe >> 24) | ((Fo >> 24) << 16)};
+  uint32_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint32_t s = wave_sum(v[q]);
+    if (lane == 2u * q) mine = s & 0xFFFFu;
+    if (lane == 2u * q + 1u) mine = s >> 16;
+  }
+  if (lane < 10) partial[b * 10 + lane] = mine;
+  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
+}
+
+// kFull: the batch's whole blocks, one ticket per workgroup (tickets are drawn in dispatch
+// order, so a wave only ever waits for running waves); otherwise the single trailing partial
+// block `nb - 1`, launched after them.
+template <bool kVec, bool kFull, bool kNodes>
+__global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt, uint64_t n_pages,
+                                                       const uint64_t* __restrict__ ev, uint64_t n,
+                                                       uint64_t nb, uint64_t* __restrict__ ws,
+                                                       uint32_t* __restrict__ partial,
+                                                       uint32_t* __restrict__ err,
+                                                       uint32_t n_nodes) {
+  uint64_t b;
+  if (kFull) {
+    // kFoldCtrs ticket counters (one 256-B line each) keyed by blockIdx % kFoldCtrs: one counter
+    // returns only ~88 atomics per us, which serialised 262144 workgroups (config 4) for 3 ms.
+    // Workgroup w = ticket * kFoldCtrs + class is a permutation of blockIdx inside each class, and
+    // every class draws its tickets in dispatch order, so the lowest block nobody has claimed is
+    // always claimed once running blocks finish: no wave waits for a block that cannot run.
+    __shared__ uint32_t ticket;
+    const uint32_t cls = blockIdx.x % kFoldCtrs;
+    if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
+    __syncthreads();
+    const uint64_t w = (uint64_t)__builtin_amdgcn_readfirstlane(ticket) * kFoldCtrs + cls;
+    b = w * 4 + (threadIdx.x >> 6);
+    if (b >= nb) return;
+  } else {
+    if (threadIdx.x >= 64) return;
+    b = nb - 1;
+  }
+  __shared__ __attribute__((aligned(16))) uint32_t tr_all[4][kFBlock + kFBlock / 16];
+  coh_fold_wave<kVec, kFull, kNodes>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err,
+                                     n_nodes, tr_all[threadIdx.x >> 6]);
+}
+
 // ---------------------------------------------------------------- D: totals
 __global__ __launch_bounds__(256) void coh_reduce_kernel(const uint32_t* __restrict__ partial,
                                                          uint64_t nb,
@@ -666,15 +1094,14 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------- launchers
-// Pass C variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = coh_apply_block_kernel, the
-// only product kernel (events that are not 16-B aligned take its scalar-load instance). Built
-// with -DGDSM_MEASURE only: 1 / 2 = without page-table stores / without any page-table traffic
-// (output invalid). (Rounds 1-2 also carried the round-1 block-scan kernel and a hit-mask
-// restatement; both were slower and are in the history.)
+// Coherence variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = the single-pass fold
+// (coh_fold_kernel, default); 1 = the round-2 four-pass path (tail aggregates, scan, block pass
+// C), kept for same-box A/B. Built with -DGDSM_MEASURE only: 2 / 3 = the four-pass path without
+// page-table stores / without any page-table traffic (output invalid).
 #ifdef GDSM_MEASURE
-constexpr int kCohVariants = 3;
+constexpr int kCohVariants = 4;
 #else
-constexpr int kCohVariants = 1;
+constexpr int kCohVariants = 2;
 #endif
 static int coh_variant_from_env() {
   const char* e = getenv("GDSM_COH_VARIANT");
@@ -692,12 +1119,17 @@ int coh_tune(const char* key, int64_t value) {
 
 static inline uint64_t coh_blocks(uint64_t n) { return (n + kCohBlock - 1) / kCohBlock; }
 static inline uint64_t coh_groups(uint64_t nb) { return (nb + kCohGroup - 1) / kCohGroup; }
+static inline uint64_t fold_blocks(uint64_t n) { return (n + kFBlock - 1) / kFBlock; }
 
 uint64_t coh_workspace_bytes(uint64_t n_events) {
   const uint64_t nb = coh_blocks(n_events);
-  // head_pt (u64) + agg, last_head, carry (u32 each) + partial rows (10 u32, one per wave of
-  // pass C: 4 per block) + groups
-  return nb * (8 + 4 * 3 + 4 * 40) + coh_groups(nb) * 4 + 512;
+  // four-pass: head_pt (u64) + agg, last_head, carry (u32 each) + partial rows (10 u32, one per
+  // wave of pass C: 4 per block) + groups
+  const uint64_t four = nb * (8 + 4 * 3 + 4 * 40) + coh_groups(nb) * 4 + 512;
+  // fold: ticket counters + one status granule per block, one partial row per block
+  const uint64_t nf = fold_blocks(n_events);
+  const uint64_t fold = 8 * (kFoldStatus + nf) + 40 * nf + 512;
+  return four > fold ? four : fold;
 }
 
 hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hipStream_t s) {
@@ -717,6 +1149,36 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   if (r != hipSuccess || n_events == 0) return r;
   const uint64_t nb = coh_blocks(n_events), ng = coh_groups(nb);
   if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
+  if (g_coh_variant == 0) {
+    const uint64_t nf = fold_blocks(n_events);
+    uint64_t* fws = reinterpret_cast<uint64_t*>(ws);
+    uint32_t* fpart = reinterpret_cast<uint32_t*>(fws + kFoldStatus + nf);
+    r = hipMemsetAsync(fws, 0, 8 * (kFoldStatus + nf), s);  // tickets + status granules
+    if (r != hipSuccess) return r;
+    {
+      ProfScope ps(prof, 7, s);
+      const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
+      const bool nodes = n_nodes < 8;
+      const uint64_t full = n_events / kFBlock;
+      if (full) {
+        auto kern = vec ? (nodes ? coh_fold_kernel<true, true, true> : coh_fold_kernel<true, true, false>)
+                        : (nodes ? coh_fold_kernel<false, true, true> : coh_fold_kernel<false, true, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
+                           events, n_events, full, fws, fpart, err, n_nodes);
+      }
+      if (nf > full) {
+        auto kern = nodes ? coh_fold_kernel<false, false, true> : coh_fold_kernel<false, false, false>;
+        hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, s, pt, n_pages, events, n_events, nf, fws,
+                           fpart, err, n_nodes);
+      }
+    }
+    uint64_t g = (nf + 255) / 256;
+    if (g > 1024) g = 1024;
+    ProfScope ps(prof, 8, s);
+    hipLaunchKernelGGL(coh_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, fpart, nf,
+                       reinterpret_cast<unsigned long long*>(totals));
+    return hipGetLastError();
+  }
   uint64_t* head_pt = reinterpret_cast<uint64_t*>(ws);
   uint32_t* agg = reinterpret_cast<uint32_t*>(head_pt + nb);
   uint32_t* lh = agg + nb;
@@ -740,8 +1202,8 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
     const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
 #ifdef GDSM_MEASURE
     auto kern = !vec                 ? coh_apply_block_kernel<0, false>
-                : g_coh_variant == 1 ? coh_apply_block_kernel<1, true>
-                : g_coh_variant == 2 ? coh_apply_block_kernel<2, true>
+                : g_coh_variant == 2 ? coh_apply_block_kernel<1, true>
+                : g_coh_variant == 3 ? coh_apply_block_kernel<2, true>
                                      : coh_apply_block_kernel<0, true>;
 #else
     auto kern = vec ? coh_apply_block_kernel<0, true> : coh_apply_block_kernel<0, false>;

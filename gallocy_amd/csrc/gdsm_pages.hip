@@ -308,6 +308,37 @@ __device__ __forceinline__ uint32_t record_size_masks(const uint32_t (&m)[4], ui
   return NR ? 4u + 4u * NR + ((NP + 3u) & ~3u) : 0u;
 }
 
+// The bytes of a 16-B chunk selected by `m` (bit j = byte j), stored from registers: one 16-B
+// store for a whole chunk, 8-B stores for whole halves, dword stores for whole dwords, else bytes.
+__device__ __forceinline__ void store_masked16(uint8_t* __restrict__ dst, uint32_t m,
+                                               const uint4& c) {
+  if (m == 0xFFFFu) {
+    *reinterpret_cast<uint4*>(dst) = c;
+    return;
+  }
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t lo = h ? c.z : c.x, hi = h ? c.w : c.y;
+    if (((m >> (8 * h)) & 0xFFu) == 0xFFu) {
+      *reinterpret_cast<u32x2*>(dst + 8 * h) = (u32x2){lo, hi};
+      continue;
+    }
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const uint32_t wv = d ? hi : lo, nib = (m >> (8 * h + 4 * d)) & 0xFu;
+      uint8_t* q = dst + 8 * h + 4 * d;
+      if (nib == 0xFu) {
+        *reinterpret_cast<uint32_t*>(q) = wv;
+      } else if (nib) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((nib >> k) & 1u) q[k] = (uint8_t)(wv >> (8 * k));
+      }
+    }
+  }
+}
+
 // ---- single-pass diff (default): every record is written straight to its final place in the
 // packed stream, so the stream crosses HBM once (no workspace slots, no scan, no pack).
 // A WAVE is the unit of work: it draws a ticket (atomic counter; tickets are drawn in dispatch
@@ -331,11 +362,15 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
-template <uint32_t kU, uint32_t kBuf, int kWaves>
+// kApply: the same runs are also applied to `target` (a home copy on this GPU, pages indexed by
+// the same ids): each dirty chunk's changed bytes, exactly the bytes its runs cover (SPEC §4),
+// are stored from the registers that found them, so the stream is not read back.
+template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, uint64_t n, uint64_t* __restrict__ rec_off,
-    uint8_t* __restrict__ data, uint64_t cap, uint64_t* __restrict__ ws) {
+    uint8_t* __restrict__ data, uint64_t cap, uint64_t* __restrict__ ws,
+    uint8_t* __restrict__ target) {
   static_assert(kU <= 32 && (kU & (kU - 1)) == 0, "unit size");
   __shared__ uint32_t sel_tab[16];
   __shared__ uint32_t ent_all[4][64];
@@ -366,7 +401,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   uint32_t my_size = 0;   // lane j: record size of page j
   uint32_t my_src = 0;    // lane j: LDS byte offset of page j's record
   uint4 t[4], c[4];
-  load_page(twin, cur, ids ? ids[i0] : i0, lane, t, c);
+  uint64_t pj = ids ? ids[i0] : i0;
+  load_page(twin, cur, pj, lane, t, c);
   for (uint32_t j = 0; j < cnt; ++j) {
     uint32_t m[4], D = 0;
 #pragma unroll
@@ -380,8 +416,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
         dat[rank] = c[k];
       }
       D += (uint32_t)__popcll(B);
+      if (kApply && m[k]) store_masked16(target + pj * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
     }
-    if (j + 1 < cnt) load_page(twin, cur, ids ? ids[i0 + j + 1] : i0 + j + 1, lane, t, c);
+    if (j + 1 < cnt) {
+      pj = ids ? ids[i0 + j + 1] : i0 + j + 1;
+      load_page(twin, cur, pj, lane, t, c);
+    }
     uint32_t size = 0;
     const uint32_t src = acc;
     if (D > 64u) {
@@ -803,7 +843,7 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
 
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
-                       uint64_t ws_bytes, hipStream_t s, Prof* prof) {
+                       uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   int v = diff_variant();
   if (v == 0) v = n <= kDiffShort ? 3 : (cap <= 384 * n) ? 2 : 1;
@@ -814,11 +854,14 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
   if (e != hipSuccess) return e;
   ProfScope ps(prof, 0, s);
-  auto kern = v == 3   ? diff_single_kernel<2, 8192, 4>
-              : v == 2 ? diff_single_kernel<32, 8192, 4>
-                       : diff_single_kernel<16, 8192, 4>;
+  auto kern = target ? (v == 3   ? diff_single_kernel<2, 8192, 4, true>
+                       : v == 2 ? diff_single_kernel<32, 8192, 4, true>
+                                : diff_single_kernel<16, 8192, 4, true>)
+                     : (v == 3   ? diff_single_kernel<2, 8192, 4, false>
+                       : v == 2 ? diff_single_kernel<32, 8192, 4, false>
+                                : diff_single_kernel<16, 8192, 4, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, n,
-                     rec_off, data, cap, reinterpret_cast<uint64_t*>(ws));
+                     rec_off, data, cap, reinterpret_cast<uint64_t*>(ws), target);
   return hipGetLastError();
 }
 

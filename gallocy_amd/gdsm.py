@@ -271,10 +271,17 @@ class Context:
         n = self._count(ids, n)
         check(lib().gdsm_twin(self.handle, self._ptr(ids), n), "gdsm_twin")
 
-    def diff(self, ids=None, n: Optional[int] = None, out: Optional[Runs] = None, cap: int = 0) -> Runs:
+    def diff(self, ids=None, n: Optional[int] = None, out: Optional[Runs] = None, cap: int = 0,
+             apply_to: Optional[str] = None) -> Runs:
+        """TWIN vs CURRENT -> Runs; with apply_to (normally "replica"), the same kernel also
+        applies the runs to that arena (gdsm_diff_apply: a home copy on this GPU)."""
         n = self._count(ids, n)
         out = out or Runs(self, n, cap)
-        check(lib().gdsm_diff(self.handle, self._ptr(ids), n, C.byref(out.s)), "gdsm_diff")
+        if apply_to is None:
+            check(lib().gdsm_diff(self.handle, self._ptr(ids), n, C.byref(out.s)), "gdsm_diff")
+        else:
+            check(lib().gdsm_diff_apply(self.handle, self._ptr(ids), n, C.byref(out.s),
+                                        _ARENA[apply_to]), "gdsm_diff_apply")
         return out
 
     def apply(self, runs: Runs, target="replica", ids=None):

@@ -41,6 +41,9 @@ extern "C" {
 #define GDSM_PAGE_SZ 4096u
 #define GDSM_MAX_RUNS 2048u
 #define GDSM_MAX_NODES 8u
+/* Largest page table gdsm_coh_init accepts: page ids of coherence events fit 28 bits (1 TiB of
+ * 4 KiB pages, beyond any one GPU's HBM). */
+#define GDSM_MAX_COH_PAGES (1ull << 28)
 /* Largest record: 4 + 4*2048 + 2048 (alternating bytes), SPEC §3. */
 #define GDSM_MAX_RECORD 10244u
 
@@ -153,6 +156,14 @@ int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs);
 /* Diffs TWIN against CURRENT for the listed pages into `out` (n <= out->n_cap; out->n is set
  * to n). Asynchronous; use gdsm_runs_total to learn the size. */
 int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out);
+/* gdsm_diff, and the same runs applied to arena `target` (GDSM_REPLICA: a home copy on this
+ * GPU, indexed by the same ids) by the same kernel: each dirty 16-B chunk's changed bytes, which
+ * are exactly the bytes its runs cover (SPEC §4), are stored from the registers that found them,
+ * so the stream is not read back. Equivalent to gdsm_diff + gdsm_apply(ctx, target, ids, out),
+ * except that every page is applied even when the stream overflows out->cap (-ENOSPC from
+ * gdsm_runs_total). Replaces the local-home half of gallocy's described release
+ * (resources/NUTSHELL.md:59-69): the home applies what the writer diffed. */
+int gdsm_diff_apply(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out, int target);
 /* Synchronises, returns rec_off[n] in *total; -ENOSPC if it exceeded runs->cap. */
 int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total);
 /* Applies `in` to arena `target` (normally GDSM_REPLICA) for the listed pages (ids unique). */
@@ -168,6 +179,9 @@ uint64_t gdsm_diff_workspace_bytes(uint64_t n);
 int gdsm_diff_raw(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                   uint64_t* rec_off, uint8_t* data, uint64_t cap, void* workspace,
                   uint64_t workspace_bytes, void* stream);
+int gdsm_diff_apply_raw(const uint8_t* twin, const uint8_t* cur, uint8_t* target,
+                        const uint32_t* ids, uint64_t n, uint64_t* rec_off, uint8_t* data,
+                        uint64_t cap, void* workspace, uint64_t workspace_bytes, void* stream);
 /* err: caller-owned device word, OR-ed with 1 on a malformed record (NULL: not reported). */
 int gdsm_apply_raw(uint8_t* target, const uint32_t* ids, uint64_t n, const uint64_t* rec_off,
                    const uint8_t* data, uint32_t* err, void* stream);
@@ -175,7 +189,8 @@ int gdsm_twin_raw(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64
                   void* stream);
 
 /* ---- batched coherence (SPEC §5) ------------------------------------------------------- */
-/* Allocates and initialises the page table (state + faults) for n_nodes <= 8. */
+/* Allocates and initialises the page table (state + faults) for n_nodes <= 8; -EINVAL for a
+ * context of more than GDSM_MAX_COH_PAGES pages. */
 int gdsm_coh_init(gdsm_ctx* ctx, uint32_t n_nodes);
 /* Applies one batch of page-sorted events (device array). Synchronises and writes
  * totals[10] = {invalidations, transfers, node_faults[8]}; -EINVAL if the batch is not sorted
