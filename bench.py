@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="double-buffered steps (exchange/apply k overlaps diff k+1); auto = on "
                          "for N > 1 (hides the RCCL exchange), off on one GPU (HBM-bound)")
+    ap.add_argument("--fuse", choices=["on", "off"], default="on",
+                    help="N = 1: on = gdsm_diff_apply (the diff kernel applies each page's runs "
+                         "to its home copy from the registers that found them); off = gdsm_diff "
+                         "then gdsm_apply of the stream")
     ap.add_argument("--compare-overlap", action="store_true",
                     help="also time the other overlap mode (reported beside the measured one)")
     ap.add_argument("--workload", choices=["pages", "coherence", "mmult", "nw"], default="pages",
@@ -134,10 +138,12 @@ def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
 DIFF_KERNEL = "gdsm::diff_single_kernel"
 
 
-def read_traffic(pages: int, mode: str, ppm: int):
-    """Per-launch HBM bytes of the diff kernel from the newest committed PMC summary that
-    measured that kernel on this workload (profiles/*traffic*.json, scripts/gpu_prof.sh), else
-    None. Summaries without a workload tag are for the default config-2 workload."""
+def read_traffic(pages: int, mode: str, ppm: int, fused: bool):
+    """Per-launch HBM bytes of the diff kernel (the instance with the apply fused in, or not)
+    from the newest committed PMC summary that measured it on this workload
+    (profiles/*traffic*.json, scripts/gpu_prof.sh), else None. Summaries without a workload tag
+    are for the default config-2 workload."""
+    suffix = ", true>" if fused else ", false>"
     default = {"pages": 1 << 20, "mode": "uniform", "ppm": 10000}
     for p in sorted((ROOT / "profiles").glob("*traffic*.json"), reverse=True):
         try:
@@ -145,6 +151,7 @@ def read_traffic(pages: int, mode: str, ppm: int):
         except Exception:  # noqa: BLE001
             continue
         if (str(j.get("diff_kernel", "")).startswith(DIFF_KERNEL)
+                and str(j.get("diff_kernel", "")).endswith(suffix)
                 and j.get("workload", default) == {"pages": pages, "mode": mode, "ppm": ppm}):
             return j.get("diff_kernel_bytes_per_launch"), p.name
     return None, None
@@ -483,6 +490,9 @@ def main():
             return
         for i in range(k):
             r = runs[i % 2] if pipelined else runs[0]
+            if fused:
+                ctx.diff(out=r, apply_to="replica")
+                continue
             ctx.diff(out=r)
             (ctx.apply_async if pipelined else ctx.apply)(r)
 
@@ -492,6 +502,7 @@ def main():
         ctx.sync()
 
     pipelined = args.overlap == "on" or (args.overlap == "auto" and world > 1)
+    fused = shard is None and args.fuse == "on" and not pipelined
     if shard is not None:
         # release 0 with exact sizes (one host read), then fixed byte budgets: no host sync
         shard.run(1, pipelined=False)
@@ -567,12 +578,15 @@ def main():
     diff_ms, diff_launches = prof["diff"]
     avg_diff_ms = diff_ms / max(1, diff_launches)
     per_step = max(1, diff_launches // args.steps)
-    diff_bytes = (n * 8192 + total) / per_step  # algorithmic per launch: twin + current, records
+    # algorithmic per launch: twin + current read, records written (+ the payload bytes stored
+    # to the home copy when the apply is fused into the diff)
+    diff_bytes = (n * 8192 + total + (pay if fused else 0)) / per_step
     achieved = diff_bytes / (avg_diff_ms * 1e-3) / 1e9
-    step_bytes = n * 8192 + 2 * total + pay  # B_page summed
+    # B_page summed; the fused step does not read the stream back
+    step_bytes = n * 8192 + (1 if fused else 2) * total + pay
     ms_step = dt / args.steps * 1e3
     value = world * n * args.steps / dt
-    traffic, traffic_src = read_traffic(n, mode_name, ppm)
+    traffic, traffic_src = read_traffic(n, mode_name, ppm, fused)
 
     if rank == 0:
         stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
@@ -605,6 +619,7 @@ def main():
                           if world > 1 and backend == "gloo" else {})},
             "step_hbm_gbs": round(step_bytes * args.steps / dt / 1e9, 1),
             "pipelined": pipelined,
+            "fused_apply": fused,
             ("serial_ms_per_step" if pipelined else "pipelined_ms_per_step"):
                 None if dt_other is None else round(dt_other / args.steps * 1e3, 4),
             "roofline": {"bound": "hbm", "kernel": DIFF_KERNEL,

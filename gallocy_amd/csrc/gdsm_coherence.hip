@@ -637,7 +637,8 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
 // has published its inclusive prefix, and every wave publishes only after its loads landed, so
 // the head's wave has read the word before anyone stores it. Page ids are taken from the low
 // dword (n_pages <= 2^28; any high-dword bit rejects the batch).
-constexpr uint32_t kFK = 16;
+constexpr uint32_t kFK = 32;                // events per lane
+constexpr uint32_t kFH = 16;                // of them held in registers at a time
 constexpr uint32_t kFBlock = 64 * kFK;
 constexpr uint32_t kHE = 0x10000u, kHW = 0x20000u, kPRE = 0x40000u, kHRead = 0x5555u;
 constexpr uint32_t kKr = kHRead | kHW | kPRE;  // kept by a read miss
@@ -683,6 +684,29 @@ __device__ __forceinline__ uint32_t wave_rev_compose_dpp(uint32_t v) {
   return lane_bcast(v, 63);
 }
 
+// LDS slot of block event e (lo dword): an XOR swizzle of the 4-dword group (bits 2-5) by bits
+// 6-9, so the coalesced b64 writes and the per-lane b128 reads of 4 consecutive events both spread
+// over all 64 banks, without padding (8 KiB per wave keeps 5 workgroups per CU).
+__device__ __forceinline__ uint32_t fold_slot(uint32_t e) { return e ^ (((e >> 6) & 15u) << 2); }
+
+// 16 of the lane's events, [16h, 16h + 16), from the wave's LDS copy of its block.
+__device__ __forceinline__ void fold_half(const uint32_t* __restrict__ tr, uint32_t lane,
+                                          uint32_t h, uint32_t (&X)[kFH]) {
+  asm volatile("" ::: "memory");  // not hoisted above the previous half's work
+#pragma unroll
+  for (uint32_t r = 0; r < kFH / 4; ++r) {
+    const uint4 w = *reinterpret_cast<const uint4*>(tr + fold_slot(kFK * lane + kFH * h + 4 * r));
+    X[4 * r] = w.x;
+    X[4 * r + 1] = w.y;
+    X[4 * r + 2] = w.z;
+    X[4 * r + 3] = w.w;
+  }
+  // the walk recomputes every per-event value from X: without this the compiler keeps the
+  // prologue's copies (pages, head flags) live through the walk
+#pragma unroll
+  for (uint32_t k = 0; k < kFH; ++k) asm volatile("" : "+v"(X[k]));
+}
+
 template <bool kVec, bool kFull, bool kNodes>
 __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                               const uint64_t* __restrict__ ev, uint64_t n,
@@ -695,78 +719,72 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   const uint64_t g0 = lo + (uint64_t)lane * kFK;  // global index of this lane's first event
   const uint32_t nv =
       kFull ? kFK : (uint32_t)min((uint64_t)kFK, g0 < n ? n - g0 : (uint64_t)0);
-  // ---- events: low dwords (page << 4 | node << 1 | rw); every high-dword bit is an error
-  uint32_t X[kFK], hib = 0;
+  // ---- events: low dwords (page << 4 | node << 1 | rw) into the wave's LDS copy of the block;
+  // every high-dword bit is an error. Coalesced 16-B loads (load q: events [128q, 128q + 128),
+  // two per lane); each lane then reads its 32 consecutive events 16 at a time. (Loading a
+  // lane's events straight, at a 256-B lane stride, touched 64 lines per load instruction and
+  // re-fetched every line from L2 once per instruction.)
+  uint32_t hib = 0;
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   if (kVec && kFull) {
-    // coalesced 16-B loads (load q: events [128q, 128q + 128), two per lane), transposed through
-    // LDS so that each lane holds 16 consecutive events: loading them straight (128-B lane stride)
-    // touched 64 lines per load, 8 loads per line, and re-fetched lines from L2 up to 8 times
-    // (4 dwords of padding per 64 events keep the b64 writes and b128 reads conflict-free)
 #pragma unroll
-    for (uint32_t q = 0; q < kFK / 2; ++q) {
+    for (uint32_t q = 0; q < kFBlock / 128; ++q) {
       const uint4 v = ld_nt16(ev + lo + 128 * q + 2 * lane);
       hib |= v.y | v.w;
-      const uint32_t e0 = 128 * q + 2 * lane;
-      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-      *reinterpret_cast<u32x2*>(tr + e0 + 4 * (e0 >> 6)) = (u32x2){v.x, v.z};
-    }
-    wave_lds_sync();
-    const uint32_t base = 16 * lane + 4 * (lane >> 2);
-#pragma unroll
-    for (uint32_t r = 0; r < kFK / 4; ++r) {
-      const uint4 w = *reinterpret_cast<const uint4*>(tr + base + 4 * r);
-      X[4 * r] = w.x;
-      X[4 * r + 1] = w.y;
-      X[4 * r + 2] = w.z;
-      X[4 * r + 3] = w.w;
+      *reinterpret_cast<u32x2*>(tr + fold_slot(128 * q + 2 * lane)) = (u32x2){v.x, v.z};
     }
   } else {
-#pragma unroll
     for (uint32_t k = 0; k < kFK; ++k) {
       const uint64_t e = (k < nv) ? ev[g0 + k] : 0ull;
-      X[k] = (uint32_t)e;
+      tr[fold_slot(kFK * lane + k)] = (uint32_t)e;
       hib |= (uint32_t)(e >> 32);
     }
   }
+  wave_lds_sync();
   const uint32_t xprev_w = lo > 0 ? (uint32_t)ev[lo - 1] : 0u;               // uniform
   const bool has_next = lo + kFBlock < n;
   const uint32_t xnext_w = has_next ? (uint32_t)ev[lo + kFBlock] : 0u;        // uniform
-  uint32_t xp = from_prev_lane(X[kFK - 1]);
+  const uint32_t xlast = nv ? tr[fold_slot(kFK * lane + nv - 1)] : 0u;       // last valid event
+  uint32_t xp = from_prev_lane(tr[fold_slot(kFK * lane + kFK - 1)]);
   if (lane == 0) xp = xprev_w;
   const bool batch_first = lo == 0 && lane == 0;
 
   // ---- heads (a new page), the first / last head events, validity
+  uint32_t X[kFH];
   uint32_t hm = 0, hc = 0, xf = 0, xl = 0, nodes = 0;
   uint32_t bad = hib ? 1u : 0u;
 #pragma unroll
-  for (uint32_t k = 0; k < kFK; ++k) {
-    if (kFull || k < nv) {
-      const uint32_t x = X[k], pv = k ? X[k ? k - 1 : 0] : xp;
-      const uint32_t pg = x >> 4, pp = pv >> 4;
-      const bool first = k == 0 && batch_first;
-      const bool head = first || pg != pp;
-      if (!first && pg < pp) bad = 1;
-      hm |= (head ? 1u : 0u) << k;
-      if (kNodes) nodes |= 1u << (x & 14u);
-      if (head) {
-        if (hc == 0) xf = x;
-        xl = x;
-        ++hc;
+  for (uint32_t h = 0; h < kFK / kFH; ++h) {
+    fold_half(tr, lane, h, X);
+#pragma unroll
+    for (uint32_t j = 0; j < kFH; ++j) {
+      const uint32_t k = kFH * h + j;
+      if (kFull || k < nv) {
+        const uint32_t x = X[j], pv = j ? X[j ? j - 1 : 0] : xp;
+        const uint32_t pg = x >> 4, pp = pv >> 4;
+        const bool first = k == 0 && batch_first;
+        const bool head = first || pg != pp;
+        if (!first && pg < pp) bad = 1;
+        hm |= (head ? 1u : 0u) << k;
+        if (kNodes) nodes |= 1u << (x & 14u);
+        if (head) {
+          if (hc == 0) xf = x;
+          xl = x;
+          ++hc;
+        }
       }
     }
+    xp = X[kFH - 1];
   }
+  // opaque from here on: the walk re-derives its per-event head flags from these words instead
+  // of the compiler keeping the prologue's 32 masks and running head counts live
+  asm volatile("" : "+v"(hm), "+v"(hc), "+v"(xf), "+v"(xl));
   if (kNodes && (nodes & ~((1u << (2 * n_nodes)) - 1u) & kHRead)) bad = 1;
-  uint32_t xlast = X[kFK - 1];  // the lane's last valid event
-  if (!kFull) {
-#pragma unroll
-    for (uint32_t k = 0; k < kFK; ++k)
-      if (k + 1 == nv) xlast = X[k];
-  }
   if (nv && (xlast >> 4) >= n_pages) bad = 1;
   // does the lane's last event end its segment? (the next lane's first event is a head, or the
   // next wave's, or the batch ends there)
   uint32_t nh0 = from_next_lane(hm & 1u);
-  if (lane == 63) nh0 = has_next ? (((xnext_w >> 4) != (X[kFK - 1] >> 4)) ? 1u : 0u) : 1u;
+  if (lane == 63) nh0 = has_next ? (((xnext_w >> 4) != (xlast >> 4)) ? 1u : 0u) : 1u;
   bool last_end = nh0 != 0;
   if (!kFull && nv > 0 && g0 + nv == n) last_end = true;
 
@@ -777,10 +795,6 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     if (hc && pl < n_pages) Wl = pt[pl];
     if (hc > 1 && pf < n_pages) Wf = pt[pf];
   }
-  // the walk recomputes every per-event value from X: without this the compiler keeps the
-  // prologue's copies (pages, head flags of 16 events) live through the walk
-#pragma unroll
-  for (uint32_t k = 0; k < kFK; ++k) asm volatile("" : "+v"(X[k]));
   const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
   const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
 
@@ -792,89 +806,91 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   // the state after the prefix and the first CONST event; both outcomes are corrected once the
   // incoming state is known. Everything after the first CONST is exact.
   uint32_t H = kPRE, O = 0x1FEu, B = 0, Bfo = 0, c0 = 0, T = 0, hs = 0;
-  uint32_t inv = 0, xfer = 0, F0 = 0, F1 = 0, Hc = kPRE, Xc = 0;
+  uint32_t inv = 0, xfer = 0, F[4] = {0, 0, 0, 0}, Hc = kPRE, Xc = 0, pm = ~0u;
   uint32_t sH = 0, sO = 0, sB = 0, sBf = 0, sN = 0, sP = 0;  // pending local segment end
   uint32_t dH = 0, dO = 0, dT = 0, dP = 0;                   // the lane's first segment end
   bool local = false, hasS = false, hasD = false;
+  uint32_t kEW = kHE | kHW;  // kept in a register (the write state's constant part)
+  asm volatile("" : "+v"(kEW));
 // (macros, not lambdas: captured flags end up in scratch memory)
 #define COH_FLUSH_S()                                                                        \
   do {                                                                                       \
     if (sP < n_pages) pt[sP] = (uint64_t)seg_final(sH, sO, sB) | ((uint64_t)(sBf + sN) << 32); \
   } while (0)
-#define COH_END_SEG(p_)    \
-  do {                     \
-    if (!local) {          \
-      dH = H;              \
-      dO = O;              \
-      dT = T;              \
-      dP = (p_);           \
-      hasD = true;         \
-    } else {               \
+#define COH_END_SEG(p_)        \
+  do {                         \
+    if (!local) {              \
+      dH = H;                  \
+      dO = O;                  \
+      dT = T;                  \
+      dP = (p_);               \
+      hasD = true;             \
+    } else {                   \
       if (hasS) COH_FLUSH_S(); \
-      sH = H;              \
-      sO = O;              \
-      sB = B;              \
-      sBf = Bfo;           \
-      sN = T - c0;         \
-      sP = (p_);           \
-      hasS = true;         \
-    }                      \
+      sH = H;                  \
+      sO = O;                  \
+      sB = B;                  \
+      sBf = Bfo;               \
+      sN = T - c0;             \
+      sP = (p_);               \
+      hasS = true;             \
+    }                          \
   } while (0)
+  uint32_t xprevh = 0;  // the event before X[0] in this lane (half 1)
 #pragma unroll
-  for (uint32_t k = 0; k < kFK; ++k) {
-    if (kFull || k < nv) {
-      const uint32_t x = X[k];
-      {
-        const uint32_t pm = (uint32_t)((int32_t)(H << 13) >> 31);  // still in the prefix
-        Xc = (x & pm) | (Xc & ~pm);
-      }
-      if ((hm >> k) & 1u) {  // a head: the previous segment ends, this one's base is its word
-        if (k > 0) COH_END_SEG(X[k ? k - 1 : 0] >> 4);
-        if (hs + 1 == hc) {
-          H = Hl;
-          O = Ol;
-          B = Bl;
-          Bfo = Bfl;
-        } else {
-          uint64_t w = Wf;
-          if (hs != 0) {
-            const uint32_t p = x >> 4;
-            w = p < n_pages ? pt[p] : 0ull;
+  for (uint32_t h = 0; h < kFK / kFH; ++h) {
+    fold_half(tr, lane, h, X);
+#pragma unroll
+    for (uint32_t j = 0; j < kFH; ++j) {
+      const uint32_t k = kFH * h + j;
+      if (kFull || k < nv) {
+        const uint32_t x = X[j];
+        Xc = (x & pm) | (Xc & ~pm);  // v_bfi: the event, while still in the prefix
+        if ((hm >> k) & 1u) {  // a head: the previous segment ends, this one's base is its word
+          if (k > 0) COH_END_SEG((j ? X[j ? j - 1 : 0] : xprevh) >> 4);
+          if (hs + 1 == hc) {
+            H = Hl;
+            O = Ol;
+            B = Bl;
+            Bfo = Bfl;
+          } else {
+            uint64_t w = Wf;
+            if (hs != 0) {
+              const uint32_t p = x >> 4;
+              w = p < n_pages ? pt[p] : 0ull;
+            }
+            B = (uint32_t)w & 0x7FFFFu;
+            Bfo = (uint32_t)(w >> 32);
+            H = hit_seed(B);
+            O = ((B >> 8) & 0xFFu) << 1;
           }
-          B = (uint32_t)w & 0x7FFFFu;
-          Bfo = (uint32_t)(w >> 32);
-          H = hit_seed(B);
-          O = ((B >> 8) & 0xFFu) << 1;
+          c0 = T;
+          local = true;
+          ++hs;
         }
-        c0 = T;
-        local = true;
-        ++hs;
+        const uint32_t bi = x & 15u, xn2 = x & 14u;
+        const bool wr = bi != xn2;
+        const uint32_t hitv = __builtin_amdgcn_ubfe(H, bi, 1u);
+        const bool hit = hitv != 0;
+        const uint32_t miss = hitv ^ 1u;
+        const uint32_t m = 1u << xn2;
+        const uint32_t sel = (wr && !hit) ? (H & kHRead & ~m) : 0u;
+        asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(inv) : "v"(sel), "v"(inv));
+        xfer += (wr && O != xn2) ? 1u : 0u;  // a write by a non-owner always faults
+        const uint32_t Hr = hit ? H : ((H | m) & kKr);
+        H = wr ? ((3u << xn2) | kEW) : Hr;
+        O = wr ? xn2 : O;
+        F[k / 8] += miss << (2u * xn2);
+        T += miss;
+        pm = (uint32_t)((int32_t)(H << 13) >> 31);  // still in the prefix after this event
+        asm volatile("" : "+v"(pm));
+        Hc = (H & pm) | (Hc & ~pm);
+        // accumulate now: left alone, the compiler sinks these sums past the walk and keeps
+        // every event's intermediate values live
+        asm volatile("" : "+v"(inv), "+v"(xfer), "+v"(F[k / 8]), "+v"(Hc), "+v"(Xc));
       }
-      const uint32_t bi = x & 15u, xn2 = x & 14u;
-      const bool wr = bi != xn2;
-      const uint32_t hitv = __builtin_amdgcn_ubfe(H, bi, 1u);
-      const bool hit = hitv != 0;
-      const uint32_t miss = hitv ^ 1u;
-      const uint32_t m = 1u << xn2;
-      const bool wmiss = wr && !hit;
-      inv += (uint32_t)__popc(wmiss ? (H & kHRead & ~m) : 0u);
-      xfer += (wmiss && O != xn2) ? 1u : 0u;
-      const uint32_t Hr = hit ? H : ((H | m) & kKr);
-      H = wr ? ((3u << xn2) | kHE | kHW) : Hr;
-      O = wr ? xn2 : O;
-      if (k < 8)
-        F0 += miss << (2u * xn2);
-      else
-        F1 += miss << (2u * xn2);
-      T += miss;
-      {
-        const uint32_t qm = (uint32_t)((int32_t)(H << 13) >> 31);
-        Hc = (H & qm) | (Hc & ~qm);
-      }
-      // accumulate now: left alone, the compiler sinks these sums past the walk and keeps every
-      // event's intermediate values live (140+ VGPRs)
-      asm volatile("" : "+v"(inv), "+v"(xfer), "+v"(F0), "+v"(F1), "+v"(Hc), "+v"(Xc));
     }
+    xprevh = X[kFH - 1];
   }
   if (nv && last_end) COH_END_SEG(xlast >> 4);
   if (hasS) COH_FLUSH_S();
@@ -980,13 +996,17 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     }
   }
   if (kFull && lane == 63 && !last_end) {  // the wave's last segment continues
-    const uint32_t p = X[kFK - 1] >> 4, c = sin & ~kConst;
+    const uint32_t p = xlast >> 4, c = sin & ~kConst;
     if (c && p < n_pages) atomicAdd(&pst[2 * (uint64_t)p + 1], c);
   }
 
   // ---- totals: one partial row per wave (16-bit fields hold a wave's sums)
-  uint32_t Fe = (F0 & 0x0F0F0F0Fu) + (F1 & 0x0F0F0F0Fu);              // nodes 0, 2, 4, 6
-  uint32_t Fo = ((F0 >> 4) & 0x0F0F0F0Fu) + ((F1 >> 4) & 0x0F0F0F0Fu);  // nodes 1, 3, 5, 7
+  uint32_t Fe = 0, Fo = 0;  // bytes: nodes 0, 2, 4, 6 / 1, 3, 5, 7
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    Fe += F[q] & 0x0F0F0F0Fu;
+    Fo += (F[q] >> 4) & 0x0F0F0F0Fu;
+  }
   {
     const uint32_t e = hitP & 0x55u, o = (hitP >> 1) & 0x55u;
     Fe -= (e & 1u) | ((e & 4u) << 6) | ((e & 16u) << 12) | ((e & 64u) << 18);
@@ -1024,6 +1044,7 @@ __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt
                                                        uint32_t* __restrict__ partial,
                                                        uint32_t* __restrict__ err,
                                                        uint32_t n_nodes) {
+  __shared__ __attribute__((aligned(16))) uint32_t tr_all[4][kFBlock];
   uint64_t b;
   if (kFull) {
     // kFoldCtrs ticket counters (one 256-B line each) keyed by blockIdx % kFoldCtrs: one counter
@@ -1031,18 +1052,20 @@ __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt
     // Workgroup w = ticket * kFoldCtrs + class is a permutation of blockIdx inside each class, and
     // every class draws its tickets in dispatch order, so the lowest block nobody has claimed is
     // always claimed once running blocks finish: no wave waits for a block that cannot run.
-    __shared__ uint32_t ticket;
+    // (the ticket passes through wave 0's event buffer: a separate LDS word would take the
+    // workgroup past 32 KiB and cost a workgroup per CU)
     const uint32_t cls = blockIdx.x % kFoldCtrs;
-    if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
+    if (threadIdx.x == 0) tr_all[0][0] = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
     __syncthreads();
-    const uint64_t w = (uint64_t)__builtin_amdgcn_readfirstlane(ticket) * kFoldCtrs + cls;
+    const uint32_t ticket = __builtin_amdgcn_readfirstlane(tr_all[0][0]);
+    __syncthreads();
+    const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
     b = w * 4 + (threadIdx.x >> 6);
     if (b >= nb) return;
   } else {
     if (threadIdx.x >= 64) return;
     b = nb - 1;
   }
-  __shared__ __attribute__((aligned(16))) uint32_t tr_all[4][kFBlock + kFBlock / 16];
   coh_fold_wave<kVec, kFull, kNodes>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err,
                                      n_nodes, tr_all[threadIdx.x >> 6]);
 }

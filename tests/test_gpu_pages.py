@@ -563,3 +563,76 @@ def test_c1_windows_pinned_by_reference_diff(golden):
         rep = c.download("replica").reshape(-1, 1024)
     for w in range(len(rep)):
         assert zlib.crc32(rep[w].tobytes()) == int(g["crc"][w][1]), w
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_diff_apply_fused_equals_diff_then_apply(variant, golden):
+    """gdsm_diff_apply (the diff kernel also applying the runs to a home copy on this GPU) writes
+    the same stream as gdsm_diff, and leaves the target exactly as gdsm_apply of that stream
+    would, also when the target is NOT the twin (bytes outside the runs keep their old values),
+    with id lists, in every diff geometry."""
+    L = _lib.load()
+    assert L.gdsm_tune(b"diff_variant", variant) == 0
+    try:
+        rng = np.random.default_rng(300 + variant)
+        g = golden["pages"]
+        cases = [(g["edge_twin"], g["edge_cur"])]
+        for density in (0.002, 0.05, 0.7):
+            tw = rng.integers(0, 256, (130, 4096), dtype=np.uint8)
+            cu = tw.copy()
+            mask = rng.random(tw.shape) < density
+            cu[mask] ^= rng.integers(1, 256, int(mask.sum()), dtype=np.uint8)
+            cases.append((tw, cu))
+        cases.append(oracle.gen_pages(300, seed=5, mode=0, ppm=10000))
+        cases.append(oracle.gen_pages(300, seed=5, mode=1, ppm=100000))
+        cases.append(_lds_overflow_pages(rng, 120))
+        for tw, cu in cases:
+            n = len(tw)
+            rep = rng.integers(0, 256, tw.shape, dtype=np.uint8)  # a home copy unlike the twin
+            ids = rng.permutation(n).astype(np.uint32)
+            ro, data = oracle.diff_pages(tw, cu, ids=ids)
+            want = rep.copy()
+            assert oracle.apply(want, ro, data, ids=ids) == 0
+            with ga.Context(n) as c:
+                c.upload("twin", tw)
+                c.upload("current", cu)
+                c.upload("replica", rep)
+                d_ids = c.ids(ids)
+                runs = c.diff(d_ids, cap=max(64, int(ro[-1])), apply_to="replica")
+                _eq_runs(runs.to_host(), ro, data)
+                assert np.array_equal(c.download("replica"), want)
+    finally:
+        L.gdsm_tune(b"diff_variant", 0)
+
+
+def test_diff_apply_applies_every_page_past_capacity():
+    """With a stream too small for the records, gdsm_diff_apply still applies every page (the
+    stream reports -ENOSPC; records past the capacity are not stored)."""
+    n = 500
+    tw, cu = oracle.gen_pages(n, seed=12, mode=1, ppm=100000)
+    with ga.Context(n) as c:
+        c.upload("twin", tw)
+        c.upload("current", cu)
+        c.upload("replica", tw)
+        runs = c.diff(cap=4096, apply_to="replica")
+        with pytest.raises(GdsmError) as ei:
+            runs.total()
+        assert ei.value.errno == 28
+        assert np.array_equal(c.download("replica"), cu)
+
+
+def test_diff_apply_config2_full_size():
+    """BASELINE config 2 at full size through the fused path the bench times: the whole stream
+    equals gdsm_diff's, REPLICA == CURRENT afterwards (the diff of the two is empty)."""
+    n = 1 << 20
+    L = _lib.load()
+    with ga.Context(n) as c:
+        c.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000)
+        a = c.diff(cap=256 << 20).to_host()
+        b = c.diff(cap=256 << 20, apply_to="replica").to_host()
+        assert np.array_equal(a.rec_off, b.rec_off) and np.array_equal(a.data, b.data)
+        chk = ga.Runs(c, n, cap=1 << 20)
+        ws = c.buffer(L.gdsm_diff_workspace_bytes(n))
+        rc = L.gdsm_diff_raw(c.arena_ptr("replica"), c.arena_ptr("current"), None, n,
+                             chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes, c.stream)
+        assert rc == 0 and chk.total() == 0
