@@ -684,6 +684,19 @@ __device__ __forceinline__ uint32_t wave_rev_compose_dpp(uint32_t v) {
   return lane_bcast(v, 63);
 }
 
+// 2v + (this lane's bit of `mask`): one v_addc with the lane mask as carry-in.
+__device__ __forceinline__ uint32_t shl1_add(uint32_t v, uint64_t mask) {
+  uint32_t r;
+  uint64_t cout;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(cout) : "v"(v), "s"(mask));
+  return r;
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {  // (a & m) | (b & ~m)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
 // LDS slot of block event e (lo dword): an XOR swizzle of the 4-dword group (bits 2-5) by bits
 // 6-9, so the coalesced b64 writes and the per-lane b128 reads of 4 consecutive events both spread
 // over all 64 banks, without padding (8 KiB per wave keeps 5 workgroups per CU).
@@ -734,6 +747,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
       *reinterpret_cast<u32x2*>(tr + fold_slot(128 * q + 2 * lane)) = (u32x2){v.x, v.z};
     }
   } else {
+#pragma unroll 8
     for (uint32_t k = 0; k < kFK; ++k) {
       const uint64_t e = (k < nv) ? ev[g0 + k] : 0ull;
       tr[fold_slot(kFK * lane + k)] = (uint32_t)e;
@@ -749,9 +763,10 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   if (lane == 0) xp = xprev_w;
   const bool batch_first = lo == 0 && lane == 0;
 
-  // ---- heads (a new page), the first / last head events, validity
+  // ---- heads (a new page), validity. (Sortedness inside a lane is checked where the walk meets
+  // a head; the first / last head events are read back from LDS.)
   uint32_t X[kFH];
-  uint32_t hm = 0, hc = 0, xf = 0, xl = 0, nodes = 0;
+  uint32_t hm = 0, nodes = 0;
   uint32_t bad = hib ? 1u : 0u;
 #pragma unroll
   for (uint32_t h = 0; h < kFK / kFH; ++h) {
@@ -764,22 +779,27 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
         const uint32_t pg = x >> 4, pp = pv >> 4;
         const bool first = k == 0 && batch_first;
         const bool head = first || pg != pp;
-        if (!first && pg < pp) bad = 1;
-        hm |= (head ? 1u : 0u) << k;
-        if (kNodes) nodes |= 1u << (x & 14u);
-        if (head) {
-          if (hc == 0) xf = x;
-          xl = x;
-          ++hc;
-        }
+        if (k == 0 && !first && pg < pp) bad = 1;
+        if (kFull)
+          hm = shl1_add(hm, __ballot(head));  // bit 31 - k, one v_addc per event
+        else
+          hm |= (head ? 1u : 0u) << k;
+        if (kNodes) nodes = max(nodes, x & 14u);  // 2 * the largest node
       }
     }
     xp = X[kFH - 1];
   }
+  if (kFull) hm = __brev(hm);
+  const uint32_t hc = (uint32_t)__popc(hm);
+  uint32_t xf = 0, xl = 0;  // the lane's first and last head events
+  if (hc) {
+    xf = tr[fold_slot(kFK * lane + (uint32_t)__builtin_ctz(hm))];
+    xl = tr[fold_slot(kFK * lane + 31u - (uint32_t)__builtin_clz(hm))];
+  }
   // opaque from here on: the walk re-derives its per-event head flags from these words instead
-  // of the compiler keeping the prologue's 32 masks and running head counts live
-  asm volatile("" : "+v"(hm), "+v"(hc), "+v"(xf), "+v"(xl));
-  if (kNodes && (nodes & ~((1u << (2 * n_nodes)) - 1u) & kHRead)) bad = 1;
+  // of the compiler keeping the prologue's 32 masks live
+  asm volatile("" : "+v"(hm), "+v"(xf), "+v"(xl), "+v"(nodes));
+  if (kNodes && (nodes >> 1) >= n_nodes) bad = 1;
   if (nv && (xlast >> 4) >= n_pages) bad = 1;
   // does the lane's last event end its segment? (the next lane's first event is a head, or the
   // next wave's, or the batch ends there)
@@ -788,12 +808,11 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   bool last_end = nh0 != 0;
   if (!kFull && nv > 0 && g0 + nv == n) last_end = true;
 
-  // ---- page-table words of the lane's first and last heads (one gathered load each)
-  uint64_t Wl = 0, Wf = 0;
-  {
-    const uint32_t pl = xl >> 4, pf = xf >> 4;
+  // ---- page-table word of the lane's last head (one gathered load)
+  uint64_t Wl = 0;  // (other heads of a lane load their word in the walk; only this one can be
+  {                  // stored by another wave, so only this one must land before the publish)
+    const uint32_t pl = xl >> 4;
     if (hc && pl < n_pages) Wl = pt[pl];
-    if (hc > 1 && pf < n_pages) Wf = pt[pf];
   }
   const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
   const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
@@ -808,10 +827,9 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   uint32_t H = kPRE, O = 0x1FEu, B = 0, Bfo = 0, c0 = 0, T = 0, hs = 0;
   uint32_t inv = 0, xfer = 0, F[4] = {0, 0, 0, 0}, Hc = kPRE, Xc = 0, pm = ~0u;
   uint32_t sH = 0, sO = 0, sB = 0, sBf = 0, sN = 0, sP = 0;  // pending local segment end
-  uint32_t dH = 0, dO = 0, dT = 0, dP = 0;                   // the lane's first segment end
+  uint32_t dHOT = 0;  // the lane's first segment end: H | O << 19 | T << 23 (read only when the
+                      // lane wrote before it: then O <= 14 and T <= 32)
   bool local = false, hasS = false, hasD = false;
-  uint32_t kEW = kHE | kHW;  // kept in a register (the write state's constant part)
-  asm volatile("" : "+v"(kEW));
 // (macros, not lambdas: captured flags end up in scratch memory)
 #define COH_FLUSH_S()                                                                        \
   do {                                                                                       \
@@ -820,10 +838,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
 #define COH_END_SEG(p_)        \
   do {                         \
     if (!local) {              \
-      dH = H;                  \
-      dO = O;                  \
-      dT = T;                  \
-      dP = (p_);               \
+      dHOT = H | ((O & 15u) << 19) | (T << 23); \
       hasD = true;             \
     } else {                   \
       if (hasS) COH_FLUSH_S(); \
@@ -845,20 +860,21 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
       const uint32_t k = kFH * h + j;
       if (kFull || k < nv) {
         const uint32_t x = X[j];
-        Xc = (x & pm) | (Xc & ~pm);  // v_bfi: the event, while still in the prefix
+        Xc = bfi(pm, x, Xc);  // the event, while still in the prefix
         if ((hm >> k) & 1u) {  // a head: the previous segment ends, this one's base is its word
-          if (k > 0) COH_END_SEG((j ? X[j ? j - 1 : 0] : xprevh) >> 4);
+          if (k > 0) {
+            const uint32_t pp = (j ? X[j ? j - 1 : 0] : xprevh) >> 4;
+            if ((x >> 4) < pp) bad = 1;  // pages must not decrease
+            COH_END_SEG(pp);
+          }
           if (hs + 1 == hc) {
             H = Hl;
             O = Ol;
             B = Bl;
             Bfo = Bfl;
           } else {
-            uint64_t w = Wf;
-            if (hs != 0) {
-              const uint32_t p = x >> 4;
-              w = p < n_pages ? pt[p] : 0ull;
-            }
+            const uint32_t p = x >> 4;
+            const uint64_t w = p < n_pages ? pt[p] : 0ull;
             B = (uint32_t)w & 0x7FFFFu;
             Bfo = (uint32_t)(w >> 32);
             H = hit_seed(B);
@@ -878,13 +894,13 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
         asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(inv) : "v"(sel), "v"(inv));
         xfer += (wr && O != xn2) ? 1u : 0u;  // a write by a non-owner always faults
         const uint32_t Hr = hit ? H : ((H | m) & kKr);
-        H = wr ? ((3u << xn2) | kEW) : Hr;
+        H = wr ? ((3u << xn2) | (kHE | kHW)) : Hr;
         O = wr ? xn2 : O;
-        F[k / 8] += miss << (2u * xn2);
+        asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(F[k / 8]) : "v"(miss), "v"(2u * xn2), "v"(F[k / 8]));
         T += miss;
         pm = (uint32_t)((int32_t)(H << 13) >> 31);  // still in the prefix after this event
         asm volatile("" : "+v"(pm));
-        Hc = (H & pm) | (Hc & ~pm);
+        Hc = bfi(pm, H, Hc);
         // accumulate now: left alone, the compiler sinks these sums past the walk and keeps
         // every event's intermediate values live
         asm volatile("" : "+v"(inv), "+v"(xfer), "+v"(F[k / 8]), "+v"(Hc), "+v"(Xc));
@@ -972,9 +988,10 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   }
   // the lane's first segment ends here: its state and count
   uint32_t Df = 0, Dc = 0;
+  const uint32_t dP = tr[fold_slot(kFK * lane)] >> 4;  // the first segment's page
   if (hasD) {
-    Df = wfirst ? seg_final(dH, dO, 0u) : (s1 & 0x7FFFFu);
-    Dc = (uint32_t)((int32_t)dT + dfirst);
+    Df = wfirst ? seg_final(dHOT & 0x7FFFFu, (dHOT >> 19) & 15u, 0u) : (s1 & 0x7FFFFu);
+    Dc = (uint32_t)((int32_t)(dHOT >> 23) + dfirst);
   }
 
   // ---- fault counts of segments that cross lanes (counts only: old counts are 32-bit)
