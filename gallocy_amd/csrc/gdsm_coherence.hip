@@ -808,11 +808,12 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   bool last_end = nh0 != 0;
   if (!kFull && nv > 0 && g0 + nv == n) last_end = true;
 
-  // ---- page-table word of the lane's last head (one gathered load)
-  uint64_t Wl = 0;  // (other heads of a lane load their word in the walk; only this one can be
-  {                  // stored by another wave, so only this one must land before the publish)
-    const uint32_t pl = xl >> 4;
+  // ---- page-table words of the lane's last and first heads (one gathered load each)
+  uint64_t Wl = 0, Wf = 0;  // last and first heads (a lane's other heads load in the walk)
+  {
+    const uint32_t pl = xl >> 4, pf = xf >> 4;
     if (hc && pl < n_pages) Wl = pt[pl];
+    if (hc > 1 && pf < n_pages) Wf = pt[pf];
   }
   const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
   const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
@@ -873,8 +874,14 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
             B = Bl;
             Bfo = Bfl;
           } else {
-            const uint32_t p = x >> 4;
-            const uint64_t w = p < n_pages ? pt[p] : 0ull;
+            // Wf holds this head's word: loaded with the last head's for the first one, and
+            // prefetched at the previous head for the ones after it
+            const uint64_t w = Wf;
+            if (k + 1 < kFK && hs + 2 < hc) {  // another head before the last: prefetch it
+              const uint32_t kn = k + 1 + (uint32_t)__builtin_ctz(hm >> (k + 1 < kFK ? k + 1 : 0));
+              const uint32_t pn = tr[fold_slot(kFK * lane + kn)] >> 4;
+              Wf = pn < n_pages ? pt[pn] : 0ull;
+            }
             B = (uint32_t)w & 0x7FFFFu;
             Bfo = (uint32_t)(w >> 32);
             H = hit_seed(B);
@@ -926,6 +933,11 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   if (lane == 0)
     __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (whead ? kFHead : 0ull) | agg,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // Only a wave that stores the state of a segment opened before it (its first segment ends
+  // here) needs the head's wave to have loaded that page's word: it looks back to a block with a
+  // head. Every other wave stops at the nearest CONST aggregate or inclusive prefix (CONST
+  // absorbs everything before it), so the blocks of a hot page do not chain their look-backs.
+  const bool ordered = __ballot(hasD && (__ballot(hc != 0) & ((1ull << lane) - 1ull)) == 0) != 0;
   uint32_t carry = 0;
   if (b > 0) {
     int64_t pos = (int64_t)b - 1;
@@ -936,7 +948,9 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
       uint32_t s, spins = 0;
       for (;;) {
         const uint64_t pub = __ballot((st >> 62) != 0);
-        const uint64_t stop = __ballot((st >> 62) == 2 || (st & kFHead));
+        const uint64_t stop =
+            __ballot(ordered ? (st & kFHead) != 0
+                             : ((st >> 62) == 2 || (st & kFHead) || (st & kConst)));
         const uint32_t u = ~pub ? (uint32_t)__builtin_ctzll(~pub) : 64u;
         s = (stop & pub) ? (uint32_t)__builtin_ctzll(stop & pub) : 64u;
         if (s < u || u == 64) break;
