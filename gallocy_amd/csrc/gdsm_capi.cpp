@@ -84,6 +84,7 @@ int check_and_clear_err(gdsm_ctx* ctx) {
   GDSM_TRY(hipMemcpyAsync(&h, ctx->err, 4, hipMemcpyDeviceToHost, ctx->stream));
   GDSM_TRY(hipMemsetAsync(ctx->err, 0, 4, ctx->stream));
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  if (h && getenv("GDSM_DEBUG_ERR")) fprintf(stderr, "gdsm err word 0x%x\n", h);
   return h ? -EINVAL : 0;
 }
 

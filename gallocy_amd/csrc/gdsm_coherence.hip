@@ -720,7 +720,8 @@ __device__ __forceinline__ void fold_half(const uint32_t* __restrict__ tr, uint3
   for (uint32_t k = 0; k < kFH; ++k) asm volatile("" : "+v"(X[k]));
 }
 
-template <bool kVec, bool kFull, bool kNodes>
+// kM (MEASUREMENT ONLY, -DGDSM_MEASURE builds, output invalid): 1 = no walk, 2 = no look-back.
+template <bool kVec, bool kFull, bool kNodes, int kM = 0>
 __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                               const uint64_t* __restrict__ ev, uint64_t n,
                                               uint64_t b, uint64_t* __restrict__ status,
@@ -854,7 +855,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   } while (0)
   uint32_t xprevh = 0;  // the event before X[0] in this lane (half 1)
 #pragma unroll
-  for (uint32_t h = 0; h < kFK / kFH; ++h) {
+  for (uint32_t h = 0; h < (kM == 1 ? 0u : kFK / kFH); ++h) {
     fold_half(tr, lane, h, X);
 #pragma unroll
     for (uint32_t j = 0; j < kFH; ++j) {
@@ -939,7 +940,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   // absorbs everything before it), so the blocks of a hot page do not chain their look-backs.
   const bool ordered = __ballot(hasD && (__ballot(hc != 0) & ((1ull << lane) - 1ull)) == 0) != 0;
   uint32_t carry = 0;
-  if (b > 0) {
+  if (b > 0 && kM != 2) {
     int64_t pos = (int64_t)b - 1;
     for (;;) {
       const int64_t q = pos - (int64_t)lane;
@@ -1062,13 +1063,13 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     if (lane == 2u * q + 1u) mine = s >> 16;
   }
   if (lane < 10) partial[b * 10 + lane] = mine;
-  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
+  if (kM == 0 && __ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
 // kFull: the batch's whole blocks, one ticket per workgroup (tickets are drawn in dispatch
 // order, so a wave only ever waits for running waves); otherwise the single trailing partial
 // block `nb - 1`, launched after them.
-template <bool kVec, bool kFull, bool kNodes>
+template <bool kVec, bool kFull, bool kNodes, int kM = 0>
 __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                        const uint64_t* __restrict__ ev, uint64_t n,
                                                        uint64_t nb, uint64_t* __restrict__ ws,
@@ -1097,7 +1098,7 @@ __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt
     if (threadIdx.x >= 64) return;
     b = nb - 1;
   }
-  coh_fold_wave<kVec, kFull, kNodes>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err,
+  coh_fold_wave<kVec, kFull, kNodes, kM>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err,
                                      n_nodes, tr_all[threadIdx.x >> 6]);
 }
 
@@ -1150,10 +1151,11 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 // ---------------------------------------------------------------- launchers
 // Coherence variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = the single-pass fold
 // (coh_fold_kernel, default); 1 = the round-2 four-pass path (tail aggregates, scan, block pass
-// C), kept for same-box A/B. Built with -DGDSM_MEASURE only: 2 / 3 = the four-pass path without
-// page-table stores / without any page-table traffic (output invalid).
+// C), kept for same-box A/B. Built with -DGDSM_MEASURE only (output invalid): 2 / 3 = the
+// four-pass path without page-table stores / without any page-table traffic; 4 / 5 = the fold
+// without its walk / without its look-back.
 #ifdef GDSM_MEASURE
-constexpr int kCohVariants = 4;
+constexpr int kCohVariants = 6;
 #else
 constexpr int kCohVariants = 2;
 #endif
@@ -1203,7 +1205,7 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   if (r != hipSuccess || n_events == 0) return r;
   const uint64_t nb = coh_blocks(n_events), ng = coh_groups(nb);
   if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
-  if (g_coh_variant == 0) {
+  if (g_coh_variant == 0 || g_coh_variant >= 4) {
     const uint64_t nf = fold_blocks(n_events);
     uint64_t* fws = reinterpret_cast<uint64_t*>(ws);
     uint32_t* fpart = reinterpret_cast<uint32_t*>(fws + kFoldStatus + nf);
@@ -1217,6 +1219,10 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
       if (full) {
         auto kern = vec ? (nodes ? coh_fold_kernel<true, true, true> : coh_fold_kernel<true, true, false>)
                         : (nodes ? coh_fold_kernel<false, true, true> : coh_fold_kernel<false, true, false>);
+#ifdef GDSM_MEASURE
+        if (vec && !nodes && g_coh_variant == 4) kern = coh_fold_kernel<true, true, false, 1>;
+        if (vec && !nodes && g_coh_variant == 5) kern = coh_fold_kernel<true, true, false, 2>;
+#endif
         hipLaunchKernelGGL(kern, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
                            events, n_events, full, fws, fpart, err, n_nodes);
       }

@@ -28,7 +28,12 @@ for r in range(4):
         assert gdsm.lib().gdsm_tune(b"coh_variant", v) == 0
         ctx.coh_init(8)
         ctx.prof_enable(True)
-        t = ctx.coherence_batch(ev)
+        try:
+            t = ctx.coherence_batch(ev)
+        except gdsm.GdsmError:
+            if v < 2:
+                raise
+            t = None  # measurement-only variants (invalid output) may flag the batch
         p = ctx.prof_read()
         ctx.prof_enable(False)
         res[v].append({k: x[0] / x[1] for k, x in p.items() if x[1]})

@@ -8,9 +8,11 @@ A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_WAIT
 B="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SALU SQ_BUSY_CYCLES SQ_LEVEL_WAVES SQ_INSTS_SMEM"
 C="SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
 for v in ${COH_PMC_VARIANTS:-0}; do
-  for p in a b c; do
-    case $p in a) CT=$A;; b) CT=$B;; c) CT=$C;; esac
-    timeout -s KILL 90 rocprofv3 --pmc $CT --kernel-trace -d $OUT/$p$v -o $p --output-format csv -- python3 scripts/coh_pmc.py 268435456 uniform $v > $OUT/$p$v.log 2>&1 || exit 1
+  for d in ${COH_PMC_DISTS:-uniform}; do
+    for p in a b c; do
+      case $p in a) CT=$A;; b) CT=$B;; c) CT=$C;; esac
+      timeout -s KILL 90 rocprofv3 --pmc $CT --kernel-trace -d $OUT/$p$v$d -o $p --output-format csv -- python3 scripts/coh_pmc.py 268435456 $d $v > $OUT/$p$v$d.log 2>&1 || exit 1
+    done
   done
 done
 python3 - <<'PY'
