@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="double-buffered steps (exchange/apply k overlaps diff k+1); auto = on "
                          "for N > 1 (hides the RCCL exchange), off on one GPU (HBM-bound)")
-    ap.add_argument("--fuse", choices=["on", "off"], default="on",
+    ap.add_argument("--fuse", choices=["on", "off"], default="off",
                     help="N = 1: on = gdsm_diff_apply (the diff kernel applies each page's runs "
                          "to its home copy from the registers that found them); off = gdsm_diff "
                          "then gdsm_apply of the stream")
@@ -158,15 +158,16 @@ def read_traffic(pages: int, mode: str, ppm: int, fused: bool):
 
 
 def read_coh_traffic(dist: str, pages: int, events: int):
-    """Per-launch HBM bytes of coherence pass C from the newest committed PMC summary of the same
-    batch shape (profiles/*coh_traffic*.json, scripts/coh_traffic.sh), else None."""
+    """Per-launch HBM bytes of the coherence fold kernel from the newest committed PMC summary of
+    the same batch shape (profiles/*coh_traffic*.json, scripts/coh_traffic.sh), else None."""
     want = {"workload": "coherence", "dist": dist, "pages": pages, "events": events}
     for p in sorted((ROOT / "profiles").glob("*coh_traffic*.json"), reverse=True):
         try:
             j = json.loads(p.read_text())
         except Exception:  # noqa: BLE001
             continue
-        if j.get("workload") == want and j.get("main_kernel_bytes_per_launch"):
+        if (j.get("workload") == want and j.get("main_kernel_bytes_per_launch")
+                and str(j.get("main_kernel", "")).startswith("gdsm::coh_fold_kernel")):
             return j["main_kernel_bytes_per_launch"], p.name
     return None, None
 
@@ -218,7 +219,7 @@ def run_coherence(args):
            "data": f"synthetic ({args.dist} page popularity, SPEC §6 events)",
            "config": {"workload": f"{n} pages, 8 nodes, {ev.count} events/batch, {args.dist}, 20% writes",
                       "touched_pages": touched},
-           "roofline": {"bound": "hbm", "kernel": "gdsm::coh_apply_block_kernel", "achieved": round(achieved, 1),
+           "roofline": {"bound": "hbm", "kernel": "gdsm::coh_fold_kernel", "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "traffic": traffic, "traffic_source": traffic_src,
                         "algorithmic_bytes_per_launch": int(alg),

@@ -13,6 +13,6 @@ for d in uniform zipf; do
   W=$(find $OUT/$d-WRITE_SIZE -name "*counter_collection.csv" | head -1)
   python3 scripts/pmc_summary.py "$F" "$W" $OUT/coh_traffic_$d.json \
     "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes, bench.py --workload coherence --dist $d --steps 3 --warmup 1 --no-cpu (16M pages, 1B events)" \
-    "gdsm::coh_apply_block_kernel" "{\"workload\": \"coherence\", \"dist\": \"$d\", \"pages\": 16777216, \"events\": 1073741824}" > /dev/null || exit 1
+    "gdsm::coh_fold_kernel" "{\"workload\": \"coherence\", \"dist\": \"$d\", \"pages\": 16777216, \"events\": 1073741824}" > /dev/null || exit 1
   echo "$d: $OUT/coh_traffic_$d.json"
 done

@@ -35,5 +35,7 @@ if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   W=$(find $OUT/write -name "*counter_collection.csv" | head -1)
   python3 scripts/pmc_summary.py "$F" "$W" $OUT/traffic.json > /dev/null && echo "traffic: $OUT/traffic.json"
   step kt_coh 600 rocprofv3 --kernel-trace --stats -d $OUT/kt_coh -o kt --output-format csv -- python3 bench.py --workload coherence --dist uniform --steps 5 --warmup 2 --no-cpu
+  step kt_coh_zipf 600 rocprofv3 --kernel-trace --stats -d $OUT/kt_coh_zipf -o kt --output-format csv -- python3 bench.py --workload coherence --dist zipf --steps 5 --warmup 2 --no-cpu
+  step coh_traffic 900 bash scripts/coh_traffic.sh
 fi
 echo "=== done"
