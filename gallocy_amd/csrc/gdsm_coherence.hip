@@ -720,7 +720,8 @@ __device__ __forceinline__ void fold_half(const uint32_t* __restrict__ tr, uint3
   for (uint32_t k = 0; k < kFH; ++k) asm volatile("" : "+v"(X[k]));
 }
 
-// kM (MEASUREMENT ONLY, -DGDSM_MEASURE builds, output invalid): 1 = no walk, 2 = no look-back.
+// kM (MEASUREMENT ONLY, -DGDSM_MEASURE builds, output invalid): 1 = no walk, 2 = no look-back,
+// 3 = no ordered look-back (no wave waits for the block holding its first segment's head).
 template <bool kVec, bool kFull, bool kNodes, int kM = 0>
 __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                               const uint64_t* __restrict__ ev, uint64_t n,
@@ -938,7 +939,8 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   // here) needs the head's wave to have loaded that page's word: it looks back to a block with a
   // head. Every other wave stops at the nearest CONST aggregate or inclusive prefix (CONST
   // absorbs everything before it), so the blocks of a hot page do not chain their look-backs.
-  const bool ordered = __ballot(hasD && (__ballot(hc != 0) & ((1ull << lane) - 1ull)) == 0) != 0;
+  const bool ordered = kM != 3 &&
+                       __ballot(hasD && (__ballot(hc != 0) & ((1ull << lane) - 1ull)) == 0) != 0;
   uint32_t carry = 0;
   if (b > 0 && kM != 2) {
     int64_t pos = (int64_t)b - 1;
@@ -1152,10 +1154,10 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 // Coherence variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = the single-pass fold
 // (coh_fold_kernel, default); 1 = the round-2 four-pass path (tail aggregates, scan, block pass
 // C), kept for same-box A/B. Built with -DGDSM_MEASURE only (output invalid): 2 / 3 = the
-// four-pass path without page-table stores / without any page-table traffic; 4 / 5 = the fold
-// without its walk / without its look-back.
+// four-pass path without page-table stores / without any page-table traffic; 4 / 5 / 6 = the
+// fold without its walk / without its look-back / without the ordered look-back.
 #ifdef GDSM_MEASURE
-constexpr int kCohVariants = 6;
+constexpr int kCohVariants = 7;
 #else
 constexpr int kCohVariants = 2;
 #endif
@@ -1222,6 +1224,7 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
 #ifdef GDSM_MEASURE
         if (vec && !nodes && g_coh_variant == 4) kern = coh_fold_kernel<true, true, false, 1>;
         if (vec && !nodes && g_coh_variant == 5) kern = coh_fold_kernel<true, true, false, 2>;
+        if (vec && !nodes && g_coh_variant == 6) kern = coh_fold_kernel<true, true, false, 3>;
 #endif
         hipLaunchKernelGGL(kern, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
                            events, n_events, full, fws, fpart, err, n_nodes);

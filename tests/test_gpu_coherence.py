@@ -241,3 +241,30 @@ def test_config4_full_size_parity(dist):
     assert rc == 0 and tot == otot
     assert np.array_equal(gst, st), np.flatnonzero(gst != st)[:10]
     assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_every_selectable_coherence_variant(variant):
+    """Both selectable coherence paths (gdsm_tune "coh_variant": 0 = the single-pass fold, the
+    default; 1 = the round-2 four-pass path kept for same-box A/B) are bit-exact on Zipf batches
+    with hot pages, uploaded arbitrary states, fewer nodes and a partial last block."""
+    L = ga.gdsm.lib()
+    assert L.gdsm_tune(b"coh_variant", variant) == 0
+    try:
+        n = 9000
+        rng = np.random.default_rng(500 + variant)
+        counts = zipf_counts(n, 130000, s=0.9, seed=31)
+        counts[rng.integers(0, n, 3)] = rng.integers(5000, 12000, 3)
+        ev = oracle.gen_events(counts, seed=32, n_nodes=5, write_pct=25)
+        with ga.Context(n, arenas=()) as c:
+            c.coh_init(5)
+            st = rng.integers(0, 1 << 19, n).astype(np.uint32)
+            fl = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+            c.coh_upload(st, fl)
+            tot = c.coherence_batch(ev)
+            rc, otot = oracle.coherence(st, fl, ev, n_nodes=5)
+            assert rc == 0 and tot == otot
+            gst, gfl = c.coh_download()
+            assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+    finally:
+        L.gdsm_tune(b"coh_variant", 0)
