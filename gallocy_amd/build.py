@@ -95,8 +95,9 @@ def build_sanitized(verbose: bool = False) -> Path:
     subprocess.run([str(clang), "-std=c99", "-O1", "-g", "-fPIC", "-shared", "-Wall",
                     "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
                     "-shared-libsan", "-fno-omit-frame-pointer",
-                    "-o", str(ROOT / "oracle" / "_san" / "liboracle.so"),
-                    str(ROOT / "oracle" / "gdsm_oracle.c")], check=True)
+                    "-fopenmp", "-o", str(ROOT / "oracle" / "_san" / "liboracle.so"),
+                    str(ROOT / "oracle" / "gdsm_oracle.c"),
+                    str(ROOT / "oracle" / "gdsm_oracle_bench.c")], check=True)
     return lib
 
 
