@@ -475,7 +475,9 @@ def main():
                   arenas=("twin", "current"))
     ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n, stride=1,
                   arenas=("replica",))
-    cap_pp = 256 if mode == ga.GEN_UNIFORM else 1024  # stream bytes per page reserved
+    # stream bytes per page reserved (uniform 1 %: ~66 B records; <= 128 B per page lets the
+    # diff take 64 pages per wave, gdsm_pages.hip diff_variant)
+    cap_pp = 128 if mode == ga.GEN_UNIFORM else 1024
     shard = None
     if world > 1:
         shard = exchange.Shard(ctx, rank, world, n, cap_pp,

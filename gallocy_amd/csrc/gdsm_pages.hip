@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     const uint32_t* __restrict__ ids, uint64_t n, uint64_t* __restrict__ rec_off,
     uint8_t* __restrict__ data, uint64_t cap, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target) {
-  static_assert(kU <= 32 && (kU & (kU - 1)) == 0, "unit size");
+  static_assert(kU <= 64 && (kU & (kU - 1)) == 0, "unit size");
   __shared__ uint32_t sel_tab[16];
   __shared__ uint32_t ent_all[4][64];
   __shared__ uint4 dat_all[4][64];
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   const uint32_t cnt = (uint32_t)min((uint64_t)kU, n - i0);
 
   uint32_t acc = 0;       // LDS bytes used by buffered records
-  uint32_t late = 0;      // bit j: page j is emitted from the arenas after the look-back
+  uint64_t late = 0;      // bit j: page j is emitted from the arenas after the look-back
   uint32_t my_size = 0;   // lane j: record size of page j
   uint32_t my_src = 0;    // lane j: LDS byte offset of page j's record
   uint4 t[4], c[4];
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     const uint32_t src = acc;
     if (D > 64u) {
       size = record_size_masks(m, lane);
-      late |= 1u << j;
+      late |= 1ull << j;
     } else if (D) {
       wave_lds_sync();
       const bool valid = lane < D;
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
       const uint32_t NR = tot & 0xFFFFu, NP = tot >> 16;
       size = 4u + 4u * NR + ((NP + 3u) & ~3u);
       if (acc + size > kBuf) {
-        late |= 1u << j;
+        late |= 1ull << j;
       } else {
         uint32_t* img = buf + acc / 4u;
         for (uint32_t q = lane; q < size / 4u; q += 64) img[q] = 0u;
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   if (u == 0 && lane == 0) rec_off[0] = 0;
   if (lane < kU) {
     tab[lane] = lane < cnt ? incl - my_size : agg;
-    tab[kU + 1 + lane] = ((late >> lane) & 1u) ? 0xFFFFFFFFu : my_src;
+    tab[kU + 1 + lane] = ((late >> lane) & 1ull) ? 0xFFFFFFFFu : my_src;
   }
   if (lane == 0) tab[kU] = agg;
   // only records that end inside the capacity are stored (SPEC §3)
@@ -520,8 +520,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     const uint32_t src = tab[kU + 1 + j];
     if (src != 0xFFFFFFFFu) __builtin_nontemporal_store(buf[(src + byte - tab[j]) / 4u], dst + g);
   }
-  for (uint32_t rem = late; rem;) {  // wave-uniform
-    const uint32_t j = (uint32_t)__builtin_ctz(rem);
+  for (uint64_t rem = late; rem;) {  // wave-uniform
+    const uint32_t j = (uint32_t)__builtin_ctzll(rem);
     rem &= rem - 1;
     if (excl + tab[j + 1] > cap) continue;
     const uint64_t i = i0 + j;
@@ -767,24 +767,26 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
 // Diff geometry, gdsm_tune("diff_variant", v) or GDSM_DIFF_VARIANT=v; every variant writes the
 // same canonical stream (tests/test_gpu_pages.py checks each):
 //   0  automatic (default): 2 pages per wave for short lists (n <= 32768: a wave walks its
-//      pages one after the other, so a few dozen pages must not share one wave), else 32 pages
-//      per wave when the caller's stream capacity allows at most 384 B per page (sparse writes:
-//      config 2's ~66 B records; fewer look-backs), else 16
+//      pages one after the other, so a few dozen pages must not share one wave), else 64 pages
+//      per wave when the caller's stream capacity allows at most 128 B per page (sparse writes:
+//      config 2's ~66 B records; 64 records fill the 8 KiB buffer; fewest look-backs), else 32
+//      pages per wave up to 384 B per page, else 16
 //   1  16 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 //   2  32 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 //   3  2 pages per wave
+//   4  64 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 // Measurement-only kernels (invalid output) are not part of the library.
 static int g_diff_variant = -1;
 static int diff_variant() {
   if (g_diff_variant < 0) {
     const char* e = getenv("GDSM_DIFF_VARIANT");
     const int v = e ? atoi(e) : 0;
-    g_diff_variant = (v >= 0 && v <= 3) ? v : 0;
+    g_diff_variant = (v >= 0 && v <= 4) ? v : 0;
   }
   return g_diff_variant;
 }
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 3) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 4) {
     g_diff_variant = (int)value;
     return 0;
   }
@@ -846,18 +848,20 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   int v = diff_variant();
-  if (v == 0) v = n <= kDiffShort ? 3 : (cap <= 384 * n) ? 2 : 1;
-  const uint32_t U = v == 3 ? 2 : v == 2 ? 32 : 16;
+  if (v == 0) v = n <= kDiffShort ? 3 : (cap <= 128 * n) ? 4 : (cap <= 384 * n) ? 2 : 1;
+  const uint32_t U = v == 4 ? 64 : v == 3 ? 2 : v == 2 ? 32 : 16;
   const uint64_t nunits = (n + U - 1) / U;
   if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
   // ticket counter + status granules, zeroed per launch (outside the timed kernel)
   hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
   if (e != hipSuccess) return e;
   ProfScope ps(prof, 0, s);
-  auto kern = target ? (v == 3   ? diff_single_kernel<2, 8192, 4, true>
+  auto kern = target ? (v == 4   ? diff_single_kernel<64, 8192, 4, true>
+                       : v == 3 ? diff_single_kernel<2, 8192, 4, true>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, true>
                                 : diff_single_kernel<16, 8192, 4, true>)
-                     : (v == 3   ? diff_single_kernel<2, 8192, 4, false>
+                     : (v == 4   ? diff_single_kernel<64, 8192, 4, false>
+                       : v == 3 ? diff_single_kernel<2, 8192, 4, false>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, n,
