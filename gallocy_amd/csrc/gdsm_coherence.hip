@@ -53,9 +53,18 @@ __device__ unsigned long long g_coh_stamps[8192 * 4 * 8];
       g_coh_stamps[((blockIdx.x / 64) * 4 + (threadIdx.x >> 6)) * 8 + (i)] =                  \
           __builtin_amdgcn_s_memtime();                                                       \
   } while (0)
+// Fold kernel: every 16th block b (by ticket), lane 0: [0] entry, [1] events in LDS, [2] walk
+// done, [3] look-back done, [4] end (s_memtime), [5] ordered | heads << 1 | look-back rounds << 16
+#define COH_FSTAMP(i, v)                                                                     \
+  do {                                                                                        \
+    if ((b & 15) == 0 && b / 16 < 32768 && lane == 0) g_coh_stamps[(b / 16) * 8 + (i)] = (v); \
+  } while (0)
 #else
 #define COH_STAMP(i) \
   do {               \
+  } while (0)
+#define COH_FSTAMP(i, v) \
+  do {                   \
   } while (0)
 #endif
 
@@ -734,6 +743,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   const uint64_t g0 = lo + (uint64_t)lane * kFK;  // global index of this lane's first event
   const uint32_t nv =
       kFull ? kFK : (uint32_t)min((uint64_t)kFK, g0 < n ? n - g0 : (uint64_t)0);
+  COH_FSTAMP(0, __builtin_amdgcn_s_memtime());
   // ---- events: low dwords (page << 4 | node << 1 | rw) into the wave's LDS copy of the block;
   // every high-dword bit is an error. Coalesced 16-B loads (load q: events [128q, 128q + 128),
   // two per lane); each lane then reads its 32 consecutive events 16 at a time. (Loading a
@@ -757,6 +767,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     }
   }
   wave_lds_sync();
+  COH_FSTAMP(1, __builtin_amdgcn_s_memtime());
   const uint32_t xprev_w = lo > 0 ? (uint32_t)ev[lo - 1] : 0u;               // uniform
   const bool has_next = lo + kFBlock < n;
   const uint32_t xnext_w = has_next ? (uint32_t)ev[lo + kFBlock] : 0u;        // uniform
@@ -924,6 +935,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
 
   // ---- lane aggregate (exact: the state after the lane's first CONST does not depend on the
   // incoming state; without a CONST the lane is READ(its reads)), scan, publish, look back
+  COH_FSTAMP(2, __builtin_amdgcn_s_memtime());
   const bool has_c = !(H & kPRE);
   const uint32_t a = has_c ? (kConst | seg_final(H, O, B)) : hit_copyset(H);
   const uint32_t inc = wave_incl_compose_dpp(a);
@@ -942,9 +954,15 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   const bool ordered = kM != 3 &&
                        __ballot(hasD && (__ballot(hc != 0) & ((1ull << lane) - 1ull)) == 0) != 0;
   uint32_t carry = 0;
+#ifdef GDSM_COH_STAMPS
+  uint32_t lb_rounds = 0;
+#endif
   if (b > 0 && kM != 2) {
     int64_t pos = (int64_t)b - 1;
     for (;;) {
+#ifdef GDSM_COH_STAMPS
+      ++lb_rounds;
+#endif
       const int64_t q = pos - (int64_t)lane;
       uint64_t st = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                            : kFIncl;
@@ -979,6 +997,11 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
       __hip_atomic_store(status + b, kFIncl | (whead ? kFHead : 0ull) | tcompose(carry, agg),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#ifdef GDSM_COH_STAMPS
+  COH_FSTAMP(3, __builtin_amdgcn_s_memtime());
+  COH_FSTAMP(5, (ordered ? 1ull : 0ull) | ((uint64_t)__popcll(__ballot(hc != 0)) << 1) |
+                    ((uint64_t)lb_rounds << 16));
+#endif
   const uint32_t cur = tcompose(carry, from_prev_lane(inc));
   const bool cont = nv && !(hm & 1u);  // the lane's first event continues a segment
   if (cont && !(cur & kConst)) bad = 1;
@@ -1066,6 +1089,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   }
   if (lane < 10) partial[b * 10 + lane] = mine;
   if (kM == 0 && __ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
+  COH_FSTAMP(4, __builtin_amdgcn_s_memtime());
 }
 
 // kFull: the batch's whole blocks, one ticket per workgroup (tickets are drawn in dispatch
