@@ -941,7 +941,9 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   const uint32_t inc = wave_incl_compose_dpp(a);
   const uint32_t agg = lane_bcast(inc, 63);
   const bool whead = __ballot(hc != 0) != 0;
-  // every load of this wave has landed before its status is visible (see above)
+  // every load of this wave has landed before its status is visible (see above). (Waiting only
+  // for the last head's word, not for the walk's stores, measured the same: the wave's tail then
+  // waits for them instead.)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (lane == 0)
@@ -999,8 +1001,8 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   }
 #ifdef GDSM_COH_STAMPS
   COH_FSTAMP(3, __builtin_amdgcn_s_memtime());
-  COH_FSTAMP(5, (ordered ? 1ull : 0ull) | ((uint64_t)__popcll(__ballot(hc != 0)) << 1) |
-                    ((uint64_t)lb_rounds << 16));
+  const uint64_t st_heads = (uint64_t)__popcll(__ballot(hc != 0));
+  COH_FSTAMP(5, (ordered ? 1ull : 0ull) | (st_heads << 1) | ((uint64_t)lb_rounds << 16));
 #endif
   const uint32_t cur = tcompose(carry, from_prev_lane(inc));
   const bool cont = nv && !(hm & 1u);  // the lane's first event continues a segment
