@@ -633,12 +633,13 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
 // it: the block's carry comes from a decoupled look-back over the other waves' published
 // aggregates (the diff kernel's protocol), so passes A and B and their head snapshots go away.
 //
-// The walk keeps, per lane, a HIT MASK instead of the state word: bit 2n = a read by node n hits
-// (n in the copyset), bit 2n+1 = a write by n hits (EXCLUSIVE, owned by n), kHE = EXCLUSIVE,
-// kHW = a write since the segment's base. The event's low nibble (node << 1 | rw) is its bit
-// index, so "does it fault" is one bit-field extract, a read miss is (H | bit) & kKr and every
-// write sets H = 3 << 2n | kHE | kHW. O = 2 * owner for transfers. The state word of a segment
-// end is rebuilt from (H, O, base) only where a segment ends.
+// The walk keeps, per lane, a HIT MASK instead of the state word: bit n = a read by node n hits
+// (n in the copyset: bits 0-7 ARE the state word's copyset), bit 8 + n = a write by n hits
+// (EXCLUSIVE, owned by n), kHE = EXCLUSIVE, kHW = a write since the segment's base. An event's
+// bit index is node + 8 * rw, so "does it fault" is one bit-field extract, a read miss is
+// (H | bit) & kKr and every write sets H = 0x101 << n | kHE | kHW. O = 2 * owner for transfers.
+// The state word of a segment end is rebuilt from (H, O, base) only where a segment ends, and a
+// head's hit mask is its word's copyset plus one write bit (no bit spreading: heads are frequent).
 //
 // Ordering without head snapshots: the only page-table word this wave loads that another wave
 // may store is the one of its last head (that segment can end in a later wave). A wave whose
@@ -649,27 +650,19 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
 constexpr uint32_t kFK = 32;                // events per lane
 constexpr uint32_t kFH = 16;                // of them held in registers at a time
 constexpr uint32_t kFBlock = 64 * kFK;
-constexpr uint32_t kHE = 0x10000u, kHW = 0x20000u, kPRE = 0x40000u, kHRead = 0x5555u;
+constexpr uint32_t kHE = 0x10000u, kHW = 0x20000u, kPRE = 0x40000u, kHRead = 0xFFu;
 constexpr uint32_t kKr = kHRead | kHW | kPRE;  // kept by a read miss
 constexpr uint64_t kFAgg = 1ull << 62, kFIncl = 2ull << 62, kFHead = 1ull << 61;
 constexpr uint32_t kFoldCtrs = 8;                   // workgroup ticket counters
 constexpr uint64_t kFoldStatus = kFoldCtrs * 32;    // u64 index of block 0's status granule
 
 __device__ __forceinline__ uint32_t hit_seed(uint32_t w) {
-  uint32_t c = w & 0xFFu;
-  c = (c | (c << 4)) & 0x0F0Fu;
-  c = (c | (c << 2)) & 0x3333u;
-  c = (c | (c << 1)) & 0x5555u;
+  const uint32_t c = w & 0xFFu;
   const uint32_t owner = (w >> 8) & 0xFFu;
-  const uint32_t wbit = owner < 8u ? (2u << (2u * owner)) : 0u;
+  const uint32_t wbit = owner < 8u ? (0x100u << owner) : 0u;
   return (((w >> 16) & 3u) == 2u) ? (c | kHE | wbit) : c;
 }
-__device__ __forceinline__ uint32_t hit_copyset(uint32_t h) {
-  uint32_t t = h & kHRead;
-  t = (t | (t >> 1)) & 0x3333u;
-  t = (t | (t >> 2)) & 0x0F0Fu;
-  return (t | (t >> 4)) & 0xFFu;
-}
+__device__ __forceinline__ uint32_t hit_copyset(uint32_t h) { return h & kHRead; }
 // The state word at a segment end: the base is the last writer's word when the lane wrote since
 // the segment's base B (a head's word or the lane's incoming state), then the reads since.
 __device__ __forceinline__ uint32_t seg_final(uint32_t h, uint32_t O, uint32_t B) {
@@ -830,6 +823,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   }
   const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
   const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
+  asm volatile("" : "+v"(Wf));  // waited for here, not inside the walk
 
   // ---- the walk, from a PROBE state: the lane's incoming state is not known yet (it comes
   // from the look-back below, which this walk hides). Only the events before the lane's first
@@ -887,16 +881,20 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
             B = Bl;
             Bfo = Bfl;
           } else {
-            // Wf holds this head's word: loaded with the last head's for the first one, and
-            // prefetched at the previous head for the ones after it
-            const uint64_t w = Wf;
-            if (k + 1 < kFK && hs + 2 < hc) {  // another head before the last: prefetch it
-              const uint32_t kn = k + 1 + (uint32_t)__builtin_ctz(hm >> (k + 1 < kFK ? k + 1 : 0));
-              const uint32_t pn = tr[fold_slot(kFK * lane + kn)] >> 4;
-              Wf = pn < n_pages ? pt[pn] : 0ull;
+            // the first head's word was loaded (and waited for) with the last head's, before the
+            // walk; a middle head (lanes with >= 3 heads) loads its word here. A word prefetched
+            // one head ahead instead made every head step wait: the wave's one vmcnt counter also
+            // counts the walk's stores, and some lane is at a head at most steps.
+            if (hs != 0) {
+              const uint32_t pg = x >> 4;  // a page >= n_pages fails the batch (clamped load)
+              const uint64_t w = pt[pg < n_pages ? pg : 0u];
+              B = (uint32_t)w & 0x7FFFFu;
+              Bfo = (uint32_t)(w >> 32);
+              asm volatile("" : "+v"(B), "+v"(Bfo));  // the wait stays on this path
+            } else {
+              B = (uint32_t)Wf & 0x7FFFFu;
+              Bfo = (uint32_t)(Wf >> 32);
             }
-            B = (uint32_t)w & 0x7FFFFu;
-            Bfo = (uint32_t)(w >> 32);
             H = hit_seed(B);
             O = ((B >> 8) & 0xFFu) << 1;
           }
@@ -904,17 +902,18 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
           local = true;
           ++hs;
         }
-        const uint32_t bi = x & 15u, xn2 = x & 14u;
-        const bool wr = bi != xn2;
+        const uint32_t xn2 = x & 14u, nd = xn2 >> 1, rw = x & 1u;
+        const bool wr = rw != 0u;
+        const uint32_t bi = nd + (rw << 3);
         const uint32_t hitv = __builtin_amdgcn_ubfe(H, bi, 1u);
         const bool hit = hitv != 0;
         const uint32_t miss = hitv ^ 1u;
-        const uint32_t m = 1u << xn2;
+        const uint32_t m = 1u << nd;
         const uint32_t sel = (wr && !hit) ? (H & kHRead & ~m) : 0u;
         asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(inv) : "v"(sel), "v"(inv));
         xfer += (wr && O != xn2) ? 1u : 0u;  // a write by a non-owner always faults
         const uint32_t Hr = hit ? H : ((H | m) & kKr);
-        H = wr ? ((3u << xn2) | (kHE | kHW)) : Hr;
+        H = wr ? ((0x101u << nd) | (kHE | kHW)) : Hr;
         O = wr ? xn2 : O;
         asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(F[k / 8]) : "v"(miss), "v"(2u * xn2), "v"(F[k / 8]));
         T += miss;
