@@ -744,12 +744,39 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   // re-fetched every line from L2 once per instruction.)
   uint32_t hib = 0;
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  uint32_t eagg = 0;
+  bool early = false;
   if (kVec && kFull) {
+    uint32_t e0 = 0, e1 = 0;  // events 1920 + 2 * lane and the one after it
 #pragma unroll
     for (uint32_t q = 0; q < kFBlock / 128; ++q) {
       const uint4 v = ld_nt16(ev + lo + 128 * q + 2 * lane);
       hib |= v.y | v.w;
       *reinterpret_cast<u32x2*>(tr + fold_slot(128 * q + 2 * lane)) = (u32x2){v.x, v.z};
+      if (q == kFBlock / 128 - 1) {
+        e0 = v.x;
+        e1 = v.z;
+      }
+    }
+    // ---- early aggregate: when the block's last 128 events hold a write W and no head follows
+    // it (W's page is the block's last page), the block's transform is CONST(W) then READ(the
+    // nodes that read after W). It is published before the walk (below), so successors do not
+    // wait for this wave's walk; the walk's own aggregate is checked against it.
+    const uint64_t bw = __ballot(((e0 | e1) & 1u) != 0);
+    if (kM == 0 && b > 0 && bw) {
+      const uint32_t Lw = 63u - (uint32_t)__builtin_clzll(bw);
+      const uint32_t y1 = lane_bcast(e1, (int)Lw);
+      const uint32_t xw = (y1 & 1u) ? y1 : lane_bcast(e0, (int)Lw);
+      const uint32_t wi = 2u * Lw + (y1 & 1u);
+      if ((xw >> 4) == (lane_bcast(e1, 63) >> 4)) {
+        const uint32_t r = (2u * lane > wi ? 1u << ((e0 >> 1) & 7u) : 0u) |
+                           (2u * lane + 1u > wi ? 1u << ((e1 >> 1) & 7u) : 0u);
+        uint32_t R = 0;
+#pragma unroll
+        for (uint32_t nd = 0; nd < 8; ++nd) R |= __ballot((r >> nd) & 1u) ? 1u << nd : 0u;
+        eagg = tcompose(kConst | wr_word(xw), R);
+        early = true;
+      }
     }
   } else {
 #pragma unroll 8
@@ -824,6 +851,16 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
   const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
   asm volatile("" : "+v"(Wf));  // waited for here, not inside the walk
+  // Early publication (see above): the words of every lane's first and last heads have landed
+  // (the wave's last head's word is the only one another wave may store), so the head flag goes
+  // out with it and ordered successors need not wait for this walk either.
+  if (early) {
+    asm volatile("" ::"v"(Bl) : "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): only the loads above are in flight here
+    if (lane == 0)
+      __hip_atomic_store(status + b, kFAgg | (__ballot(hc != 0) ? kFHead : 0ull) | eagg,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   // ---- the walk, from a PROBE state: the lane's incoming state is not known yet (it comes
   // from the look-back below, which this walk hides). Only the events before the lane's first
@@ -940,12 +977,15 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   const uint32_t inc = wave_incl_compose_dpp(a);
   const uint32_t agg = lane_bcast(inc, 63);
   const bool whead = __ballot(hc != 0) != 0;
+  if (early && agg != eagg) bad = 1;  // never expected
   // every load of this wave has landed before its status is visible (see above). (Waiting only
   // for the last head's word, not for the walk's stores, measured the same: the wave's tail then
   // waits for them instead.)
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane == 0)
+  if (!early) {  // (an early publication went out after its loads already)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  }
+  if (lane == 0 && !early)
     __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (whead ? kFHead : 0ull) | agg,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // Only a wave that stores the state of a segment opened before it (its first segment ends
