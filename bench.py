@@ -10,9 +10,11 @@ gdsm_exchange ships them over RCCL (xGMI) and applies them at the homes
 run on a second stream while k+1 is diffed) and, after the first release has fixed every
 stream's byte budget, never synchronise the host. Every step is complete when the clock stops.
 
-Workloads: N = 1 (default): BASELINE.json configs[1], 1M x 4 KiB pages, 1 % random 8-byte word
-writes. N > 1 (default): configs[2], 16M pages in all (64 GiB), clustered 10 % writes,
-page-sharded over the N GPUs: strong scaling. `--scaling weak` keeps 1M pages per GPU instead.
+Workloads (`--config`): the default at EVERY N is the north_star target, 16M x 4 KiB pages in all
+(64 GiB per copy) with 1 % random 8-byte word writes, strong-scaled: N = 1 holds all 16M pages
+on one GPU (three arenas, 192 GiB), N > 1 holds 16M/N per GPU, so the driver's N = 1..8 lines
+are one workload. `--config 2` is BASELINE configs[1] (1M pages per GPU, 1 % words, weak);
+`--config 3` is configs[2] (16M pages in all, clustered 10 %, strong).
 Synthetic inputs (SPEC §6), resident in HBM before the timed region.
 
 Prints ONE JSON line on rank 0 (contract in the task statement); everything else -> stderr.
@@ -44,14 +46,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pages", type=int, default=1 << 20, help="pages per GPU (weak scaling)")
-    ap.add_argument("--total-pages", type=int, default=None,
-                    help="pages in all (strong scaling; default 16M for N > 1: configs[2])")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
-                    help="default: weak (1M pages) on one GPU, strong (16M in all) for N > 1")
-    ap.add_argument("--mode", choices=["uniform", "clustered"], default=None,
-                    help="default: uniform 1 %% words (configs[1]); clustered 10 %% (configs[2]) "
-                         "for strong scaling over N > 1 GPUs")
+    ap.add_argument("--config", choices=["northstar", "2", "3"], default="northstar",
+                    help="northstar (default): 16M pages in all, 1 %% word writes, strong scaling "
+                         "at every N; 2: BASELINE configs[1], 1M pages per GPU, 1 %% words, weak; "
+                         "3: configs[2], 16M pages in all, clustered 10 %%, strong")
+    ap.add_argument("--pages", type=int, default=None, help="pages per GPU (weak scaling)")
+    ap.add_argument("--total-pages", type=int, default=None, help="pages in all (strong scaling)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
+    ap.add_argument("--mode", choices=["uniform", "clustered"], default=None)
     ap.add_argument("--ppm", type=int, default=None, help="write density in parts per million")
     ap.add_argument("--seed", type=int, default=2026)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -92,6 +94,50 @@ def payload_bytes(rec_off: np.ndarray, data: np.ndarray) -> int:
     first_hdr = np.repeat(starts + 1, nr)
     within = np.arange(nr.sum()) - np.repeat(np.cumsum(nr) - nr, nr)
     return int((w[first_hdr + within] >> 16).astype(np.int64).sum())
+
+
+CONFIGS = {  # --config -> (scaling, mode, ppm, pages: in all when strong, per GPU when weak)
+    "northstar": ("strong", "uniform", 10000, 16 << 20),
+    "2": ("weak", "uniform", 10000, 1 << 20),
+    "3": ("strong", "clustered", 100000, 16 << 20),
+}
+
+
+def workload_shape(args, world: int):
+    """(scaling, mode name, ppm, pages per GPU) of the pages workload: --config, then overrides."""
+    scaling, mode_name, ppm, pages = CONFIGS[args.config]
+    scaling = args.scaling or scaling
+    mode_name = args.mode or mode_name
+    if args.mode and args.ppm is None:
+        ppm = 10000 if mode_name == "uniform" else 100000
+    ppm = args.ppm if args.ppm is not None else ppm
+    if scaling == "strong":
+        total = args.total_pages or (args.pages * world if args.pages else pages)
+        if total % (world * world):
+            raise SystemExit("the total page count must be a multiple of GPUs^2")
+        return scaling, mode_name, ppm, total // world
+    n = args.pages or (args.total_pages // world if args.total_pages else pages)
+    if n % world:
+        raise SystemExit("--pages must be a multiple of the GPU count")
+    return scaling, mode_name, ppm, n
+
+
+def efficiency_ref(pages_total: int, mode: str, ppm: int):
+    """The same workload's N = 1 line committed under profiles/ (newest first): (ms_per_step,
+    file name), or (None, None). Parallel efficiency at N is ref_ms / (N * ms_per_step_N)."""
+    for p in sorted((ROOT / "profiles").glob("*bench*n1*.json"), reverse=True):
+        try:
+            j = json.loads(p.read_text().strip().splitlines()[-1])
+        except Exception:  # noqa: BLE001
+            continue
+        c = j.get("config", {})
+        if (j.get("n_gpus") == 1 and c.get("total_pages") == pages_total
+                and c.get("mode") == mode and c.get("ppm") == ppm):
+            return j.get("ms_per_step"), p.name
+    return None, None
+
+
+XGMI_LINK_GBS = 153.0  # per xGMI link, one direction (MI355X_MICROARCH.md); 7 links per GPU
 
 
 def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
@@ -207,7 +253,7 @@ def run_coherence(args):
     dt = time.perf_counter() - t0
     prof = ctx.prof_read()
     totals = tot_dev.download(np.uint64, 10)
-    main_ms = prof["coh_apply"][0] / max(1, prof["coh_apply"][1])
+    main_ms = prof["coh_fold"][0] / max(1, prof["coh_fold"][1])
     alg = ev.count * 8 + touched * 16  # events read + state/faults words read and written
     achieved = alg / (main_ms * 1e-3) / 1e9
     traffic, traffic_src = read_coh_traffic(args.dist, n, E)
@@ -454,21 +500,8 @@ def main():
     import gallocy_amd as ga
     from gallocy_amd import exchange
 
-    # N = 1: BASELINE configs[1] (1M pages, 1 % word writes). N > 1: configs[2] by default: 16M
-    # pages in all, clustered 10 %, page-sharded over the N GPUs (strong scaling).
-    scaling = args.scaling or ("strong" if world > 1 else "weak")
-    mode_name = args.mode or ("clustered" if scaling == "strong" and world > 1 else "uniform")
+    scaling, mode_name, ppm, n = workload_shape(args, world)
     mode = ga.GEN_UNIFORM if mode_name == "uniform" else ga.GEN_CLUSTERED
-    ppm = args.ppm if args.ppm is not None else (10000 if mode == ga.GEN_UNIFORM else 100000)
-    if scaling == "strong":
-        total_pages = args.total_pages if args.total_pages else (16 << 20 if world > 1 else args.pages)
-        if total_pages % (world * world):
-            raise SystemExit("--total-pages must be a multiple of GPUs^2")
-        n = total_pages // world
-    else:
-        n = args.pages
-        if n % world:
-            raise SystemExit("--pages must be a multiple of the GPU count")
     ctx = ga.Context(n, device=local)
     # writer(p) = p mod G, home(p) = p // n (gallocy_amd/exchange.py); N = 1 is the identity
     ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank, stride=world,
@@ -591,6 +624,29 @@ def main():
     value = world * n * args.steps / dt
     traffic, traffic_src = read_traffic(n, mode_name, ppm, fused)
 
+    # per-stage time per step, max over ranks (HIP events on the stream each stage runs on)
+    stage_ms = {k: prof[k][0] / args.steps for k in ("diff", "exchange", "apply")}
+    if world > 1:
+        t = torch.tensor([stage_ms[k] for k in ("diff", "exchange", "apply")], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        stage_ms = dict(zip(("diff", "exchange", "apply"), t.tolist()))
+    xgmi = None
+    if shard is not None and stage_ms["exchange"] > 0:
+        moved = shard.moved_remote  # bytes this rank's exchange hands the transport per step
+        ach = moved / (stage_ms["exchange"] * 1e-3) / 1e9
+        peak_node, peak_used = 7 * XGMI_LINK_GBS, (world - 1) * XGMI_LINK_GBS
+        xgmi = {"bound": "xgmi", "achieved": round(ach, 2), "unit": "GB/s",
+                "peak": peak_node, "frac": round(ach / peak_node, 4),
+                "peak_links_used": peak_used, "frac_links_used": round(ach / peak_used, 4),
+                "bytes_per_step": int(moved),
+                "exchange_ms_per_step": round(stage_ms["exchange"], 4),
+                "note": "bytes one rank sends to its N-1 peers per step (rec_off + page indices + "
+                        "the byte budget of each stream) / the RCCL group's time on the exchange "
+                        "stream (HIP events; it includes waiting for the peers' diffs, so it is a "
+                        "lower bound on the link rate). peak: 7 links x 153 GB/s (all of an "
+                        "MI355X's xGMI); peak_links_used: the N-1 links one rank's peers use"}
+    ref_ms, ref_src = efficiency_ref(world * n, mode_name, ppm) if world > 1 else (None, None)
+
     if rank == 0:
         stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
                   for k, v in prof.items() if v[1]}
@@ -615,7 +671,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (counter-hash pages, docs/SPEC.md §6)",
-            "config": {"workload": workload, "pages_per_gpu": n, "total_pages": world * n,
+            "config": {"workload": workload, "config": args.config, "mode": mode_name,
+                       "ppm": ppm, "pages_per_gpu": n, "total_pages": world * n,
                        "seed": args.seed, "parallelism": f"page-shard x{world}",
                        "diff_bytes_per_step": int(total), "payload_bytes_per_step": int(pay),
                        **({"backend": "gloo (REHEARSAL, not a measurement)"}
@@ -632,10 +689,15 @@ def main():
                          "algorithmic_bytes_per_launch": int(diff_bytes),
                          "avg_launch_ms": round(avg_diff_ms, 4)},
             "stages": stages,
+            "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "exchange": None if shard is None else {
                 "transport": shard.transport, "fixed_budgets": bool(shard.flags),
+                "recoveries": shard.recoveries,
                 "sent_remote_bytes_per_step": shard.sent_remote,
                 "received_bytes_per_step": shard.received},
+            **({"roofline_xgmi": xgmi} if xgmi else {}),
+            **({"efficiency_ref_ms": ref_ms, "efficiency_ref_source": ref_src}
+               if world > 1 else {}),
             "replica_equals_current": bool(replica_ok),
             "cpu_baseline": None,
         }

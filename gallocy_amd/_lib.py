@@ -104,6 +104,11 @@ SIGNATURES = {
     "gdsm_comm_init": (C.c_int, [C.POINTER(vp), vp, C.c_int, C.c_int, vp]),
     "gdsm_comm_fini": (C.c_int, [vp]),
     "gdsm_comm_size": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "gdsm_comm_init_loopback": (C.c_int, [C.POINTER(vp), C.POINTER(vp), C.c_int]),
+    "gdsm_comm_agree": (C.c_int, [vp, vp, u64p]),
+    "gdsm_route_events": (C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint64, vp, C.c_uint64, u64p]),
+    "gdsm_coherence_notify": (C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint64, vp, vp, C.c_uint64,
+                                        u64p]),
     "gdsm_exchange": (C.c_int, [vp, vp, C.POINTER(GdsmRuns), C.POINTER(vp), C.POINTER(GdsmRuns),
                                 C.POINTER(vp), C.c_int, C.c_uint32]),
 }

@@ -17,7 +17,7 @@ CSRC = PKG / "csrc"
 LIBDIR = PKG / "lib"
 LIB = LIBDIR / "libgdsm.so"
 SOURCES = ["gdsm_pages.hip", "gdsm_coherence.hip", "gdsm_capi.cpp", "legacy_diff.cpp",
-           "gdsm_track.cpp", "gdsm_nw.hip", "gdsm_wire.hip", "gdsm_exchange.cpp"]
+           "gdsm_track.cpp", "gdsm_nw.hip", "gdsm_wire.hip", "gdsm_exchange.cpp", "gdsm_route.hip"]
 HEADERS = ["gdsm_common.h", "gdsm_launch.h", "gdsm_prof.h", "gdsm_track.h", "gdsm_ctx.h"]
 ARCH = os.environ.get("GDSM_ARCH", "gfx950")
 

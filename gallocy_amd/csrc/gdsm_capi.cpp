@@ -49,13 +49,11 @@ int ensure_aux(gdsm_ctx* ctx) {
   return 0;
 }
 
-// Contexts with a graph capture open (gdsm_capture_begin): workspaces may not move under a
-// capture, since the recorded kernels keep their addresses.
-std::atomic<int> g_capturing{0};
-
-int ensure(uint8_t** buf, uint64_t* have, uint64_t need) {
+// A context whose calls are being recorded (gdsm_capture_begin / _join) may not move its
+// workspaces, since the recorded kernels keep their addresses; other contexts are unaffected.
+int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need) {
   if (*have >= need) return 0;
-  if (g_capturing.load()) return -EBUSY;  // size workspaces with gdsm_reserve before capturing
+  if (ctx && ctx->capturing) return -EBUSY;  // size workspaces with gdsm_reserve before capturing
   if (*buf) (void)hipFree(*buf);
   *buf = nullptr;
   *have = 0;
@@ -70,7 +68,7 @@ int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const ui
   *out = ids;
   if (!ids || n == 0) return 0;
   uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[which]);
-  int rc = ensure(&buf, &ctx->ids_safe_bytes[which], 4 * n);
+  int rc = ensure(ctx, &buf, &ctx->ids_safe_bytes[which], 4 * n);
   ctx->ids_safe[which] = reinterpret_cast<uint32_t*>(buf);
   if (rc) return rc;
   GDSM_TRY(gdsm::launch_check_ids(ids, n, ctx->n_pages, ctx->ids_safe[which], ctx->err,
@@ -85,6 +83,9 @@ int check_and_clear_err(gdsm_ctx* ctx) {
   GDSM_TRY(hipMemsetAsync(ctx->err, 0, 4, ctx->stream));
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   if (h && getenv("GDSM_DEBUG_ERR")) fprintf(stderr, "gdsm err word 0x%x\n", h);
+  // a fixed-budget exchange stream over its budget, and nothing else: the release can be redone
+  // with exact sizes (gdsm.h GDSM_XCHG_FIXED)
+  if (h == kErrOverBudget) return -EOVERFLOW;
   return h ? -EINVAL : 0;
 }
 
@@ -113,7 +114,7 @@ int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* id
     GDSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->track_host), bytes));
     ctx->track_host_bytes = bytes;
   }
-  rc = ensure(&ctx->track_dev, &ctx->track_dev_bytes, bytes ? bytes : 1);
+  rc = ensure(ctx, &ctx->track_dev, &ctx->track_dev_bytes, bytes ? bytes : 1);
   if (rc) return rc;
   uint8_t* h_twin = ctx->track_host;
   uint8_t* h_cur = h_twin + n * GDSM_PAGE_SZ;
@@ -128,7 +129,7 @@ int gdsm_track_diff(gdsm_ctx* ctx, gdsm_tracker* t, gdsm_runs* out, uint32_t* id
     GDSM_TRY(hipMemcpyAsync(ids_dev, ctx->track_dev + 2 * n * GDSM_PAGE_SZ, n * sizeof(uint32_t),
                             hipMemcpyDeviceToDevice, ctx->stream));
   }
-  rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
+  rc = ensure(ctx, &ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
   if (rc) return rc;
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->track_dev, ctx->track_dev + n * GDSM_PAGE_SZ, nullptr, n,
@@ -264,7 +265,7 @@ int gdsm_capture_begin(gdsm_ctx* ctx) {
   if (g.rc) return g.rc;
   GDSM_TRY(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
   ctx->capturing = true;
-  ++g_capturing;
+  ctx->capture_origin = true;
   return 0;
 }
 
@@ -287,7 +288,8 @@ int gdsm_capture_join(gdsm_ctx* ctx, gdsm_ctx* other) {
 }
 
 int gdsm_capture_end(gdsm_ctx* ctx, gdsm_graph** out) {
-  if (!ctx || !out || !ctx->capturing) return -EINVAL;
+  // only the context that began the capture ends it (a joined one has no capture of its own)
+  if (!ctx || !out || !ctx->capturing || !ctx->capture_origin) return -EINVAL;
   DeviceGuard g(ctx->device);
   int rc = 0;
   for (gdsm_ctx* o : ctx->capture_joined) {  // the joined streams rejoin before the capture ends
@@ -302,7 +304,7 @@ int gdsm_capture_end(gdsm_ctx* ctx, gdsm_graph** out) {
   hipGraph_t graph = nullptr;
   const hipError_t ee = hipStreamEndCapture(ctx->stream, &graph);
   ctx->capturing = false;
-  --g_capturing;
+  ctx->capture_origin = false;
   for (hipEvent_t e : ctx->capture_events) (void)hipEventDestroy(e);
   ctx->capture_events.clear();
   ctx->capture_joined.clear();
@@ -373,16 +375,16 @@ int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events) {
   if (g.rc) return g.rc;
   int rc = 0;
   if (diff_pages) {
-    rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(diff_pages));
+    rc = ensure(ctx, &ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(diff_pages));
     // checked copies of the id lists of diff / twin / apply on the main stream
     if (!rc) {
       uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[0]);
-      rc = ensure(&buf, &ctx->ids_safe_bytes[0], 4 * diff_pages);
+      rc = ensure(ctx, &buf, &ctx->ids_safe_bytes[0], 4 * diff_pages);
       ctx->ids_safe[0] = reinterpret_cast<uint32_t*>(buf);
     }
   }
   if (!rc && coh_events)
-    rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(coh_events));
+    rc = ensure(ctx, &ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(coh_events));
   return rc;
 }
 
@@ -561,7 +563,7 @@ static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* 
   }
   auto busy = ctx->runs_busy.find(out->rec_off);
   if (busy != ctx->runs_busy.end()) GDSM_TRY(hipStreamWaitEvent(ctx->stream, busy->second, 0));
-  int rc = ensure(&ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
+  int rc = ensure(ctx, &ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
   if (!rc) rc = safe_ids(ctx, ids, n, 0, &ids);
   if (rc) return rc;
   out->n = n;
@@ -649,11 +651,19 @@ int gdsm_diff_apply_raw(const uint8_t* twin, const uint8_t* cur, uint8_t* target
 int gdsm_apply_raw(uint8_t* target, const uint32_t* ids, uint64_t n, const uint64_t* rec_off,
                    const uint8_t* data, uint32_t* err, void* stream) {
   if (!target || !rec_off || (!data && n)) return -EINVAL;
-  static uint32_t* sink = nullptr;  // unreported errors land here
+  // unreported errors land in a sink word on the stream's own device (one per device)
+  static std::map<int, uint32_t*> sinks;
   static std::mutex mu;
   if (!err) {
+    int dev = -1;
+    if (!stream || hipStreamGetDevice(static_cast<hipStream_t>(stream), &dev) != hipSuccess)
+      GDSM_TRY(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(mu);
-    if (!sink) GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&sink), 4));
+    uint32_t*& sink = sinks[dev];
+    if (!sink) {
+      DeviceGuard g(dev);
+      GDSM_TRY(hipMalloc(reinterpret_cast<void**>(&sink), 4));
+    }
     err = sink;
   }
   GDSM_TRY(gdsm::launch_apply(target, ids, n, rec_off, data, err,
@@ -690,7 +700,7 @@ int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n
   if (!ctx || !ctx->coh_pt || !totals_dev || (!events && n_events)) return -EINVAL;
   CtxGuard g(ctx);
   if (g.rc) return g.rc;
-  int rc = ensure(&ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
+  int rc = ensure(ctx, &ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
   if (rc) return rc;
   GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, ctx->n_nodes, events, n_events,
                                   totals_dev, ctx->coh_ws, ctx->coh_ws_bytes, ctx->err,
@@ -770,7 +780,7 @@ int gdsm_nw_diff_batch(gdsm_ctx* ctx, const uint8_t* a, const uint64_t* a_off, c
   uint64_t pairs = (4ull << 30) / per;
   if (pairs < 1) pairs = 1;
   if (pairs > n) pairs = n;
-  int rc = ensure(&ctx->nw_ws, &ctx->nw_ws_bytes, pairs * per);
+  int rc = ensure(ctx, &ctx->nw_ws, &ctx->nw_ws_bytes, pairs * per);
   if (rc) return rc;
   GDSM_TRY(gdsm::launch_nw(a, a_off, b, b_off, n, max_len, out1, out2, out_len, ctx->nw_ws,
                            pairs * per, ctx->err, ctx->stream, ctx->P()));
@@ -845,7 +855,7 @@ int wire_decode_frame(gdsm_ctx* ctx, const char* text, uint64_t len, uint64_t n_
   if (magic != kWireMagic || ver != 1 || flags != 0 || D % 4 || n >= (1ull << 32) ||
       D > F || gdsm::wire_frame_bytes(n, D) != F)
     return -EINVAL;
-  int rc = ensure(&ctx->wire_ws, &ctx->wire_ws_bytes, up16(T) + up16(F) + 16);
+  int rc = ensure(ctx, &ctx->wire_ws, &ctx->wire_ws_bytes, up16(T) + up16(F) + 16);
   if (rc) return rc;
   uint8_t* dtext = ctx->wire_ws;
   uint8_t* frame = dtext + up16(T);
@@ -888,7 +898,7 @@ int gdsm_wire_encode(gdsm_ctx* ctx, const uint32_t* ids, const gdsm_runs* runs, 
   const uint64_t T = 4 * ((F + 2) / 3);
   *len = kWirePrefixLen + T;
   if (cap < kWirePrefixLen + T + 1) return -ENOSPC;
-  int rc = ensure(&ctx->wire_ws, &ctx->wire_ws_bytes, up16(T) + up16(F) + 16);
+  int rc = ensure(ctx, &ctx->wire_ws, &ctx->wire_ws_bytes, up16(T) + up16(F) + 16);
   if (rc) return rc;
   uint8_t* dtext = ctx->wire_ws;
   uint8_t* frame = dtext + up16(T);
@@ -971,7 +981,7 @@ int nw_host(gdsm_ctx* ctx, const char* m1, size_t n1, const char* m2, size_t n2,
   auto up16 = [](uint64_t v) { return (v + 15) & ~15ull; };
   const uint64_t out_bytes = n1 + n2 + 1;
   const uint64_t need = up16(n1 + 1) + up16(n2 + 1) + 64 + 2 * up16(out_bytes) + 16;
-  int rc = ensure(&ctx->nw_stage, &ctx->nw_stage_bytes, need);
+  int rc = ensure(ctx, &ctx->nw_stage, &ctx->nw_stage_bytes, need);
   if (rc) return rc;
   uint8_t* da = ctx->nw_stage;
   uint8_t* db = da + up16(n1 + 1);

@@ -33,6 +33,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+
 namespace gdsm {
 
 constexpr uint32_t kConst = 1u << 31;
@@ -41,8 +43,8 @@ constexpr uint32_t kCohBlock = 256 * kCohK;     // events per block
 constexpr uint32_t kSamp = kCohBlock / 64;       // pass A: sampling stride over a block
 static_assert(kSamp <= 64, "pass A samples the block with one wave");
 constexpr uint32_t kCohGroup = 1024;            // blocks per scan group
-constexpr uint32_t kNoHead = 0xFFFFFFFFu;
-constexpr uint64_t kNoHead64 = ~0ull;
+[[maybe_unused]] constexpr uint32_t kNoHead = 0xFFFFFFFFu;
+[[maybe_unused]] constexpr uint64_t kNoHead64 = ~0ull;
 
 #ifdef GDSM_COH_STAMPS
 // Debug build only: per-wave phase time stamps (s_memtime) of every 64th block.
@@ -162,6 +164,9 @@ __global__ __launch_bounds__(256) void coh_init_kernel(uint64_t* __restrict__ pt
   }
 }
 
+#ifdef GDSM_MEASURE
+// The round-2 four-pass path (A, B, C below), kept for same-box A/B in measurement builds only
+// (coh_variant 1); the product library ships the single-pass fold (F) alone.
 // ---------------------------------------------------------------- A: block aggregates
 __global__ __launch_bounds__(256) void coh_tail_kernel(const uint64_t* __restrict__ pt,
                                                        uint64_t n_pages,
@@ -627,6 +632,8 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
   if (lane < 10) partial[(b * 4 + wave) * 10 + lane] = mine;
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
+
+#endif  // GDSM_MEASURE
 
 // ---------------------------------------------------------------- F: single-pass fold
 // One wave = one block of kFBlock events (kFK consecutive events per lane), no other pass before
@@ -1217,24 +1224,25 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 
 // ---------------------------------------------------------------- launchers
 // Coherence variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = the single-pass fold
-// (coh_fold_kernel, default); 1 = the round-2 four-pass path (tail aggregates, scan, block pass
-// C), kept for same-box A/B. Built with -DGDSM_MEASURE only (output invalid): 2 / 3 = the
-// four-pass path without page-table stores / without any page-table traffic; 4 / 5 / 6 = the
-// fold without its walk / without its look-back / without the ordered look-back.
+// (coh_fold_kernel), the only one in the product library. Measurement builds (-DGDSM_MEASURE,
+// scripts/build_measure.sh) add 1 = the round-2 four-pass path (tail aggregates, scan, block pass
+// C) for same-box A/B, and (output invalid) 2 / 3 = the four-pass path without page-table stores
+// / without any page-table traffic; 4 / 5 / 6 = the fold without its walk / without its
+// look-back / without the ordered look-back.
 #ifdef GDSM_MEASURE
 constexpr int kCohVariants = 7;
 #else
-constexpr int kCohVariants = 2;
+constexpr int kCohVariants = 1;
 #endif
 static int coh_variant_from_env() {
   const char* e = getenv("GDSM_COH_VARIANT");
   const int v = e ? atoi(e) : 0;
   return (v >= 0 && v < kCohVariants) ? v : 0;
 }
-static int g_coh_variant = coh_variant_from_env();
+static std::atomic<int> g_coh_variant{coh_variant_from_env()};
 int coh_tune(const char* key, int64_t value) {
   if (!strcmp(key, "coh_variant") && value >= 0 && value < kCohVariants) {
-    g_coh_variant = (int)value;
+    g_coh_variant.store((int)value, std::memory_order_relaxed);
     return 0;
   }
   return -1;
@@ -1268,18 +1276,18 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                             const uint64_t* events, uint64_t n_events, uint64_t* totals,
                             uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
                             Prof* prof) {
+  const int cv = g_coh_variant.load(std::memory_order_relaxed);
   hipError_t r = hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
   if (r != hipSuccess || n_events == 0) return r;
-  const uint64_t nb = coh_blocks(n_events), ng = coh_groups(nb);
   if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
-  if (g_coh_variant == 0 || g_coh_variant >= 4) {
+  if (cv == 0 || cv >= 4) {
     const uint64_t nf = fold_blocks(n_events);
     uint64_t* fws = reinterpret_cast<uint64_t*>(ws);
     uint32_t* fpart = reinterpret_cast<uint32_t*>(fws + kFoldStatus + nf);
     r = hipMemsetAsync(fws, 0, 8 * (kFoldStatus + nf), s);  // tickets + status granules
     if (r != hipSuccess) return r;
     {
-      ProfScope ps(prof, 7, s);
+      ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
       const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
       const bool nodes = n_nodes < 8;
       const uint64_t full = n_events / kFBlock;
@@ -1287,9 +1295,9 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
         auto kern = vec ? (nodes ? coh_fold_kernel<true, true, true> : coh_fold_kernel<true, true, false>)
                         : (nodes ? coh_fold_kernel<false, true, true> : coh_fold_kernel<false, true, false>);
 #ifdef GDSM_MEASURE
-        if (vec && !nodes && g_coh_variant == 4) kern = coh_fold_kernel<true, true, false, 1>;
-        if (vec && !nodes && g_coh_variant == 5) kern = coh_fold_kernel<true, true, false, 2>;
-        if (vec && !nodes && g_coh_variant == 6) kern = coh_fold_kernel<true, true, false, 3>;
+        if (vec && !nodes && cv == 4) kern = coh_fold_kernel<true, true, false, 1>;
+        if (vec && !nodes && cv == 5) kern = coh_fold_kernel<true, true, false, 2>;
+        if (vec && !nodes && cv == 6) kern = coh_fold_kernel<true, true, false, 3>;
 #endif
         hipLaunchKernelGGL(kern, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
                            events, n_events, full, fws, fpart, err, n_nodes);
@@ -1302,11 +1310,13 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
     }
     uint64_t g = (nf + 255) / 256;
     if (g > 1024) g = 1024;
-    ProfScope ps(prof, 8, s);
+    ProfScope ps(prof, GDSM_PROF_COH_REDUCE, s);
     hipLaunchKernelGGL(coh_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, fpart, nf,
                        reinterpret_cast<unsigned long long*>(totals));
     return hipGetLastError();
   }
+#ifdef GDSM_MEASURE
+  const uint64_t nb = coh_blocks(n_events), ng = coh_groups(nb);
   uint64_t* head_pt = reinterpret_cast<uint64_t*>(ws);
   uint32_t* agg = reinterpret_cast<uint32_t*>(head_pt + nb);
   uint32_t* lh = agg + nb;
@@ -1314,24 +1324,24 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   uint32_t* partial = carry + nb;
   uint32_t* groups = partial + nb * 40;
   {
-    ProfScope ps(prof, 5, s);
+    ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
     hipLaunchKernelGGL(coh_tail_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, pt,
                        n_pages, events, n_events, nb, agg, lh, head_pt);
   }
   {
-    ProfScope ps(prof, 6, s);
+    ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
     hipLaunchKernelGGL(coh_group_kernel, dim3((unsigned)ng), dim3(256), 0, s, agg, nb, groups);
     hipLaunchKernelGGL(coh_top_kernel, dim3(1), dim3(1024), 0, s, groups, ng);
     hipLaunchKernelGGL(coh_rescan_kernel, dim3((unsigned)ng), dim3(256), 0, s, agg, nb, groups,
                        carry);
   }
   {
-    ProfScope ps(prof, 7, s);
+    ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
     const bool vec = (reinterpret_cast<uintptr_t>(events) & 15) == 0;
 #ifdef GDSM_MEASURE
     auto kern = !vec                 ? coh_apply_block_kernel<0, false>
-                : g_coh_variant == 2 ? coh_apply_block_kernel<1, true>
-                : g_coh_variant == 3 ? coh_apply_block_kernel<2, true>
+                : cv == 2 ? coh_apply_block_kernel<1, true>
+                : cv == 3 ? coh_apply_block_kernel<2, true>
                                      : coh_apply_block_kernel<0, true>;
 #else
     auto kern = vec ? coh_apply_block_kernel<0, true> : coh_apply_block_kernel<0, false>;
@@ -1343,11 +1353,14 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   uint64_t g = (rows + 255) / 256;
   if (g > 1024) g = 1024;
   {
-    ProfScope ps(prof, 8, s);
+    ProfScope ps(prof, GDSM_PROF_COH_REDUCE, s);
     hipLaunchKernelGGL(coh_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, partial, rows,
                        reinterpret_cast<unsigned long long*>(totals));
   }
   return hipGetLastError();
+#else
+  return hipErrorInvalidValue;  // unreachable: coh_variant is 0 outside measurement builds
+#endif
 }
 
 hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,

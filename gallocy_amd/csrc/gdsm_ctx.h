@@ -55,6 +55,7 @@ struct gdsm_ctx {
   uint64_t ids_safe_bytes[2] = {0, 0};
   // graph capture (gdsm_capture_*): open on this context's stream (or joined into another's)
   bool capturing = false;
+  bool capture_origin = false;  // this context began the capture (only it may end it)
   std::vector<gdsm_ctx*> capture_joined;
   std::vector<hipEvent_t> capture_events;
 };
@@ -62,9 +63,18 @@ struct gdsm_ctx {
 namespace gdsm {
 namespace detail {
 
+// Bits of the device error word (gdsm_ctx::err).
+constexpr uint32_t kErrRecord = 1;       // malformed record (apply)
+constexpr uint32_t kErrEvents = 2;       // coherence batch not sorted / out of range
+constexpr uint32_t kErrNw = 4;           // GPU NW input out of range
+constexpr uint32_t kErrIds = 8;          // page id / index out of range
+constexpr uint32_t kErrStream = 16;      // exchanged stream with malformed offsets
+constexpr uint32_t kErrOverBudget = 32;  // fixed-budget exchanged stream over its budget
+
 int map_err(hipError_t e);
-// hipMalloc-backed buffer that only grows (contents are not kept).
-int ensure(uint8_t** buf, uint64_t* have, uint64_t need);
+// hipMalloc-backed buffer that only grows (contents are not kept); -EBUSY while ctx (the owner of
+// the buffer, or NULL) is recording a graph.
+int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need);
 // Makes ctx->stream wait for every pending operation on ctx->aux.
 int join_aux(gdsm_ctx* ctx);
 // Creates ctx->aux and its events on first use.

@@ -27,10 +27,16 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
 hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         const uint64_t* rec_off, const uint8_t* data, uint32_t* err,
                         hipStream_t s, Prof* prof = nullptr);
-// A received fixed-budget stream: zeroes rec_off (nothing applied) and err |= 4 unless
-// rec_off[0] == 0 and rec_off[n] <= cap.
-hipError_t launch_guard_stream(uint64_t* rec_off, uint64_t n, uint64_t cap, uint32_t* err,
-                               hipStream_t s);
+// A stream about to be applied by gdsm_exchange: checked whole (offsets from 0, non-decreasing,
+// 4-aligned, rec_off[n] <= budget; page indices < n_pages, copied to safe[n]). A rejected stream
+// has every offset zeroed (nothing applied); err |= 16 (malformed offsets), 32 (over budget),
+// 8 (bad page index). `verdict` is one device word of scratch.
+hipError_t launch_xchg_guard(uint64_t* rec_off, const uint32_t* ids, uint64_t n, uint64_t budget,
+                             uint64_t n_pages, uint32_t* safe, uint32_t* verdict, uint32_t* err,
+                             hipStream_t s);
+// err |= 32 when rec_off[n] > budget (a fixed-budget stream its sender shipped over budget).
+hipError_t launch_budget_check(const uint64_t* rec_off, uint64_t n, uint64_t budget,
+                               uint32_t* err, hipStream_t s);
 // Caller page-id lists at the context level: safe[i] = ids[i] if < n_pages, else n_pages (the
 // arenas' guard page), and err |= 8 when any id was out of range.
 hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, uint32_t* safe,
@@ -48,6 +54,27 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
 hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,
                              uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,
                              hipStream_t s);
+
+// Coherence across GPUs (SPEC §5b; gdsm_route.hip).
+// A node's stamped events: validation (bad |= 1), per-home bounds[G+1] and counts[G] (u64).
+hipError_t launch_route_split(const uint64_t* ev, uint64_t n, uint64_t total_pages, uint64_t per,
+                              uint32_t G, uint64_t* counts, uint64_t* bounds, uint32_t* bad,
+                              hipStream_t s);
+// G sorted runs (host offsets off[G+1] into `runs`) merged into one page-sorted local batch.
+hipError_t launch_route_merge(const uint64_t* runs, const uint64_t* off, uint32_t G, uint64_t base,
+                              uint64_t* out, hipStream_t s);
+uint64_t notice_blocks(uint64_t n);
+hipError_t launch_notice_pre(const uint64_t* pt, uint64_t n_pages, const uint64_t* batch,
+                             uint64_t n, uint32_t* pre, hipStream_t s);
+// blk: notice_blocks(n) x 8 u32; blk_off the same in u64; dest_total / dest_base: G u64 each.
+hipError_t launch_notice_count(const uint64_t* pt, uint64_t n_pages, const uint64_t* batch,
+                               uint64_t n, const uint32_t* pre, uint32_t G, uint32_t* blk,
+                               uint64_t* blk_off, uint64_t* dest_total, uint64_t* dest_base,
+                               hipStream_t s);
+hipError_t launch_notice_emit(const uint64_t* pt, uint64_t n_pages, const uint64_t* batch,
+                              uint64_t n, const uint32_t* pre, uint32_t G, uint64_t base,
+                              const uint64_t* blk_off, const uint64_t* dest_base, uint64_t* out,
+                              hipStream_t s);
 
 // GPU NW alignment (legacy diff()): workspace per pair and the fill + trace launches.
 uint64_t nw_pair_ws_bytes(uint32_t max_len);

@@ -293,14 +293,14 @@ hipError_t launch_nw(const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
     uint32_t* rowbuf = reinterpret_cast<uint32_t*>(ws + cnt * recs * 16);
     uint8_t* mv = reinterpret_cast<uint8_t*>(rowbuf + cnt * 2 * ((uint64_t)max_len + 64));
     {
-      ProfScope ps(prof, 9, s);
+      ProfScope ps(prof, GDSM_PROF_NW_FILL, s);
       hipLaunchKernelGGL(nw_fill_kernel, dim3((uint32_t)cnt), dim3(64 * kWaves), 0, s, a, a_off,
                          b, b_off, first, max_len, NB, recs, tb, rowbuf, err);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     {
-      ProfScope ps(prof, 10, s);
+      ProfScope ps(prof, GDSM_PROF_NW_TRACE, s);
       hipLaunchKernelGGL(nw_trace_kernel, dim3((uint32_t)cnt), dim3(64), 0, s, a, a_off, b,
                          b_off, first, max_len, NB, recs, tb, mv, out1, out2, out_len);
     }

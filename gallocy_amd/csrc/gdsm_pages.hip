@@ -17,6 +17,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+
 namespace gdsm {
 
 // ------------------------------------------------------------------------- synthetic pages
@@ -96,20 +98,61 @@ __global__ __launch_bounds__(256) void check_ids_kernel(const uint32_t* __restri
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(err, 8u);
 }
 
-// ------------------------------------------------------------------------- received streams
-// A stream received with a fixed byte budget (gdsm_exchange GDSM_XCHG_FIXED) is applied only if
-// it is well-formed at its ends: rec_off[0] == 0 and rec_off[n] <= cap (the bytes past rec_off[n]
-// are the sender's padding). Otherwise every offset is zeroed (all records empty: the apply
-// writes nothing) and err |= 4.
-__global__ __launch_bounds__(256) void guard_stream_kernel(uint64_t* __restrict__ rec_off,
-                                                           uint64_t n, uint64_t cap,
-                                                           uint32_t* __restrict__ err) {
-  const bool bad = rec_off[0] != 0 || rec_off[n] > cap || (rec_off[n] & 3u);
-  if (!bad) return;  // uniform: every thread read the same two words
+// ------------------------------------------------------------------------- exchanged streams
+// Every stream gdsm_exchange applies (received ones and the rank's own) is checked whole before
+// the apply: rec_off[0] == 0, offsets non-decreasing and 4-aligned, rec_off[n] <= budget, and
+// every page index < n_pages (copied to `safe`). Two launches, so no block ever judges a stream
+// another block has already zeroed: the check ORs its verdict into one word (bit 0 malformed
+// offsets, bit 1 over budget, bit 2 bad page index) and the err word (16 / 32 / 8); the zeroing
+// pass then empties every record of a rejected stream, so the apply writes nothing of it.
+__global__ __launch_bounds__(256) void xchg_check_kernel(const uint64_t* __restrict__ rec_off,
+                                                         const uint32_t* __restrict__ ids,
+                                                         uint64_t n, uint64_t budget,
+                                                         uint64_t n_pages,
+                                                         uint32_t* __restrict__ safe,
+                                                         uint32_t* __restrict__ verdict,
+                                                         uint32_t* __restrict__ err) {
+  uint32_t v = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t o = rec_off[i];
+    if (o & 3u) v |= 1u;
+    if (i == 0 && o != 0) v |= 1u;
+    if (i < n) {
+      if (rec_off[i + 1] < o) v |= 1u;
+      const uint32_t p = ids[i];
+      const bool ok = p < n_pages;
+      safe[i] = ok ? p : (uint32_t)n_pages;
+      if (!ok) v |= 4u;
+    } else if (o > budget) {
+      v |= 2u;
+    }
+  }
+  // one atomic per wave that found something
+  const uint64_t any = __ballot(v != 0);
+  if (any) {
+    uint32_t w = v;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) w |= __shfl_xor(w, d, 64);
+    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(any)) {
+      atomicOr(verdict, w);
+      atomicOr(err, ((w & 1u) ? 16u : 0u) | ((w & 2u) ? 32u : 0u) | ((w & 4u) ? 8u : 0u));
+    }
+  }
+}
+
+// The sender's view of a stream it shipped with a fixed budget: err |= 32 if it did not fit.
+__global__ void budget_check_kernel(const uint64_t* __restrict__ rec_off, uint64_t n,
+                                    uint64_t budget, uint32_t* __restrict__ err) {
+  if (threadIdx.x == 0 && rec_off[n] > budget) atomicOr(err, 32u);
+}
+
+__global__ __launch_bounds__(256) void xchg_zero_kernel(uint64_t* __restrict__ rec_off, uint64_t n,
+                                                        const uint32_t* __restrict__ verdict) {
+  if (*verdict == 0) return;  // written by the previous launch: every block reads the same word
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n;
        i += (uint64_t)gridDim.x * blockDim.x)
     rec_off[i] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 4u);
 }
 
 // ------------------------------------------------------------------------- diff (SPEC §3)
@@ -776,18 +819,17 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
 //   3  2 pages per wave
 //   4  64 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 // Measurement-only kernels (invalid output) are not part of the library.
-static int g_diff_variant = -1;
-static int diff_variant() {
-  if (g_diff_variant < 0) {
-    const char* e = getenv("GDSM_DIFF_VARIANT");
-    const int v = e ? atoi(e) : 0;
-    g_diff_variant = (v >= 0 && v <= 4) ? v : 0;
-  }
-  return g_diff_variant;
+// Process-wide and atomic: a launch on any thread reads one consistent value.
+static int diff_variant_from_env() {
+  const char* e = getenv("GDSM_DIFF_VARIANT");
+  const int v = e ? atoi(e) : 0;
+  return (v >= 0 && v <= 4) ? v : 0;
 }
+static std::atomic<int> g_diff_variant{diff_variant_from_env()};
+static int diff_variant() { return g_diff_variant.load(std::memory_order_relaxed); }
 int tune(const char* key, int64_t value) {
   if (!strcmp(key, "diff_variant") && value >= 0 && value <= 4) {
-    g_diff_variant = (int)value;
+    g_diff_variant.store((int)value, std::memory_order_relaxed);
     return 0;
   }
   return coh_tune(key, value);
@@ -827,17 +869,28 @@ hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, u
   return hipGetLastError();
 }
 
-hipError_t launch_guard_stream(uint64_t* rec_off, uint64_t n, uint64_t cap, uint32_t* err,
-                               hipStream_t s) {
-  hipLaunchKernelGGL(guard_stream_kernel, dim3(grid_for(n + 1, 256, 1024)), dim3(256), 0, s,
-                     rec_off, n, cap, err);
+hipError_t launch_xchg_guard(uint64_t* rec_off, const uint32_t* ids, uint64_t n, uint64_t budget,
+                             uint64_t n_pages, uint32_t* safe, uint32_t* verdict, uint32_t* err,
+                             hipStream_t s) {
+  hipError_t e = hipMemsetAsync(verdict, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  const unsigned g = grid_for(n + 1, 256, 2048);
+  hipLaunchKernelGGL(xchg_check_kernel, dim3(g), dim3(256), 0, s, rec_off, ids, n, budget, n_pages,
+                     safe, verdict, err);
+  hipLaunchKernelGGL(xchg_zero_kernel, dim3(g), dim3(256), 0, s, rec_off, n, verdict);
+  return hipGetLastError();
+}
+
+hipError_t launch_budget_check(const uint64_t* rec_off, uint64_t n, uint64_t budget,
+                               uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(budget_check_kernel, dim3(1), dim3(64), 0, s, rec_off, n, budget, err);
   return hipGetLastError();
 }
 
 hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
-  ProfScope ps(prof, 4, s);
+  ProfScope ps(prof, GDSM_PROF_TWIN, s);
   hipLaunchKernelGGL(twin_kernel, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur, ids,
                      n);
   return hipGetLastError();
@@ -855,7 +908,7 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   // ticket counter + status granules, zeroed per launch (outside the timed kernel)
   hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
   if (e != hipSuccess) return e;
-  ProfScope ps(prof, 0, s);
+  ProfScope ps(prof, GDSM_PROF_DIFF, s);
   auto kern = target ? (v == 4   ? diff_single_kernel<64, 8192, 4, true>
                        : v == 3 ? diff_single_kernel<2, 8192, 4, true>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, true>
@@ -873,7 +926,7 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         const uint64_t* rec_off, const uint8_t* data, uint32_t* err,
                         hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
-  ProfScope ps(prof, 3, s);
+  ProfScope ps(prof, GDSM_PROF_APPLY, s);
   // one task per wave, 4 waves per workgroup: no workgroup launched without work. A task is 64
   // records (one staging window serves many small records); short lists take 4 per task, so a
   // few dense records are spread over waves instead of queueing in one

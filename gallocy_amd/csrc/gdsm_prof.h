@@ -5,10 +5,12 @@
 
 #include <vector>
 
+#include "gdsm.h"
+
 namespace gdsm {
 
 struct Prof {
-  static constexpr int kStages = 12;
+  static constexpr int kStages = GDSM_PROF_STAGES;
   bool on = false;
   hipStream_t stream = nullptr;
   struct Mark { int stage; hipEvent_t a, b; };

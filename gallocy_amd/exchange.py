@@ -18,6 +18,7 @@ home (send_ids). Protocol per release (gdsm_exchange; `GlooTransport` restates i
 from __future__ import annotations
 
 import ctypes as C
+from errno import EIO, EOVERFLOW
 
 import numpy as np
 
@@ -92,10 +93,15 @@ class GlooTransport:
 
 # ---------------------------------------------------------------- the GPU shard
 class Comm:
-    """An RCCL communicator owned by libgdsm (gdsm_comm_*), bootstrapped with a torch.distributed
-    group (any backend) that carries the 128-byte unique id."""
+    """A communicator owned by libgdsm (gdsm_comm_*). RCCL (the product transport): bootstrapped
+    with a torch.distributed group (any backend) that carries the 128-byte unique id. Loopback
+    (`Comm.loopback`, tests): several ranks as threads of one process on one GPU."""
 
-    def __init__(self, ctx: gdsm.Context, rank: int, world: int, group=None):
+    def __init__(self, ctx: gdsm.Context, rank: int, world: int, group=None, handle=None):
+        self.rank, self.world = rank, world
+        if handle is not None:
+            self.handle = handle
+            return
         import torch
         import torch.distributed as dist
         L = gdsm.lib()
@@ -110,7 +116,22 @@ class Comm:
         h = C.c_void_p()
         check(L.gdsm_comm_init(C.byref(h), ctx.handle, world, rank, uid), "gdsm_comm_init")
         self.handle = h.value
-        self.rank, self.world = rank, world
+
+    @classmethod
+    def loopback(cls, ctxs: list) -> list:
+        """gdsm_comm_init_loopback: one communicator per context, rank r bound to ctxs[r]; each
+        must then be driven by its own thread (every collective blocks until all ranks call it)."""
+        G = len(ctxs)
+        hs = (C.c_void_p * G)()
+        cs = (C.c_void_p * G)(*[c.handle for c in ctxs])
+        check(gdsm.lib().gdsm_comm_init_loopback(hs, cs, G), "gdsm_comm_init_loopback")
+        return [cls(ctxs[r], r, G, handle=hs[r]) for r in range(G)]
+
+    def agree(self, ctx: gdsm.Context, value: int) -> int:
+        """gdsm_comm_agree: the maximum of every rank's value (collective, synchronous)."""
+        v = C.c_uint64(value)
+        check(gdsm.lib().gdsm_comm_agree(self.handle, ctx.handle, C.byref(v)), "gdsm_comm_agree")
+        return v.value
 
     def close(self):
         if self.handle:
@@ -168,12 +189,18 @@ class Shard:
     waits on the device for the exchange that last read it (libgdsm orders that itself).
 
     transport "rccl": gdsm_exchange (RCCL inside libgdsm). After `calibrate()`, releases use
-    GDSM_XCHG_FIXED byte budgets: no host synchronisation at all per release.
+    GDSM_XCHG_FIXED byte budgets: no host synchronisation at all per release. A release whose
+    stream outgrew its budget is rejected whole at the home (and reported on both ends as
+    -EOVERFLOW); `drain()` has the ranks agree on it (gdsm_comm_agree) and redoes the release with
+    exact sizes, then re-calibrates. The twin is never refreshed inside the Shard, so one exact
+    release of the current state restores every home.
+    transport "loopback": the same calls through a `Comm.loopback` communicator (`comm=`): ranks
+    are threads of one process on one GPU (tests of the multi-rank C++ path).
     transport "gloo": the GlooTransport restatement with host staging (rehearsal of several ranks
-    on one GPU, where RCCL cannot run); not a measurement."""
+    on one GPU as processes); not a measurement."""
 
     def __init__(self, ctx: gdsm.Context, rank: int, world: int, n: int, cap_per_page: int,
-                 transport: str = "rccl", group=None, sets: int = 2):
+                 transport: str = "rccl", group=None, sets: int = 2, comm: "Comm" = None):
         if n % world:
             raise ValueError("pages per rank must be a multiple of the rank count")
         self.ctx, self.rank, self.world, self.n = ctx, rank, world, n
@@ -193,11 +220,16 @@ class Shard:
                      else gdsm.Runs(ctx, 1, cap=16) for s in range(world)]
         self.rids = [ctx.buffer(4 * rmax if s != rank else 4) for s in range(world)]
         self.transport = transport
-        self.comm = Comm(ctx, rank, world, group) if transport == "rccl" else None
+        if transport == "loopback" and comm is None:
+            raise ValueError("transport loopback needs comm= (Comm.loopback)")
+        self.comm = comm if comm is not None else (
+            Comm(ctx, rank, world, group) if transport == "rccl" else None)
+        self.own_comm = comm is None
         self.gloo = GlooTransport(group) if transport == "gloo" else None
         self.flags = 0
-        self.sent_remote = self.received = 0
+        self.sent_remote = self.received = self.moved_remote = 0
         self.k = 0
+        self.recoveries = 0
 
     # -- one release
     def diff(self, k: int):
@@ -257,11 +289,39 @@ class Shard:
             r.s.cap = min(r.cap_alloc, budget(int(t[0])))
         self.sent_remote = sum(b for d, b in enumerate(sent) if d != self.rank)
         self.received = sum(recvd) + sent[self.rank]
+        # what the transport carries to the peers per fixed-budget release
+        self.moved_remote = sum(8 * (c + 1) + 4 * c + self.send[0][d].s.cap
+                                for d, c in enumerate(self.counts) if d != self.rank)
         self.flags = XCHG_FIXED
 
     def drain(self):
-        """Waits for both streams; raises on a malformed or over-budget stream."""
-        self.ctx.sync()
+        """Waits for both streams. With a communicator the ranks then agree on the outcome
+        (gdsm_comm_agree: 0 ok, 1 some fixed-budget stream overflowed, 2 anything else): on 1
+        every rank redoes the release with exact sizes and re-calibrates (`recoveries` counts
+        them); on 2 every rank raises."""
+        rc = self.L.gdsm_sync(self.ctx.handle)
+        if self.comm is None:
+            check(rc, "gdsm_sync")
+            return
+        verdict = 0 if rc == 0 else (1 if rc == -EOVERFLOW else 2)
+        agreed = self.comm.agree(self.ctx, verdict)
+        if agreed >= 2:
+            check(rc if rc else -EIO, "gdsm_sync (a rank failed its release)")
+        if agreed == 1:
+            self.recover()
+
+    def recover(self):
+        """Redoes the release with exact sizes (TWIN vs CURRENT is unchanged, so the streams
+        carry everything the rejected fixed-budget releases did; the apply is idempotent), then
+        fixes new budgets."""
+        self.flags = 0
+        for r in [x for st in self.send for x in st] + self.recv:
+            r.s.cap = r.cap_alloc  # budgets off: the whole allocation again
+        self.diff(0)
+        self.exchange(0)
+        check(self.L.gdsm_sync(self.ctx.handle), "gdsm_sync (recovery release)")
+        self.calibrate()
+        self.recoveries += 1
 
     def verify(self, seed: int, mode: int, ppm: int) -> bool:
         """REPLICA (home block) == CURRENT content of those pages, generated independently."""
@@ -281,5 +341,5 @@ class Shard:
         return ok
 
     def close(self):
-        if self.comm is not None:
+        if self.comm is not None and self.own_comm:
             self.comm.close()

@@ -219,8 +219,8 @@ class Context:
         check(lib().gdsm_capture_end(self.handle, C.byref(g)), "gdsm_capture_end")
         return Graph(g.value)
 
-    PROF_STAGES = ("diff", "scan", "pack", "apply", "twin", "coh_tail", "coh_scan", "coh_apply",
-                   "coh_reduce", "nw_fill", "nw_trace", "exchange")
+    PROF_STAGES = ("diff", "apply", "twin", "coh_fold", "coh_reduce", "nw_fill", "nw_trace",
+                   "exchange", "route")
 
     def prof_enable(self, on: bool = True):
         check(lib().gdsm_prof_enable(self.handle, int(on)), "gdsm_prof_enable")

@@ -24,7 +24,9 @@
  *     (gallocy/include/gallocy/allocators/internal.h:75-82), which own diff()'s outputs.
  *
  * Conventions: every function returns 0 or a negative errno (-EINVAL -22, -ENOMEM -12,
- * -EIO -5 for a HIP failure, -ENOSPC -28, -ENODEV -19) and never aborts. Device work is
+ * -EIO -5 for a HIP failure, -ENOSPC -28, -ENODEV -19, -EOVERFLOW -75 for a fixed-budget exchange
+ * stream over its budget, -ETIMEDOUT -110 for a loopback rank that never arrived) and never
+ * aborts. Device work is
  * enqueued on the context's HIP stream and is asynchronous unless the comment says it
  * synchronises. One context per host thread, or external synchronisation.
  */
@@ -58,18 +60,15 @@ enum gdsm_init_flags {
 };
 /* Per-kernel stages timed by gdsm_prof_* (HIP events on the context stream). */
 enum gdsm_prof_stage {
-  GDSM_PROF_DIFF = 0, /* diff_single_kernel: the dominant kernel of the hot path */
-  GDSM_PROF_SCAN,     /* unused since round 2 (the diff packs its stream itself) */
-  GDSM_PROF_PACK,     /* unused since round 2 */
-  GDSM_PROF_APPLY,
-  GDSM_PROF_TWIN,
-  GDSM_PROF_COH_TAIL,
-  GDSM_PROF_COH_SCAN,
-  GDSM_PROF_COH_APPLY,
-  GDSM_PROF_COH_REDUCE,
-  GDSM_PROF_NW_FILL,  /* GPU diff(): DP fill */
-  GDSM_PROF_NW_TRACE, /* GPU diff(): traceback + alignment strings */
-  GDSM_PROF_EXCHANGE, /* gdsm_exchange: the RCCL transfer of the record streams */
+  GDSM_PROF_DIFF = 0,   /* diff_single_kernel: the dominant kernel of the hot path */
+  GDSM_PROF_APPLY,      /* apply_kernel */
+  GDSM_PROF_TWIN,       /* twin_kernel */
+  GDSM_PROF_COH_FOLD,   /* coh_fold_kernel: the coherence batch */
+  GDSM_PROF_COH_REDUCE, /* the batch totals */
+  GDSM_PROF_NW_FILL,    /* GPU diff(): DP fill */
+  GDSM_PROF_NW_TRACE,   /* GPU diff(): traceback + alignment strings */
+  GDSM_PROF_EXCHANGE,   /* gdsm_exchange: the transfer of the record streams (RCCL group) */
+  GDSM_PROF_ROUTE,      /* gdsm_route_events / gdsm_route_notices: the transfer */
   GDSM_PROF_STAGES
 };
 
@@ -303,6 +302,17 @@ int gdsm_comm_unique_id(uint8_t* id);
 int gdsm_comm_init(gdsm_comm** out, gdsm_ctx* ctx, int nranks, int rank, const uint8_t* id);
 int gdsm_comm_fini(gdsm_comm* comm);
 int gdsm_comm_size(const gdsm_comm* comm, int* nranks, int* rank);
+/* Test transport: nranks communicators over nranks contexts of ONE process (normally all on one
+ * GPU), comms[r] bound to ctxs[r] and driven by its own host thread. Every collective below makes
+ * the same calls at the same points as over RCCL; the moves become device-to-device copies on
+ * the contexts' streams, ordered by HIP events (a receiver copies after the sender's stream
+ * reached the send; the sender's stream continues after every receiver copied). It lets the
+ * multi-rank code paths run on a one-GPU box. RCCL stays the transport of gdsm_comm_init. */
+int gdsm_comm_init_loopback(gdsm_comm** comms, gdsm_ctx* const* ctxs, int nranks);
+/* Collective, synchronous (after the work enqueued on ctx): *value becomes the maximum of every
+ * rank's *value. The ranks' agreement on what to do next, e.g. whether to redo a release whose
+ * fixed budget overflowed (-EOVERFLOW on some rank, below). */
+int gdsm_comm_agree(gdsm_comm* comm, gdsm_ctx* ctx, uint64_t* value);
 
 /* gdsm_exchange flags */
 enum gdsm_exchange_flags {
@@ -310,9 +320,13 @@ enum gdsm_exchange_flags {
    * send[d] ships exactly send[d].n records and send[d].cap data bytes (cap is the byte budget:
    * the stream's real size, rec_off[n], must not exceed it; the bytes past it are padding);
    * recv[s].n and recv[s].cap must equal what rank s ships here. A stream found larger than its
-   * budget is not applied and the next gdsm_sync reports -EINVAL. Without the flag the library
-   * learns the sizes with one device all-to-all of (records, bytes) and one host read, and agrees
-   * on capacity with every rank (all return -ENOSPC when any receive stream is too small). */
+   * budget is not applied (its offsets are zeroed) and the next gdsm_sync of the home AND of the
+   * sender reports -EOVERFLOW (when nothing else went wrong). Nothing of the release is lost
+   * that the same release redone without the flag does not restore: gdsm_comm_agree on the
+   * verdict, then re-diff and exchange with exact sizes (diff streams are idempotent). Without
+   * the flag the library learns the sizes with one device all-to-all of (records, bytes) and
+   * one host read, and agrees on capacity with every rank (all return -ENOSPC when any stream
+   * is too small). */
   GDSM_XCHG_FIXED = 1u << 0,
 };
 /* Collective: every rank of `comm` calls it with arrays of nranks entries.
@@ -324,11 +338,52 @@ enum gdsm_exchange_flags {
  *                         place from send[rank].
  * Runs on the context's second stream after everything enqueued on the main stream (the diffs
  * that produced send[]); it overlaps the gdsm_diff calls that follow, and a later gdsm_diff into
- * one of the send streams waits for it (as gdsm_apply_async). Malformed records and out-of-range
- * page indices are reported by the next gdsm_sync. */
+ * one of the send streams waits for it (as gdsm_apply_async). Every stream (the own one too) is
+ * checked whole before it is applied: offsets from 0, non-decreasing, 4-aligned, within the
+ * budget, every page index < the arena's pages; a stream failing any check is not applied at
+ * all and the next gdsm_sync reports -EINVAL (-EOVERFLOW when the budget was the only fault);
+ * a malformed record inside a well-formed stream is caught by the apply (SPEC §4). */
 int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* comm, const gdsm_runs* send,
                   const uint32_t* const* send_ids, gdsm_runs* recv, uint32_t* const* recv_ids,
                   int target, uint32_t flags);
+
+/* ---- coherence across GPUs (docs/SPEC.md §5b) ----------------------------------
+ * Rank r of the communicator is DSM node r and the home of the page block
+ * [r * per, (r+1) * per), per = ceil(total_pages / nranks) (SPEC §5's initial home); its page-table
+ * context holds that block (local page = global page - base). A batch of faults is handled in two
+ * collective, host-synchronising steps (every rank calls both, in this order, with its own data):
+ *   1. gdsm_route_events: each node's fault events go to their pages' homes, where the sources'
+ *      lists are merged into one page-sorted batch;
+ *   2. gdsm_coherence_notify: each home folds its batch into its page-table shard (SPEC §5) and
+ *      sends every node whose access to a page changed a notice, the "negotiate access / copy over
+ *      the latest contents / update protections" step of resources/NUTSHELL.md:61-69 that the
+ *      reference only describes (its transport would be gallocy/http/client.cpp:39-91).
+ * The shards then equal the sequential fold of all nodes' events in (page, seq) order. */
+#define GDSM_STAMP_PAGE_SHIFT 36
+/* A node's fault event, stamped: (page << 36) | (seq << 4) | (node << 1) | rw, page < 2^28 the
+ * GLOBAL page, seq < 2^32 the event's position in the batch's global order (a logical clock; unique
+ * per page), node = the calling rank. A node's list is sorted ascending (by page, then seq). */
+/* Routes this node's n stamped events (device) to the homes; on return *n_batch events of this
+ * rank's home block, from every node, merged by (page, seq) and packed as SPEC §5 events with the
+ * LOCAL page, are being written to `batch` (device, cap entries) on ctx's stream. All ranks return
+ * -EINVAL if any node's list is unsorted or names a page >= total_pages or a node >= nranks, and
+ * -ENOSPC if any home's cap is too small; nothing moves then. */
+int gdsm_route_events(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* events, uint64_t n,
+                      uint64_t total_pages, uint64_t* batch, uint64_t cap, uint64_t* n_batch);
+/* Home side: folds `batch` (n events, local pages, e.g. from gdsm_route_events) into ctx's page
+ * table (gdsm_coh_init'd, pages [base, base + n_pages)) with its totals into totals_dev (10 x u64,
+ * as gdsm_coherence_batch_async), then sends each node its notices. On return *n_notices notices
+ * for THIS rank as a node, from every home, sorted by page, are being written to `notices`
+ * (device, cap entries) on ctx's stream. A notice (u64) for page p and node d:
+ *   bits 0-31 global page | 32-33 d's access before the batch | 34-35 d's access after |
+ *   40-47 owner before | 48-55 owner after
+ * with access 0 none, 1 read (d in the copyset), 2 write (EXCLUSIVE and d the owner); d gets one
+ * iff its access changed or it is the old or the new owner of a page whose owner changed. All
+ * ranks return -EINVAL if any home's batch was rejected by the fold, -ENOSPC if any node's cap is
+ * too small. */
+int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* batch, uint64_t n,
+                          uint64_t base, uint64_t* totals_dev, uint64_t* notices, uint64_t cap,
+                          uint64_t* n_notices);
 
 const char* gdsm_version(void);
 /* Process-wide kernel-variant knobs for measurement, e.g. ("diff_variant", 0..4). */

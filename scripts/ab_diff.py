@@ -38,7 +38,7 @@ for r in range(ROUNDS):
         p = ctx.prof_read()
         ctx.prof_enable(False)
         res[v].append(p["diff"][0] / p["diff"][1])
-        full.setdefault(v, []).append(sum(p[k][0] for k in ("diff", "scan", "pack")) / REPS)
+        full.setdefault(v, []).append(sum(p[k][0] for k in ("diff",)) / REPS)
         if True:
             t = runs.total()
             assert total is None or t == total, (v, t, total)

@@ -117,14 +117,16 @@ def test_legacy_caller_on_gallocy_internal_heap():
 
 
 def test_tune_rejects_measurement_only_variants():
-    """Kernels that do not produce valid output are not selectable in the product library
-    (they exist only in a -DGDSM_MEASURE build); the valid variants are."""
+    """Kernels that do not produce valid output, and the retired four-pass coherence path, are not
+    selectable in the product library (they exist only in a -DGDSM_MEASURE build); the valid
+    variants are."""
     from gallocy_amd import _lib
     L = _lib.load()
-    for key, bad in ((b"coh_variant", 2), (b"coh_variant", 3), (b"diff_variant", 5),
+    for key, bad in ((b"coh_variant", 1), (b"coh_variant", 2), (b"coh_variant", 3),
+                     (b"diff_variant", 5),
                      (b"apply_variant", 1), (b"no_such_knob", 0)):
         assert L.gdsm_tune(key, bad) == -22, (key, bad)
     for key, ok in ((b"diff_variant", 1), (b"diff_variant", 2), (b"diff_variant", 3),
-                    (b"diff_variant", 4), (b"coh_variant", 1), (b"coh_variant", 0)):
+                    (b"diff_variant", 4), (b"coh_variant", 0)):
         assert L.gdsm_tune(key, ok) == 0
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0
