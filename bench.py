@@ -295,18 +295,21 @@ def run_coherence(args):
 
 def run_mmult_ranks(args, rank: int, world: int):
     """BASELINE configs[4] at N > 1: one process (GPU) per DSM node of the trace
-    (gallocy_amd.replay.MmultRankReplay): page-table shards at the homes, per-round diffs shipped
-    to the home GPUs with gdsm_exchange (RCCL). Strong scaling: the same NDIM = 1000 product."""
+    (gallocy_amd.replay.MmultRankReplay): each node's fault events routed to the page-table shards
+    at the homes and the access-change notices returned (gdsm_route_events /
+    gdsm_coherence_notify), the per-round diffs shipped to the home GPUs with gdsm_exchange, all
+    over RCCL. Strong scaling: the same NDIM = 1000 product. (Several ranks on one GPU are
+    rehearsed by tests/test_gpu_replay.py with the loopback communicator.)"""
     import torch
     import torch.distributed as dist
 
     from gallocy_amd.replay import MmultRankReplay
-    backend = os.environ.get("GDSM_BENCH_BACKEND", "nccl")
+    if os.environ.get("GDSM_BENCH_BACKEND", "nccl") != "nccl":
+        raise SystemExit("--workload mmult at N > 1 runs on RCCL only")
     local = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist.init_process_group("gloo")
-    R = MmultRankReplay(rank, world, ndim=args.ndim, seed=args.seed, device=local,
-                        transport="gloo" if backend == "gloo" else "rccl")
+    R = MmultRankReplay(rank, world, ndim=args.ndim, seed=args.seed, device=local)
     dist.barrier()
     dt = R.run()
     ok = torch.tensor([1 if np.array_equal(R.home_block(), R.final_block()) else 0],
@@ -326,10 +329,9 @@ def run_mmult_ranks(args, rank: int, world: int):
                "scaling": "strong", "vs_baseline": None, "dtype": "u8/u64",
                "data": "test_mmult trace from the reference heap layout (gallocy_amd/trace.py)",
                "config": {"workload": f"NDIM={args.ndim}, {world} DSM nodes = {world} GPUs, "
-                                      f"{R.Z} zone pages, page-table shards + RCCL diff exchange",
-                          "rows": args.ndim, "events": int(ev[0]), "pages_diffed": int(ev[1]),
-                          **({"backend": "gloo (REHEARSAL, not a measurement)"}
-                             if backend == "gloo" else {})},
+                                      f"{R.Z} zone pages, events routed to page-table shards + notices back + "
+                                      f"diff exchange, RCCL",
+                          "rows": args.ndim, "events": int(ev[0]), "pages_diffed": int(ev[1])},
                "seconds_total": round(dt, 4), "rows_per_s": round(args.ndim / dt, 1),
                "home_copy_equals_product": bool(ok.item()),
                "totals": {"invalidations": int(tot[0]), "transfers": int(tot[1]),

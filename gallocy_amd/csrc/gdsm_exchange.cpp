@@ -648,7 +648,24 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
   if (rc) return rc;
   uint32_t* pre = reinterpret_cast<uint32_t*>(c->pre);
   uint64_t* cnt = c->rcnt_dev;  // [0,G) notices per node, [G,2G) received, [2G,3G) bases
-  GDSM_TRY(gdsm::launch_notice_pre(ctx->coh_pt, ctx->n_pages, batch, n, pre, s));
+  uint64_t* h = c->rcnt_host;
+  // capacity first, before the page table changes: a node gets at most one notice per page that
+  // any home's batch touches, so every node needs cap >= the sum of the homes' distinct pages
+  GDSM_TRY(gdsm::launch_notice_pre(ctx->coh_pt, ctx->n_pages, batch, n, pre, cnt + 4 * G, s));
+  GDSM_TRY(hipMemcpyAsync(h + 4 * G, cnt + 4 * G, 8, hipMemcpyDeviceToHost, s));
+  GDSM_TRY(hipStreamSynchronize(s));
+  for (int p = 0; p < G; ++p) h[p] = h[4 * G];
+  GDSM_TRY(hipMemcpyAsync(cnt, h, 8 * (size_t)G, hipMemcpyHostToDevice, s));
+  rc = xp->all_to_all_u64(cnt, cnt + G, 1, s);
+  if (rc) return rc;
+  GDSM_TRY(hipMemcpyAsync(h + G, cnt + G, 8 * (size_t)G, hipMemcpyDeviceToHost, s));
+  GDSM_TRY(hipStreamSynchronize(s));
+  uint64_t bound = 0;
+  for (int p = 0; p < G; ++p) bound += h[G + p];
+  uint64_t small = bound > cap ? 1u : 0u;
+  rc = xp->agree_max(&small, s);
+  if (rc) return rc;
+  if (small) return -ENOSPC;
   rc = gdsm_coherence_batch_async(ctx, batch, n, totals_dev);
   if (rc) return rc;
   uint32_t* blk = reinterpret_cast<uint32_t*>(c->blk);
@@ -657,7 +674,6 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
                                      blk_off, cnt, cnt + 2 * G, s));
   rc = xp->all_to_all_u64(cnt, cnt + G, 1, s);
   if (rc) return rc;
-  uint64_t* h = c->rcnt_host;
   GDSM_TRY(hipMemcpyAsync(h, cnt, 8 * 3 * (size_t)G, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipMemcpyAsync(h + 4 * G, ctx->err, 4, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipStreamSynchronize(s));
@@ -667,15 +683,12 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
     off[p + 1] = off[p] + h[G + p];
     sent += h[p];
   }
-  // 2 = some home's batch was rejected by the fold (its page table is unspecified), 1 = some
-  // node's notice buffer is too small
-  uint64_t verdict = ((reinterpret_cast<uint32_t*>(h + 4 * G)[0] & gdsm::detail::kErrEvents)
-                          ? 2u : 0u) |
-                     (off[G] > cap ? 1u : 0u);
+  // some home's batch was rejected by the fold (its page table is unspecified): all refuse
+  uint64_t verdict = (reinterpret_cast<uint32_t*>(h + 4 * G)[0] & gdsm::detail::kErrEvents) ||
+                     off[G] > cap;  // (cannot exceed the bound checked above)
   rc = xp->agree_max(&verdict, s);
   if (rc) return rc;
-  if (verdict & 2) return -EINVAL;
-  if (verdict & 1) return -ENOSPC;
+  if (verdict) return -EINVAL;
   rc = ensure(ctx, &c->staging, &c->staging_bytes, 8 * (sent ? sent : 1));
   if (rc) return rc;
   uint64_t* stg = reinterpret_cast<uint64_t*>(c->staging);

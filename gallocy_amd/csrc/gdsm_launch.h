@@ -64,8 +64,9 @@ hipError_t launch_route_split(const uint64_t* ev, uint64_t n, uint64_t total_pag
 hipError_t launch_route_merge(const uint64_t* runs, const uint64_t* off, uint32_t G, uint64_t base,
                               uint64_t* out, hipStream_t s);
 uint64_t notice_blocks(uint64_t n);
+// pre[i] = the page-table word at each page's first event; *heads = the batch's distinct pages.
 hipError_t launch_notice_pre(const uint64_t* pt, uint64_t n_pages, const uint64_t* batch,
-                             uint64_t n, uint32_t* pre, hipStream_t s);
+                             uint64_t n, uint32_t* pre, uint64_t* heads, hipStream_t s);
 // blk: notice_blocks(n) x 8 u32; blk_off the same in u64; dest_total / dest_base: G u64 each.
 hipError_t launch_notice_count(const uint64_t* pt, uint64_t n_pages, const uint64_t* batch,
                                uint64_t n, const uint32_t* pre, uint32_t G, uint32_t* blk,

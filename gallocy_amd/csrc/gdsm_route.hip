@@ -126,16 +126,24 @@ __device__ __forceinline__ bool batch_head(const uint64_t* __restrict__ batch, u
   return i == 0 || ((uint32_t)batch[i - 1] >> 4) != page;
 }
 
-// Before the fold: the state word of every page the batch touches, at its first event.
+// Before the fold: the state word of every page the batch touches, at its first event, and the
+// number of such pages (heads += one atomic per wave; the bound on any node's notices).
 __global__ __launch_bounds__(256) void notice_pre_kernel(const uint64_t* __restrict__ pt,
                                                          uint64_t n_pages,
                                                          const uint64_t* __restrict__ batch,
-                                                         uint64_t n, uint32_t* __restrict__ pre) {
+                                                         uint64_t n, uint32_t* __restrict__ pre,
+                                                         unsigned long long* __restrict__ heads) {
+  uint32_t cnt = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t page;
-    if (batch_head(batch, i, page) && page < n_pages) pre[i] = (uint32_t)pt[page];
+    if (batch_head(batch, i, page)) {
+      ++cnt;
+      if (page < n_pages) pre[i] = (uint32_t)pt[page];
+    }
   }
+  const uint32_t w = wave_sum(cnt);
+  if ((threadIdx.x & 63) == 0 && w) atomicAdd(heads, (unsigned long long)w);
 }
 
 // After the fold, one event per thread, 256 per block. kEmit = false: per-block notice counts per
@@ -252,10 +260,11 @@ hipError_t launch_route_merge(const uint64_t* runs, const uint64_t* off, uint32_
 uint64_t notice_blocks(uint64_t n) { return (n + 255) / 256; }
 
 hipError_t launch_notice_pre(const uint64_t* pt, uint64_t n_pages, const uint64_t* batch,
-                             uint64_t n, uint32_t* pre, hipStream_t s) {
-  if (n == 0) return hipSuccess;
+                             uint64_t n, uint32_t* pre, uint64_t* heads, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(heads, 0, 8, s);
+  if (e != hipSuccess || n == 0) return e;
   hipLaunchKernelGGL(notice_pre_kernel, dim3(grid_of(n, 8192)), dim3(256), 0, s, pt, n_pages, batch,
-                     n, pre);
+                     n, pre, reinterpret_cast<unsigned long long*>(heads));
   return hipGetLastError();
 }
 

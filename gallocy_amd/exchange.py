@@ -343,3 +343,24 @@ class Shard:
     def close(self):
         if self.comm is not None and self.own_comm:
             self.comm.close()
+
+
+# ---------------------------------------------------------------- coherence across GPUs
+def route_events(ctx: gdsm.Context, comm: Comm, events: int, n: int, total_pages: int,
+                 batch: int, cap: int) -> int:
+    """gdsm_route_events (SPEC §5b): this node's n stamped events (device pointer) to their
+    homes; returns how many events of this rank's home block land in `batch` (device, cap)."""
+    nb = C.c_uint64(0)
+    check(gdsm.lib().gdsm_route_events(ctx.handle, comm.handle, events, n, total_pages, batch,
+                                       cap, C.byref(nb)), "gdsm_route_events")
+    return nb.value
+
+
+def coherence_notify(ctx: gdsm.Context, comm: Comm, batch: int, n: int, base: int, totals: int,
+                     notices: int, cap: int) -> int:
+    """gdsm_coherence_notify (SPEC §5b): fold this home's batch into ctx's page-table shard and
+    exchange the notices; returns how many notices for this node land in `notices`."""
+    nn = C.c_uint64(0)
+    check(gdsm.lib().gdsm_coherence_notify(ctx.handle, comm.handle, batch, n, base, totals,
+                                           notices, cap, C.byref(nn)), "gdsm_coherence_notify")
+    return nn.value

@@ -158,17 +158,22 @@ class MmultRankReplay:
     """Config 5 with one process (one GPU) per DSM node: rank t of P = node t of the trace.
 
     Pages are homed in contiguous blocks, home(p) = p // ceil(Z / P), which is also the home the
-    page table is initialised with (SPEC §5). Per round, on every rank:
-      1. coherence: the round's events on the pages homed here, in the trace's order, folded into
-         this rank's page-table shard (local page p - base);
+    page table is initialised with (SPEC §5). Per round, on every rank (SPEC §5b):
+      1. coherence: the node's OWN fault events of the round (stamped with the round's logical
+         clock, MmultTrace.round_stamped) go to their pages' homes with gdsm_route_events; each
+         home folds the merged batch into its page-table shard and returns the access-change
+         notices to the nodes with gdsm_coherence_notify (kept per round in `notices_of(r)`);
       2. twin, then the node's own row writes c[i][*] in its view of the zone (CURRENT);
       3. release: the written pages are diffed into one stream per home rank and shipped with
-         gdsm_exchange (RCCL), each home applying what it receives to its REPLICA (indexed by
-         global page: the home block is REPLICA[base, base + per)).
-    At the end every home block equals the zone after the multiplication, and the page-table
-    shards together equal the sequential fold of the whole trace (tests/test_gpu_replay.py).
-    transport "gloo": the exchange goes through host memory (GlooTransport), so several ranks
-    can rehearse on one GPU; not a measurement."""
+         gdsm_exchange, each home applying what it receives to its REPLICA (indexed by global
+         page: the home block is REPLICA[base, base + per)).
+    At the end every home block equals the zone after the multiplication, the page-table shards
+    together equal the sequential fold of the whole trace, and every node's notices equal the
+    ones the sequential fold implies (tests/test_gpu_replay.py).
+    Two communicators: one for page data (on the data context), one for coherence (on the
+    page-table context), so the two kinds of collective never share an RCCL communicator across
+    streams. transport "rccl" creates them; transport "loopback" (several ranks as threads of one
+    process on one GPU) takes them from `wire_loopback`."""
 
     def __init__(self, rank: int, world: int, ndim: int = 1000, seed: int = 0, device: int = 0,
                  transport: str = "rccl", group=None):
@@ -186,13 +191,14 @@ class MmultRankReplay:
         # ---- host preparation (not part of the replay time)
         self.rounds = []
         rowvals = np.stack([c_row_values(L, i) for i in range(L.ndim)]).view(np.uint8)
-        max_per_dest, max_ev = 1, 1
+        max_per_dest, bcap, ncap = 1, 1, 1
 
         def written(rows):
             return np.unique(np.concatenate(
                 [np.arange(int(L.c_rows[i]) // PAGE_SZ,
                            (int(L.c_rows[i]) + 8 * L.ndim - 1) // PAGE_SZ + 1) for _, i in rows])
                              ) if rows else np.zeros(0, np.int64)
+        evs = []
         for r in range(self.T.rounds):
             all_rows = self.T.round_rows(r)
             for t in range(world):  # receive streams are sized for the largest sender
@@ -202,13 +208,14 @@ class MmultRankReplay:
             rows = [(t, i) for t, i in all_rows if t == rank]
             pages = written(rows)
             by_dest = [pages[home(pages) == d].astype(np.uint32) for d in range(world)]
-            ev = self.T.round_events(r)
-            pg = (ev >> 4).astype(np.int64)
-            mine = (pg >= self.base) & (pg < self.base + self.nh)
-            ev = (((pg[mine] - self.base).astype(np.uint64) << 4) | (ev[mine] & 15)).astype(np.uint64)
-            self.rounds.append((rows, pages.astype(np.uint32), by_dest, ev))
+            stamped = self.T.round_stamped(r)
+            evs.append(stamped[rank])
+            total = sum(len(x) for x in stamped)
+            bcap = max(bcap, total)  # a home may receive the whole round
+            ncap = max(ncap, len(np.unique(np.concatenate(stamped) >> np.uint64(36)))
+                       if total else 1)  # one notice per node and page at most
+            self.rounds.append((rows, pages.astype(np.uint32), by_dest))
             max_per_dest = max([max_per_dest] + [len(x) for x in by_dest])
-            max_ev = max(max_ev, len(ev))
         # ---- device state
         self.data = gdsm.Context(Z, device=device)
         self.pt = gdsm.Context(max(1, self.nh), device=device, arenas=())
@@ -224,7 +231,7 @@ class MmultRankReplay:
         # per round: written pages (twin list) and per-destination lists, in one device buffer
         flat, self.offs = [], []
         pos = 0
-        for rows, pages, by_dest, ev in self.rounds:
+        for rows, pages, by_dest in self.rounds:
             o = [pos]
             flat.append(pages)
             pos += len(pages)
@@ -235,10 +242,15 @@ class MmultRankReplay:
             self.offs.append(o)
         allids = np.concatenate(flat).astype(np.uint32) if pos else np.zeros(1, np.uint32)
         self.d_ids = self.data.ids(allids)
-        evs = [e for *_, e in self.rounds]
+        # this node's stamped events of every round, back to back; the home batch; the notices
         self.ev_off = np.concatenate([[0], np.cumsum([len(e) for e in evs])]).astype(np.int64)
         allev = np.concatenate(evs).astype(np.uint64) if self.ev_off[-1] else np.zeros(1, np.uint64)
         self.d_ev = self.pt.buffer(max(8, allev.nbytes)).upload(allev)
+        self.bcap, self.ncap = bcap, ncap
+        self.d_batch = self.pt.buffer(8 * bcap)
+        self.d_notices = self.pt.buffer(8 * ncap * max(1, self.T.rounds))
+        self.n_notices = np.zeros(self.T.rounds, np.int64)
+        self.n_batch = np.zeros(self.T.rounds, np.int64)
         self.d_tot = self.pt.buffer(8 * 10 * max(1, self.T.rounds))
         cap = max_per_dest * 10244
         self.send = [gdsm.Runs(self.data, max_per_dest, cap=cap) for _ in range(world)]
@@ -246,22 +258,39 @@ class MmultRankReplay:
                      else gdsm.Runs(self.data, 1, cap=16) for s in range(world)]
         self.rids = [self.data.buffer(4 * max_per_dest) for _ in range(world)]
         gdsm.check(gdsm.lib().gdsm_reserve(self.data.handle, max_per_dest, 0), "reserve")
-        gdsm.check(gdsm.lib().gdsm_reserve(self.pt.handle, 0, max_ev), "reserve")
+        gdsm.check(gdsm.lib().gdsm_reserve(self.pt.handle, 0, bcap), "reserve")
         self.transport = transport
-        self.comm = exchange.Comm(self.data, rank, world, group) if transport == "rccl" else None
-        self.gloo = exchange.GlooTransport(group) if transport == "gloo" else None
+        self.comm = self.coh_comm = None
+        if transport == "rccl":
+            self.comm = exchange.Comm(self.data, rank, world, group)
+            self.coh_comm = exchange.Comm(self.pt, rank, world, group)
+        elif transport != "loopback":
+            raise ValueError("transport: rccl or loopback")
         self.events_total = int(self.ev_off[-1])
-        self.pages_diffed = sum(len(p) for _, p, _, _ in self.rounds)
+        self.pages_diffed = sum(len(p) for _, p, _ in self.rounds)
         self.totals = None
+
+    @staticmethod
+    def wire_loopback(replays: list):
+        """Loopback communicators for replays built with transport="loopback" (one per rank,
+        all in this process, each then driven by its own thread)."""
+        from . import exchange
+        data = exchange.Comm.loopback([R.data for R in replays])
+        coh = exchange.Comm.loopback([R.pt for R in replays])
+        for R, a, b in zip(replays, data, coh):
+            R.comm, R.coh_comm = a, b
 
     def round(self, r: int):
         from . import exchange
         lib = gdsm.lib()
-        rows, pages, by_dest, ev = self.rounds[r]
+        rows, pages, by_dest = self.rounds[r]
         e0, e1 = int(self.ev_off[r]), int(self.ev_off[r + 1])
-        if e1 > e0:                                                                      # 1
-            gdsm.check(lib.gdsm_coherence_batch_async(self.pt.handle, self.d_ev.ptr + 8 * e0,
-                                                      e1 - e0, self.d_tot.ptr + 80 * r), "coherence")
+        nb = exchange.route_events(self.pt, self.coh_comm, self.d_ev.ptr + 8 * e0, e1 - e0,  # 1
+                                   self.Z, self.d_batch.ptr, self.bcap)
+        self.n_batch[r] = nb
+        self.n_notices[r] = exchange.coherence_notify(
+            self.pt, self.coh_comm, self.d_batch.ptr, nb, self.base, self.d_tot.ptr + 80 * r,
+            self.d_notices.ptr + 8 * self.ncap * r, self.ncap)
         o = self.offs[r]
         if len(pages):
             self.data.twin(self.d_ids.ptr + 4 * o[0], n=len(pages))                         # 2
@@ -274,13 +303,8 @@ class MmultRankReplay:
         sids = [self.d_ids.ptr + 4 * o[1 + d] for d in range(self.P)]
         for d in range(self.P):                                                          # 3
             self.data.diff(sids[d], n=counts[d], out=self.send[d])  # n = 0: rec_off[0] = 0
-        if self.comm is not None:
-            exchange.exchange_runs(self.data, self.comm, self.send, sids, self.recv,
-                                   [b.ptr for b in self.rids])
-        else:
-            self.data.sync()
-            exchange.exchange_gloo(self.data, self.gloo, self.send,
-                                   [_Ptr(self.data, p) for p in sids], counts, self.rank)
+        exchange.exchange_runs(self.data, self.comm, self.send, sids, self.recv,
+                               [b.ptr for b in self.rids])
 
     def run(self) -> float:
         self.data.sync()
@@ -293,6 +317,16 @@ class MmultRankReplay:
         dt = time.perf_counter() - t0
         self.totals = self.d_tot.download(np.uint64, 10 * self.T.rounds).reshape(-1, 10).sum(0).astype(np.int64)
         return dt
+
+    def notices_of(self, r: int) -> np.ndarray:
+        """The notices this node received in round r (SPEC §5b), sorted by page."""
+        n = int(self.n_notices[r])
+        out = np.empty(n, np.uint64)
+        if n:
+            gdsm.check(gdsm.lib().gdsm_memcpy_d2h(self.pt.handle, out.ctypes.data,
+                                                  self.d_notices.ptr + 8 * self.ncap * r, 8 * n),
+                       "d2h")
+        return out
 
     def home_block(self) -> np.ndarray:
         """REPLICA pages [base, base + per) (this rank's home block)."""
@@ -310,22 +344,11 @@ class MmultRankReplay:
         return z[self.base * PAGE_SZ:(self.base + self.nh) * PAGE_SZ]
 
     def close(self):
-        if self.comm is not None:
-            self.comm.close()
+        for c in (self.comm, self.coh_comm):
+            if c is not None:
+                c.close()
+        self.comm = self.coh_comm = None
         for r in self.send + self.recv:
             r.free()
         self.data.close()
         self.pt.close()
-
-
-class _Ptr:
-    """A device pointer that downloads like a DeviceBuffer (exchange_gloo reads id lists)."""
-
-    def __init__(self, ctx, ptr):
-        self.ctx, self.ptr = ctx, ptr
-
-    def download(self, dtype, count):
-        out = np.empty(count, dtype=dtype)
-        gdsm.check(gdsm.lib().gdsm_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr,
-                                              out.nbytes), "d2h")
-        return out

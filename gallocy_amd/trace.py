@@ -161,6 +161,21 @@ class MmultTrace:
         # stable by page: rows stay in execution order, and inside a row R precedes W
         return ev[np.argsort(ev >> 4, kind="stable")]
 
+    def round_stamped(self, r: int) -> list:
+        """Per node t: its own events of round r as SPEC §5b stamped events (page << 36 | seq << 4
+        | node << 1 | rw), sorted. seq = 2 * (the row's position in the round's execution order)
+        + rw, a logical clock every node knows locally; merging all nodes' lists by (page, seq)
+        gives exactly round_events(r)."""
+        out = [np.zeros(0, np.uint64) for _ in range(self.P)]
+        for pos, (t, i) in enumerate(self.round_rows(r)):
+            rp, wp = self.row_sets(i)
+            e = np.concatenate([(rp.astype(np.uint64) << np.uint64(36))
+                                | np.uint64((2 * pos) << 4 | (t << 1)),
+                                (wp.astype(np.uint64) << np.uint64(36))
+                                | np.uint64((2 * pos + 1) << 4 | (t << 1) | 1)])
+            out[t] = np.sort(np.concatenate([out[t], e]))
+        return out
+
     def all_events(self) -> np.ndarray:
         """The whole trace as ONE page-sorted batch (per-page order = execution order)."""
         ev = np.concatenate([self.round_events(r) for r in range(self.rounds)])

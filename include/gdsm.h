@@ -68,7 +68,7 @@ enum gdsm_prof_stage {
   GDSM_PROF_NW_FILL,    /* GPU diff(): DP fill */
   GDSM_PROF_NW_TRACE,   /* GPU diff(): traceback + alignment strings */
   GDSM_PROF_EXCHANGE,   /* gdsm_exchange: the transfer of the record streams (RCCL group) */
-  GDSM_PROF_ROUTE,      /* gdsm_route_events / gdsm_route_notices: the transfer */
+  GDSM_PROF_ROUTE,      /* gdsm_route_events / gdsm_coherence_notify: the transfers */
   GDSM_PROF_STAGES
 };
 
@@ -378,9 +378,11 @@ int gdsm_route_events(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* events, ui
  *   bits 0-31 global page | 32-33 d's access before the batch | 34-35 d's access after |
  *   40-47 owner before | 48-55 owner after
  * with access 0 none, 1 read (d in the copyset), 2 write (EXCLUSIVE and d the owner); d gets one
- * iff its access changed or it is the old or the new owner of a page whose owner changed. All
- * ranks return -EINVAL if any home's batch was rejected by the fold, -ENOSPC if any node's cap is
- * too small. */
+ * iff its access changed or it is the old or the new owner of a page whose owner changed, so a
+ * node never gets more notices than there are distinct pages in all homes' batches: every rank
+ * returns -ENOSPC, before any page table changes, when some node's cap is below that count. All
+ * ranks return -EINVAL if any home's batch was rejected by the fold (that page table is then
+ * unspecified, as after a rejected gdsm_coherence_batch). */
 int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* batch, uint64_t n,
                           uint64_t base, uint64_t* totals_dev, uint64_t* notices, uint64_t cap,
                           uint64_t* n_notices);

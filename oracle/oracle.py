@@ -142,3 +142,44 @@ def bench_diff_apply(n, mode, ppm, seed, seconds, threads):
     if rc:
         raise OSError(-rc, "or_bench_diff_apply")
     return pages.value, dt.value, bool(ok.value)
+
+
+# ---------------------------------------------------------------- SPEC §5b (multi-GPU coherence)
+def _access(w, d):
+    """Node d's access to pages with state words w: 0 none, 1 read, 2 write (SPEC §5b)."""
+    w = np.asarray(w, np.uint32)
+    st = (w >> 16) & 3
+    held = ((w >> d) & 1).astype(bool) & (st != 0)
+    own = (st == 2) & (((w >> 8) & 0xFF) == d)
+    return np.where(held, np.where(own, 2, 1), 0).astype(np.uint64)
+
+
+def notices(pre, post, pages, n_nodes):
+    """Per node d < n_nodes: the notices (u64, SPEC §5b packing) for the pages `pages` (global
+    ids, ascending, unique) whose state words went from pre to post, sorted by page. Node d gets
+    one iff its access changed or it is the old or new owner of a page whose owner changed."""
+    pre = np.asarray(pre, np.uint32)
+    post = np.asarray(post, np.uint32)
+    pages = np.asarray(pages, np.uint64)
+    ob, oa = (pre >> 8) & 0xFF, (post >> 8) & 0xFF
+    out = []
+    for d in range(n_nodes):
+        ab, aa = _access(pre, d), _access(post, d)
+        m = (ab != aa) | ((ob != oa) & ((ob == d) | (oa == d)))
+        out.append((pages[m] | (ab[m] << np.uint64(32)) | (aa[m] << np.uint64(34))
+                    | (ob[m].astype(np.uint64) << np.uint64(40))
+                    | (oa[m].astype(np.uint64) << np.uint64(48))).astype(np.uint64))
+    return out
+
+
+def route_round(state, faults, stamped, n_nodes, total_pages):
+    """The multi-GPU protocol of SPEC §5b restated sequentially: the nodes' stamped events of one
+    batch merged by (page, seq), folded into the whole page table (state, faults updated in
+    place), and the notices each node receives. Returns (rc, totals, notices per node)."""
+    ev = np.sort(np.concatenate([np.asarray(s, np.uint64) for s in stamped]) if stamped
+                 else np.zeros(0, np.uint64), kind="stable")
+    plain = (((ev >> np.uint64(36)) << np.uint64(4)) | (ev & np.uint64(15))).astype(np.uint64)
+    pages = np.unique((plain >> np.uint64(4)).astype(np.int64))
+    pre = state[pages].copy()
+    rc, tot = coherence(state, faults, plain, n_nodes=n_nodes)
+    return rc, tot, notices(pre, state[pages], pages.astype(np.uint64), n_nodes)

@@ -5,7 +5,9 @@ oracle's fold of the whole trace on its pages, and the totals summed over ranks 
 oracle's.
 
     python -m torch.distributed.run --nproc-per-node 4 --master-addr 127.0.0.1 \\
-        scripts/rank_replay.py --ndim 1000 --transport gloo"""
+        scripts/rank_replay.py --ndim 1000
+
+One GPU per rank (RCCL); several ranks on one GPU: tests/test_gpu_replay.py (loopback)."""
 import argparse
 import json
 import os
@@ -21,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ndim", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--transport", choices=["rccl", "gloo"], default="gloo")
+    ap.add_argument("--transport", choices=["rccl"], default="rccl")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import torch
@@ -36,8 +38,13 @@ def main():
         dt = R.run()
         ok = bool(np.array_equal(R.home_block(), R.final_block()))
         st, fl = oracle.coh_init(R.Z, world)
-        rc, t = oracle.coherence(st, fl, R.T.all_events(), n_nodes=world)
-        ok &= rc == 0
+        acc = np.zeros(10, np.int64)
+        for r in range(R.T.rounds):
+            rc, t, want = oracle.route_round(st, fl, R.T.round_stamped(r), world, R.Z)
+            ok &= rc == 0 and bool(np.array_equal(R.notices_of(r), want[rank]))
+            acc += [t["invalidations"], t["transfers"], *t["node_faults"]]
+        t = {"invalidations": int(acc[0]), "transfers": int(acc[1]),
+             "node_faults": [int(x) for x in acc[2:]]}
         if R.nh:
             gst, gfl = R.pt.coh_download()
             ok &= bool(np.array_equal(gst[:R.nh], st[R.base:R.base + R.nh]))

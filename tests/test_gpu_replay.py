@@ -35,47 +35,71 @@ def test_mmult_replay_end_to_end(ndim, nodes, graph):
         R.close()
 
 
+def _check_rank_replays(Rs, world):
+    """Every home block equals the product zone; the page-table shards, the totals summed over
+    ranks and every node's notices of every round equal the oracle's sequential fold of the whole
+    trace (SPEC §5b, oracle.route_round)."""
+    T = Rs[0].T
+    st, fl = oracle.coh_init(Rs[0].Z, world)
+    acc = np.zeros(10, np.int64)
+    for r in range(T.rounds):
+        rc, t, want = oracle.route_round(st, fl, T.round_stamped(r), world, Rs[0].Z)
+        assert rc == 0
+        acc += [t["invalidations"], t["transfers"], *t["node_faults"]]
+        for R in Rs:
+            assert np.array_equal(R.notices_of(r), want[R.rank]), (r, R.rank)
+    assert np.sum([R.totals for R in Rs], axis=0).tolist() == acc.tolist()
+    for R in Rs:
+        assert np.array_equal(R.home_block(), R.final_block())
+        if R.nh:
+            gst, gfl = R.pt.coh_download()
+            assert np.array_equal(gst[:R.nh], st[R.base:R.base + R.nh])
+            assert np.array_equal(gfl[:R.nh], fl[R.base:R.base + R.nh])
+
+
 def test_rank_replay_single_rank_rccl():
     """Config 5 with one process per DSM node (gallocy_amd.replay.MmultRankReplay), here the
-    1-rank case on RCCL through gdsm_exchange: NDIM = 1000."""
+    1-rank case on RCCL (two communicators: page data, coherence): NDIM = 1000."""
     from gallocy_amd.replay import MmultRankReplay
     R = MmultRankReplay(0, 1, ndim=1000, seed=7)
     try:
         R.run()
-        assert np.array_equal(R.home_block(), R.final_block())
-        st, fl = oracle.coh_init(R.Z, 1)
-        rc, t = oracle.coherence(st, fl, R.T.all_events(), n_nodes=1)
-        assert rc == 0
-        gst, gfl = R.pt.coh_download()
-        assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
-        assert R.totals.tolist() == [t["invalidations"], t["transfers"], *t["node_faults"]]
+        _check_rank_replays([R], 1)
     finally:
         R.close()
 
 
-@pytest.mark.parametrize("ranks,ndim", [(2, 300), (4, 1000)])
-def test_rank_replay_multi_rank_rehearsal_gloo(ranks, ndim):
-    """MmultRankReplay with `ranks` processes sharing cuda:0, the exchange over gloo (RCCL cannot
-    put two ranks on one GPU): every rank's home block equals the product zone, its page-table
-    shard equals the oracle's fold of the whole trace on those pages, and the totals summed over
-    ranks equal the oracle's (scripts/rank_replay.py)."""
-    import json
-    import os
-    import socket
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
-           str(root / "scripts" / "rank_replay.py"), "--ndim", str(ndim), "--transport", "gloo"]
-    r = subprocess.run(cmd, cwd=root, env=dict(os.environ), capture_output=True, text=True,
-                       timeout=110)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
-    assert lines[0]["ok"] is True, lines[0]
+@pytest.mark.parametrize("ranks,ndim", [(2, 300), (3, 257), (4, 1000)])
+def test_rank_replay_multi_rank_loopback(ranks, ndim):
+    """MmultRankReplay with `ranks` DSM nodes as threads on cuda:0 over the loopback communicator:
+    every round routes each node's own fault events to the homes (gdsm_route_events), folds them
+    there and returns the notices (gdsm_coherence_notify), then ships the row writes' diffs to
+    the homes (gdsm_exchange) -- the multi-GPU code path, with device-to-device copies for the
+    moves."""
+    import threading
+
+    from gallocy_amd.replay import MmultRankReplay
+    Rs = [MmultRankReplay(r, ranks, ndim=ndim, seed=7, transport="loopback")
+          for r in range(ranks)]
+    try:
+        MmultRankReplay.wire_loopback(Rs)
+        errs = [None] * ranks
+
+        def body(r):
+            try:
+                Rs[r].run()
+            except BaseException as e:  # noqa: BLE001
+                errs[r] = e
+        th = [threading.Thread(target=body, args=(r,)) for r in range(ranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=110)
+        assert not any(t.is_alive() for t in th)
+        for e in errs:
+            if e is not None:
+                raise e
+        _check_rank_replays(Rs, ranks)
+    finally:
+        for R in Rs:
+            R.close()

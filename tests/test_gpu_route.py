@@ -1,0 +1,174 @@
+"""Coherence across GPUs on ONE GPU (docs/SPEC.md §5b): G ranks as threads, each a DSM node with its
+own page-table shard context on cuda:0, wired by the loopback communicator. Every batch goes
+through gdsm_route_events (nodes -> homes, merged by (page, seq)) and gdsm_coherence_notify (fold
++ notices back); the shards, the per-batch totals and every node's notices must equal the
+oracle's sequential fold of all nodes' events (oracle.route_round). Also: empty nodes, empty
+batches, and the collective refusals (-EINVAL for an unsorted list, -ENOSPC for a small buffer)
+returned on every rank with nothing moved."""
+import errno
+import threading
+
+import numpy as np
+import pytest
+
+import gallocy_amd as ga
+from gallocy_amd import exchange
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def run_ranks(G, fn):
+    errs = [None] * G
+
+    def body(r):
+        try:
+            fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+    th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=110)
+    assert not any(t.is_alive() for t in th), "a rank is stuck"
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+def stamped_batch(rng, G, Z, n_per_node, hot=0):
+    """Random stamped events per node: pages uniform (plus `hot` events on page 0 from every
+    node), seq = a global clock shuffled over the batch, 20 % writes."""
+    tot = n_per_node * G + hot * G
+    clock = rng.permutation(tot).astype(np.uint64)
+    out, k = [], 0
+    for t in range(G):
+        m = n_per_node + hot
+        pages = np.concatenate([rng.integers(0, Z, n_per_node), np.zeros(hot, np.int64)])
+        rw = (rng.random(m) < 0.2).astype(np.uint64)
+        seq = clock[k:k + m]
+        k += m
+        e = (pages.astype(np.uint64) << np.uint64(36)) | (seq << np.uint64(4)) \
+            | np.uint64(t << 1) | rw
+        out.append(np.sort(e))
+    return out
+
+
+class Shard:
+    def __init__(self, rank, G, Z):
+        self.per = -(-Z // G)
+        self.base = min(Z, rank * self.per)
+        self.nh = max(0, min(Z, self.base + self.per) - self.base)
+        self.ctx = ga.Context(max(1, self.nh), arenas=())
+        self.ctx.coh_init(G)
+        if self.nh:
+            self.ctx.coh_upload(np.full(self.nh, (1 << rank) | (rank << 8) | (2 << 16), np.uint32),
+                                np.zeros(self.nh, np.uint32))
+
+
+@pytest.mark.parametrize("G,Z,n,hot", [(2, 5000, 3000, 0), (3, 4099, 20000, 500), (4, 777, 4000, 0)])
+def test_route_notify_equal_sequential_fold(G, Z, n, hot):
+    rng = np.random.default_rng(G * 1000 + Z)
+    shards = [Shard(r, G, Z) for r in range(G)]
+    comms = exchange.Comm.loopback([s.ctx for s in shards])
+    gst, gfl = oracle.coh_init(Z, G)
+    try:
+        for batch in range(3):
+            # node 1 sends nothing in batch 1; batch 2 is empty on every node
+            stamped = stamped_batch(rng, G, Z, n if batch < 2 else 0, hot if batch < 2 else 0)
+            if batch == 1:
+                stamped[1] = stamped[1][:0]
+            rc_ref, tot_ref, want = oracle.route_round(gst, gfl, stamped, G, Z)
+            assert rc_ref == 0
+            got, tots, nb = [None] * G, [None] * G, [None] * G
+
+            def rank(r):
+                s, c = shards[r], comms[r]
+                ev = s.ctx.buffer(max(8, 8 * len(stamped[r]))).upload(stamped[r])
+                cap = sum(len(x) for x in stamped) + 1
+                bt = s.ctx.buffer(8 * cap)
+                nt = s.ctx.buffer(8 * (Z + 1))
+                tot = s.ctx.buffer(80)
+                nb[r] = exchange.route_events(s.ctx, c, ev.ptr, len(stamped[r]), Z, bt.ptr, cap)
+                k = exchange.coherence_notify(s.ctx, c, bt.ptr, nb[r], s.base, tot.ptr, nt.ptr,
+                                              Z + 1)
+                s.ctx.sync()
+                got[r] = nt.download(np.uint64, k) if k else np.zeros(0, np.uint64)
+                tots[r] = tot.download(np.uint64, 10).astype(np.int64)
+                for b in (ev, bt, nt, tot):
+                    b.free()
+            run_ranks(G, rank)
+            assert sum(nb) == sum(len(x) for x in stamped)
+            for r in range(G):
+                assert np.array_equal(got[r], want[r]), (batch, r, len(got[r]), len(want[r]))
+            assert np.sum(tots, axis=0).tolist() == [tot_ref["invalidations"],
+                                                     tot_ref["transfers"], *tot_ref["node_faults"]]
+        for r, s in enumerate(shards):
+            if s.nh:
+                st, fl = s.ctx.coh_download()
+                assert np.array_equal(st, gst[s.base:s.base + s.nh])
+                assert np.array_equal(fl, gfl[s.base:s.base + s.nh])
+    finally:
+        for c in comms:
+            c.close()
+        for s in shards:
+            s.ctx.close()
+
+
+def test_route_refusals_are_collective():
+    """One node's unsorted list: every rank gets -EINVAL from gdsm_route_events. One home's batch
+    buffer too small: every rank gets -ENOSPC. A notice buffer too small on one node: every rank
+    gets -ENOSPC from gdsm_coherence_notify. Afterwards the group still works."""
+    G, Z = 3, 3000
+    rng = np.random.default_rng(5)
+    shards = [Shard(r, G, Z) for r in range(G)]
+    comms = exchange.Comm.loopback([s.ctx for s in shards])
+    lib = ga.gdsm.lib()
+    try:
+        stamped = stamped_batch(rng, G, Z, 2000)
+        bad = stamped[2].copy()
+        bad[[10, 11]] = bad[[11, 10]]
+        rcs = {}
+
+        def call(r, evs, cap, ncap):
+            import ctypes as C
+            s, c = shards[r], comms[r]
+            ev = s.ctx.buffer(8 * len(evs[r])).upload(evs[r])
+            bt = s.ctx.buffer(8 * max(cap, 1))
+            nt = s.ctx.buffer(8 * max(ncap, 1))
+            tot = s.ctx.buffer(80)
+            nb, nn = C.c_uint64(0), C.c_uint64(0)
+            rc1 = lib.gdsm_route_events(s.ctx.handle, c.handle, ev.ptr, len(evs[r]), Z, bt.ptr,
+                                        cap, C.byref(nb))
+            rc2 = None
+            if rc1 == 0:
+                rc2 = lib.gdsm_coherence_notify(s.ctx.handle, c.handle, bt.ptr, nb.value, s.base,
+                                                tot.ptr, nt.ptr, ncap, C.byref(nn))
+            s.ctx.sync()
+            return rc1, rc2
+
+        def case(name, evs, caps, ncaps):
+            def rank(r):
+                rcs[(name, r)] = call(r, evs, caps[r], ncaps[r])
+            run_ranks(G, rank)
+            return [rcs[(name, r)] for r in range(G)]
+
+        big = 3 * 2000 + 1
+        assert case("unsorted", [stamped[0], stamped[1], bad], [big] * 3, [Z] * 3) == \
+            [(-errno.EINVAL, None)] * 3
+        assert case("small batch", stamped, [big, 10, big], [Z] * 3) == [(-errno.ENOSPC, None)] * 3
+        assert case("small notices", stamped, [big] * 3, [Z, Z, 1]) == [(0, -errno.ENOSPC)] * 3
+        assert case("ok", stamped, [big] * 3, [Z] * 3) == [(0, 0)] * 3
+        # the refusals changed nothing: the shards equal one sequential fold of the batch
+        gst, gfl = oracle.coh_init(Z, G)
+        assert oracle.route_round(gst, gfl, stamped, G, Z)[0] == 0
+        for s in shards:
+            st, fl = s.ctx.coh_download()
+            assert np.array_equal(st, gst[s.base:s.base + s.nh])
+            assert np.array_equal(fl, gfl[s.base:s.base + s.nh])
+    finally:
+        for c in comms:
+            c.close()
+        for s in shards:
+            s.ctx.close()
