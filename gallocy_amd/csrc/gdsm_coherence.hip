@@ -108,13 +108,9 @@ __device__ __forceinline__ uint32_t wave_incl_compose(uint32_t v) {
   return v;
 }
 
-// Segmented sum: bit 31 = "a segment starts in here", low bits = count since the last start.
-__device__ __forceinline__ uint32_t segsum(uint32_t a, uint32_t b) {
-  return ((b & kConst) ? (b & ~kConst) : ((a & ~kConst) + (b & ~kConst))) | ((a | b) & kConst);
-}
 
-// The same two scans on DPP (no LDS traffic): 0 is the identity of tcompose and of segsum,
-// and it is what an out-of-range or masked-off DPP source reads.
+// The compose scan on DPP (no LDS traffic): 0 is the identity of tcompose (and of segsum,
+// gdsm_common.h), and it is what an out-of-range or masked-off DPP source reads.
 __device__ __forceinline__ uint32_t wave_incl_compose_dpp(uint32_t v) {
   v = tcompose(dpp0<0x111>(v), v);
   v = tcompose(dpp0<0x112>(v), v);
@@ -122,15 +118,6 @@ __device__ __forceinline__ uint32_t wave_incl_compose_dpp(uint32_t v) {
   v = tcompose(dpp0<0x118>(v), v);
   v = tcompose(dpp0<0x142, 0xA>(v), v);
   v = tcompose(dpp0<0x143, 0xC>(v), v);
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_segsum_dpp(uint32_t v) {
-  v = segsum(dpp0<0x111>(v), v);
-  v = segsum(dpp0<0x112>(v), v);
-  v = segsum(dpp0<0x114>(v), v);
-  v = segsum(dpp0<0x118>(v), v);
-  v = segsum(dpp0<0x142, 0xA>(v), v);
-  v = segsum(dpp0<0x143, 0xC>(v), v);
   return v;
 }
 

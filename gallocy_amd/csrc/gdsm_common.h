@@ -56,6 +56,14 @@ __device__ __forceinline__ uint64_t lane_bcast64(uint64_t v, int lane) {
   return (uint64_t)lane_bcast((uint32_t)v, lane) | ((uint64_t)lane_bcast((uint32_t)(v >> 32), lane) << 32);
 }
 
+// A 64-bit value from lane `src` (both halves as unsigned dwords: __shfl returns int, and a
+// negative int widened to 64 bits would sign-extend into the high half).
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane_bcast(wave_incl_sum(v), 63); }
 
 // Value of lane l-1 (lane 0 gets 0) / of lane l+1 (lane 63 gets 0).
@@ -81,6 +89,23 @@ __device__ __forceinline__ uint32_t row_incl_max(uint32_t x) {
 __device__ __forceinline__ uint32_t row_last(uint32_t x) { return dpp0<0x15F>(x); }
 // Lane r-1 of the row (lane 0 of the row gets 0).
 __device__ __forceinline__ uint32_t row_prev(uint32_t x) { return dpp0<0x111>(x); }
+
+// Segmented sum: bit 31 = "a segment starts in here", low bits = the sum since the last start
+// (the sums stay below 2^31). 0 is the identity.
+constexpr uint32_t kSegStart = 1u << 31;
+__device__ __forceinline__ uint32_t segsum(uint32_t a, uint32_t b) {
+  return ((b & kSegStart) ? (b & ~kSegStart) : ((a & ~kSegStart) + (b & ~kSegStart))) |
+         ((a | b) & kSegStart);
+}
+__device__ __forceinline__ uint32_t wave_incl_segsum_dpp(uint32_t v) {
+  v = segsum(dpp0<0x111>(v), v);
+  v = segsum(dpp0<0x112>(v), v);
+  v = segsum(dpp0<0x114>(v), v);
+  v = segsum(dpp0<0x118>(v), v);
+  v = segsum(dpp0<0x142, 0xA>(v), v);
+  v = segsum(dpp0<0x143, 0xC>(v), v);
+  return v;
+}
 
 // Inclusive suffix minimum across lanes (lane l gets min over lanes >= l); bpermute based.
 __device__ __forceinline__ uint32_t wave_incl_suffix_min(uint32_t v) {

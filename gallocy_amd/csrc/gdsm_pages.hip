@@ -408,12 +408,20 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // kApply: the same runs are also applied to `target` (a home copy on this GPU, pages indexed by
 // the same ids): each dirty chunk's changed bytes, exactly the bytes its runs cover (SPEC §4),
 // are stored from the registers that found them, so the stream is not read back.
-template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply>
+// kSpill (bytes, 0 = none): when a record no longer fits the wave's LDS buffer, the buffer's
+// records are flushed to the wave's slot of a global spill pool and the buffer starts over, so a
+// unit holds kBuf + kSpill bytes of records before any page has to be re-read ("late"). The pool
+// has kSpillWGs workgroup slots (4 wave slots each); workgroup ticket t uses slot t % kSpillWGs
+// once the workgroup with ticket t - kSpillWGs has released it (a generation word per slot;
+// that workgroup drew its ticket earlier, so it is running or done and never waits for t).
+constexpr uint32_t kSpillWGs = 1280;  // > the workgroups of this kernel one MI355X holds at once
+
+template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, uint64_t n, uint64_t* __restrict__ rec_off,
     uint8_t* __restrict__ data, uint64_t cap, uint64_t* __restrict__ ws,
-    uint8_t* __restrict__ target) {
+    uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool) {
   static_assert(kU <= 64 && (kU & (kU - 1)) == 0, "unit size");
   __shared__ uint32_t sel_tab[16];
   __shared__ uint32_t ent_all[4][64];
@@ -430,11 +438,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   const uint64_t nunits = (n + kU - 1) / kU;
   // one ticket per workgroup (a single counter takes ~88 returning atomics per us, so per-wave
   // tickets would queue on it); unit = 4 * ticket + wave
-  __shared__ uint32_t ticket;
-  if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u);
+  __shared__ uint32_t ticket, done_waves;
+  if (threadIdx.x == 0) {
+    const uint32_t t = atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u);
+    ticket = t;
+    done_waves = 0;
+    if (kSpill && (uint64_t)t * 4 < nunits) {  // wait for the spill slot's previous user
+      const uint32_t want = t / kSpillWGs;
+      while (__hip_atomic_load(gen + t % kSpillWGs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+             want)
+        __builtin_amdgcn_s_sleep(2);
+    }
+  }
   __syncthreads();
   const uint64_t u = (uint64_t)ticket * 4 + wave;
   if (u >= nunits) return;  // wave-uniform: the grid's spare waves
+  uint32_t* slot = kSpill ? reinterpret_cast<uint32_t*>(
+                                pool + ((uint64_t)(ticket % kSpillWGs) * 4 + wave) * kSpill)
+                          : nullptr;
+  uint32_t spilled = 0;  // bytes of this wave's records flushed to its slot
   uint64_t* status = ws + 1;
   const uint64_t i0 = u * kU;
   const uint32_t cnt = (uint32_t)min((uint64_t)kU, n - i0);
@@ -466,7 +488,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
       load_page(twin, cur, pj, lane, t, c);
     }
     uint32_t size = 0;
-    const uint32_t src = acc;
+    uint32_t src = spilled + acc;  // logical offset: [0, spilled) in the slot, then LDS
     if (D > 64u) {
       size = record_size_masks(m, lane);
       late |= 1ull << j;
@@ -487,6 +509,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
       const uint32_t ps = from_prev_lane(wave_incl_max(ls));
       const uint32_t NR = tot & 0xFFFFu, NP = tot >> 16;
       size = 4u + 4u * NR + ((NP + 3u) & ~3u);
+      if (kSpill && acc + size > kBuf && spilled + acc <= kSpill) {
+        // the buffer is full: its records go to the slot (coalesced dword stores), then it starts
+        // over (every record with <= 64 dirty chunks fits an empty 8 KiB buffer)
+        for (uint32_t q = lane; q < acc / 4u; q += 64) slot[spilled / 4u + q] = buf[q];
+        wave_lds_sync();
+        spilled += acc;
+        acc = 0;
+        src = spilled;
+      }
       if (acc + size > kBuf) {
         late |= 1ull << j;
       } else {
@@ -554,14 +585,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   }
   wave_lds_sync();
   uint32_t* dst = reinterpret_cast<uint32_t*>(data + excl);
-  for (uint32_t g = lane; g < limit / 4u; g += 64) {
-    const uint32_t byte = 4u * g;
-    uint32_t j = 0;
+  if (!kSpill || spilled == 0) {
+    for (uint32_t g = lane; g < limit / 4u; g += 64) {
+      const uint32_t byte = 4u * g;
+      uint32_t j = 0;
 #pragma unroll
-    for (uint32_t step = kU / 2; step; step >>= 1)
-      if (tab[j + step] <= byte) j += step;
-    const uint32_t src = tab[kU + 1 + j];
-    if (src != 0xFFFFFFFFu) __builtin_nontemporal_store(buf[(src + byte - tab[j]) / 4u], dst + g);
+      for (uint32_t step = kU / 2; step; step >>= 1)
+        if (tab[j + step] <= byte) j += step;
+      const uint32_t src = tab[kU + 1 + j];
+      if (src != 0xFFFFFFFFu)
+        __builtin_nontemporal_store(buf[(src + byte - tab[j]) / 4u], dst + g);
+    }
+  } else {
+    // records from the slot and from LDS; four dwords per lane in flight. The slot is read at
+    // agent scope (past this CU's L1, which may hold the slot's previous user's lines).
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the flushes have landed
+    for (uint32_t g0 = 0; g0 < limit / 4u; g0 += 256) {
+      uint32_t v[4];
+      bool ok[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t g = g0 + 64 * q + lane;
+        const uint32_t byte = 4u * g;
+        uint32_t j = 0;
+#pragma unroll
+        for (uint32_t step = kU / 2; step; step >>= 1)
+          if (tab[j + step] <= byte) j += step;
+        const uint32_t src = tab[kU + 1 + j];
+        ok[q] = g < limit / 4u && src != 0xFFFFFFFFu;
+        const uint32_t lg = (src + byte - tab[j]) / 4u;  // logical dword
+        v[q] = 0;
+        if (ok[q])
+          v[q] = lg < spilled / 4u
+                     ? __hip_atomic_load(slot + lg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : buf[lg - spilled / 4u];
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q)
+        if (ok[q]) __builtin_nontemporal_store(v[q], dst + g0 + 64 * q + lane);
+    }
   }
   for (uint64_t rem = late; rem;) {  // wave-uniform
     const uint32_t j = (uint32_t)__builtin_ctzll(rem);
@@ -572,6 +634,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     PageRuns P;
     scan_page(t, c, lane, P);
     emit_bytes(P, c, lane, data + excl + tab[j]);
+  }
+  if (kSpill) {
+    // the last active wave of the workgroup hands the slot to ticket + kSpillWGs once every wave's
+    // slot reads have returned
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    uint32_t prev = 0;
+    if (lane == 0) prev = atomicAdd(&done_waves, 1u);
+    prev = lane_bcast(prev, 0);
+    const uint32_t active = (uint32_t)min((uint64_t)4, nunits - (uint64_t)ticket * 4);
+    if (prev + 1 == active && lane == 0)
+      __hip_atomic_store(gen + ticket % kSpillWGs, ticket / kSpillWGs + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -806,42 +880,313 @@ __global__ __launch_bounds__(256) void apply_kernel(uint8_t* __restrict__ target
   if (kMode == 1 && sink == 0x9E3779B9u) atomicOr(err, 2u);
 }
 
+// 16 payload bytes starting at LDS byte offset q (4-B aligned base `pay32`): five aligned dword
+// reads and four funnel shifts.
+__device__ __forceinline__ u32x4 lds_load16(const uint32_t* __restrict__ pay32, uint32_t q) {
+  const uint32_t i = q >> 2, sh = (q & 3u) * 8u;
+  const uint32_t w0 = pay32[i], w1 = pay32[i + 1], w2 = pay32[i + 2], w3 = pay32[i + 3],
+                 w4 = pay32[i + 4];
+  if (!sh) return (u32x4){w0, w1, w2, w3};
+  return (u32x4){__builtin_amdgcn_alignbit(w1, w0, sh), __builtin_amdgcn_alignbit(w2, w1, sh),
+                 __builtin_amdgcn_alignbit(w3, w2, sh), __builtin_amdgcn_alignbit(w4, w3, sh)};
+}
+
+// One 16-B destination chunk per lane (where `valid`): bytes [lo, hi) of the chunk at `dst`
+// (16-B aligned), their payload at LDS byte offset q (the byte for lo). The wave stores
+//   whole chunks with one 16-B store, chunks whose bytes are one aligned 8-B half with one 8-B
+//   store, and every other chunk's bytes 16 lanes per chunk, four chunks per step,
+// so no lane walks a byte mask on its own while the others wait (a partial chunk among 64 made
+// every lane of the old per-lane mask walk pay for it).
+__device__ __forceinline__ void store_chunks_wave(bool valid, uint8_t* dst, uint32_t lo,
+                                                  uint32_t hi, const uint32_t* __restrict__ pay32,
+                                                  uint32_t q) {
+  const bool full = valid && lo == 0 && hi == 16;
+  const bool half = valid && (hi - lo) == 8 && (lo & 7u) == 0;
+  if (full) {
+    *reinterpret_cast<u32x4*>(dst) = lds_load16(pay32, q);
+  } else if (half) {
+    const u32x4 v = lds_load16(pay32, q);
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<u32x2*>(dst + lo) = (u32x2){v.x, v.y};
+  }
+  uint64_t G = __ballot(valid && !full && !half);
+  const uint32_t lane = lane_id(), r = lane >> 4, b = lane & 15u;
+  const uint8_t* pay8 = reinterpret_cast<const uint8_t*>(pay32);
+  while (G) {  // wave-uniform
+    // the four lowest remaining chunks, one per 16-lane row
+    uint32_t own[4];
+    uint64_t g = G;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      own[k] = g ? (uint32_t)__builtin_ctzll(g) : 64u;
+      g &= g ? g - 1 : 0ull;
+    }
+    G = g;
+    const uint32_t o = r == 0 ? own[0] : r == 1 ? own[1] : r == 2 ? own[2] : own[3];
+    const uint32_t os = o < 64u ? o : 0u;
+    const uint64_t d = shfl64((uint64_t)(uintptr_t)dst, (int)os);
+    const uint32_t l2 = (uint32_t)__shfl((int)lo, (int)os, 64);
+    const uint32_t h2 = (uint32_t)__shfl((int)hi, (int)os, 64);
+    const uint32_t q2 = (uint32_t)__shfl((int)q, (int)os, 64);
+    if (o < 64u && b >= l2 && b < h2)
+      *reinterpret_cast<__attribute__((address_space(1))) uint8_t*>((uintptr_t)d + b) =
+          pay8[q2 + b - l2];
+  }
+}
+
+// ---- apply, flat form (long lists): a wave stages a window of records in LDS as above, then
+// works on the window's RUNS, one lane per run, instead of on records row by row:
+//   records  lane per record: header checks and a lane-serial walk over its run headers (sorted,
+//            in the page, sizes adding up: SPEC §4), exclusive scan of the run counts;
+//   runs     64 at a time, lane q = the window's run q: its record by a 6-step search over the
+//            records' run offsets, its header, its payload offset (segmented scan of the lengths
+//            within the record), then its 16-B chunks spread over the wave by a search over the
+//            batch's chunk offsets (consecutive lanes, consecutive chunks of a run), or lane by
+//            lane when every run of the batch spans at most two chunks.
+// A malformed record writes nothing (its runs are dropped after the record walk); a record
+// larger than the window goes through apply_rows from global memory, as in apply_kernel.
+constexpr uint32_t kChunkMap = 512;  // chunks of one run batch mapped through LDS (else: search)
+
+template <uint32_t kWin>
+__global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ target,
+                                                         const uint32_t* __restrict__ ids,
+                                                         uint64_t n,
+                                                         const uint64_t* __restrict__ rec_off,
+                                                         const uint8_t* __restrict__ data,
+                                                         uint32_t* __restrict__ err) {
+  // +4 dwords: an unaligned payload read of the window's last bytes stays inside the buffer
+  __shared__ __attribute__((aligned(16))) uint32_t win_all[4][kWin / 4 + 4];
+  __shared__ uint4 ri_all[4][64];  // per record of the window: LDS offset, runs, first run, page
+  __shared__ uint4 rp_all[4][64];  // per run of a batch: page, off | end << 16, payload offset
+  __shared__ uint8_t cm_all[4][kChunkMap];  // chunk -> run of the batch
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, row = lane >> 4;
+  uint32_t* win = win_all[wave];
+  uint4* ri = ri_all[wave];
+  uint4* rp = rp_all[wave];
+  uint8_t* cm = cm_all[wave];
+  const uint64_t ntask = (n + 63) / 64;
+  uint32_t bad = 0, sink = 0;
+  for (uint64_t task = (uint64_t)blockIdx.x * 4 + wave; task < ntask;
+       task += (uint64_t)gridDim.x * 4) {
+    const uint64_t a = task * 64;
+    const uint32_t cnt = (uint32_t)min((uint64_t)64, n - a);
+    const uint64_t my_off = rec_off[a + min(lane, cnt)];  // lane l: start of record a+l
+    const uint64_t end_off = rec_off[a + cnt];
+    const uint32_t my_page = lane < cnt ? (ids ? ids[a + lane] : (uint32_t)(a + lane)) : 0u;
+    uint32_t j = 0;
+    while (j < cnt) {
+      const uint64_t start = lane_bcast64(my_off, j);
+      const bool fits = lane > j && lane <= cnt && (my_off - start) <= kWin;
+      const uint64_t fm = __ballot(fits);
+      uint32_t k = fm ? 63u - (uint32_t)__clzll(fm) : j;
+      if (cnt == 64 && (end_off - start) <= kWin) k = 64;
+      if (k == j) {  // record j alone exceeds the window: straight from global, row 0 only
+        const uint64_t r1 = (j + 1 < 64) ? lane_bcast64(my_off, j + 1) : end_off;
+        const uint32_t p = lane_bcast(my_page, j);
+        const uint8_t* rec = data + start;
+        const bool has = row == 0 && r1 > start;
+        if (!apply_rows<0>(target + (uint64_t)p * kPage, reinterpret_cast<const uint32_t*>(rec),
+                           rec, (uint32_t)(r1 - start), has, sink))
+          bad = 1;
+        ++j;
+        continue;
+      }
+      const uint64_t stop = (k == 64) ? end_off : lane_bcast64(my_off, k);
+      const uint32_t words = (uint32_t)((stop - start) >> 2);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(data + start);
+      for (uint32_t q0 = 0; q0 < words; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        __builtin_amdgcn_global_load_lds(
+            (__attribute__((address_space(1))) void*)(src + (q < words ? q : 0)),
+            (__attribute__((address_space(3))) void*)(win + q0), 4, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed
+      wave_lds_sync();
+
+      // ---- records: lane l = record j + l of the window
+      const uint32_t nrec = k - j;
+      const bool inrec = lane < nrec;
+      const uint32_t r = min(j + lane, 63u);
+      const uint64_t o0 = __shfl(my_off, (int)r, 64);
+      const uint64_t o1n = __shfl(my_off, (int)min(r + 1, 63u), 64);
+      const uint64_t o1 = (j + lane + 1 == k) ? stop : o1n;
+      const uint32_t rs = inrec ? (uint32_t)(o0 - start) : 0u;
+      const uint32_t size = inrec ? (uint32_t)(o1 - o0) : 0u;
+      uint32_t nr = size ? win[rs / 4] : 0u;
+      bool rbad = size && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr);
+      if (rbad) nr = 0;
+      if (nr) {  // the record's run headers, lane-serially: sorted, inside the page, sizes add up
+        uint32_t prev_end = 0, tot = 0;
+        for (uint32_t i = 0; i < nr; ++i) {
+          const uint32_t h = win[rs / 4 + 1 + i];
+          const uint32_t off = h & 0xFFFFu, len = h >> 16;
+          if (len == 0 || off + len > kPage || off < prev_end) rbad = true;
+          prev_end = off + len;
+          tot += len;
+        }
+        if (size != 4u + 4u * nr + ((tot + 3u) & ~3u)) rbad = true;
+        if (rbad) nr = 0;
+      }
+      bad |= rbad ? 1u : 0u;
+      const uint32_t rinc = wave_incl_sum(nr);
+      const uint32_t RB = rinc - nr;                 // the record's first run in the window
+      const uint32_t NRW = lane_bcast(rinc, 63);     // runs in the window
+      const uint32_t RBs = inrec ? RB : 0xFFFFFFFFu;  // search key (records past the window: never)
+      ri[lane] = make_uint4(rs, nr, RB, __shfl(my_page, (int)r, 64));
+      wave_lds_sync();
+
+      // ---- runs: 64 at a time
+      uint32_t carry_sum = 0;  // payload bytes of the previous batch's last record so far
+      for (uint32_t q0 = 0; q0 < NRW; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool vq = q < NRW;
+        uint32_t pos = 0;
+#pragma unroll
+        for (uint32_t st = 32; st; st >>= 1) {
+          const uint32_t c = (uint32_t)__shfl((int)RBs, (int)(pos + st), 64);
+          if (c <= q) pos += st;
+        }
+        const uint4 R = ri[pos];  // .x LDS offset, .y runs, .z first run, .w page
+        const uint32_t i = q - R.z;
+        const uint32_t h = vq ? win[R.x / 4 + 1 + i] : 0u;
+        const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
+        // payload offset: lengths summed within the record (segments start at a record's run 0)
+        const uint32_t sg = wave_incl_segsum_dpp(len | ((vq && i == 0) ? kSegStart : 0u));
+        const uint32_t incl = (sg & ~kSegStart) + ((sg & kSegStart) ? 0u : carry_sum);
+        const uint32_t pp = R.x + 4u + 4u * R.y + incl - len;
+        carry_sum = lane_bcast(incl, 63);
+        const uint32_t nch = len ? ((end - 1u) >> 4) - (off >> 4) + 1u : 0u;
+        const uint32_t M = lane_bcast(wave_incl_max(nch), 63);
+        uint8_t* page = target + (uint64_t)R.w * kPage;
+        if (M <= 2) {
+          // short runs (word-sized edits): each lane stores its own run's one or two chunks
+          for (uint32_t c = 0; c < M; ++c) {
+            const uint32_t cs = ((off >> 4) + c) << 4;
+            const uint32_t lo = max(off, cs), hi = min(end, cs + 16u);
+            store_chunks_wave(c < nch, page + cs, lo - cs, hi - cs, win, pp + (lo - off));
+          }
+        } else {
+          // the batch's (run, chunk) pairs spread over the wave, 64 per step: consecutive lanes
+          // store consecutive chunks of a run, so one store instruction writes whole segments
+          // (lane-per-run stores, 16 B into 64 different runs per instruction, measured 1.3x
+          // slower on clustered records)
+          const uint32_t cinc = wave_incl_sum(nch), cex = cinc - nch;
+          const uint32_t T = lane_bcast(cinc, 63);
+          if (T <= kChunkMap) {
+            // chunk -> run through LDS: each run writes its index over its chunks' slots and its
+            // parameters once; a chunk lane then needs two LDS reads (a 6-step search over the
+            // runs' chunk offsets was 6 dependent ds_bpermute round trips per 64 chunks)
+            if (vq) rp[lane] = make_uint4(R.w, off | (end << 16), pp, cex);
+            for (uint32_t c = 0; c < M; ++c)
+              if (c < nch) cm[cex + c] = (uint8_t)lane;
+            wave_lds_sync();
+            for (uint32_t g0 = 0; g0 < T; g0 += 64) {
+              const uint32_t g = g0 + lane;
+              const uint4 P = rp[cm[g < T ? g : 0]];
+              const uint32_t oi = P.y & 0xFFFFu, ei = P.y >> 16;
+              const uint32_t cs = ((oi >> 4) + (g - P.w)) << 4;
+              const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
+              store_chunks_wave(g < T, target + (uint64_t)P.x * kPage + cs, lo - cs, hi - cs, win,
+                                P.z + (lo - oi));
+            }
+            wave_lds_sync();  // the next batch rewrites rp / cm
+            continue;
+          }
+          for (uint32_t g0 = 0; g0 < T; g0 += 64) {
+            const uint32_t g = g0 + lane;
+            uint32_t p2 = 0;
+#pragma unroll
+            for (uint32_t st = 32; st; st >>= 1) {
+              const uint32_t c = (uint32_t)__shfl((int)cex, (int)(p2 + st), 64);
+              if (c <= g) p2 += st;
+            }
+            const uint32_t oi = (uint32_t)__shfl((int)off, (int)p2, 64);
+            const uint32_t ei = (uint32_t)__shfl((int)end, (int)p2, 64);
+            const uint32_t pi = (uint32_t)__shfl((int)pp, (int)p2, 64);
+            const uint32_t ci = (uint32_t)__shfl((int)cex, (int)p2, 64);
+            const uint32_t wi = (uint32_t)__shfl((int)R.w, (int)p2, 64);
+            const uint32_t cs = ((oi >> 4) + (g - ci)) << 4;
+            const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
+            store_chunks_wave(g < T, target + (uint64_t)wi * kPage + cs, lo - cs, hi - cs, win,
+                              pi + (lo - oi));
+          }
+        }
+      }
+      wave_lds_sync();
+      j = k;
+    }
+  }
+  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 1u);
+  (void)sink;  // apply_rows<0> leaves it alone (measurement builds only)
+}
+
 // ------------------------------------------------------------------------- launchers
 // Diff geometry, gdsm_tune("diff_variant", v) or GDSM_DIFF_VARIANT=v; every variant writes the
 // same canonical stream (tests/test_gpu_pages.py checks each):
 //   0  automatic (default): 2 pages per wave for short lists (n <= 32768: a wave walks its
 //      pages one after the other, so a few dozen pages must not share one wave), else 64 pages
-//      per wave when the caller's stream capacity allows at most 128 B per page (sparse writes:
-//      config 2's ~66 B records; 64 records fill the 8 KiB buffer; fewest look-backs), else 32
-//      pages per wave up to 384 B per page, else 16
+//      per wave with a 24 KiB spill slot per wave (variant 5), whatever the stream's capacity;
+//      a raw caller whose workspace predates the spill pool gets the capacity-based choice of
+//      round 2 (64 / 32 / 16 pages at <= 128 / 384 / more bytes of capacity per page)
 //   1  16 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 //   2  32 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 //   3  2 pages per wave
-//   4  64 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
+//   4  64 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD (no spill)
+//   5  64 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
 // Measurement-only kernels (invalid output) are not part of the library.
-// Process-wide and atomic: a launch on any thread reads one consistent value.
 static int diff_variant_from_env() {
   const char* e = getenv("GDSM_DIFF_VARIANT");
   const int v = e ? atoi(e) : 0;
-  return (v >= 0 && v <= 4) ? v : 0;
+  return (v >= 0 && v <= 5) ? v : 0;
 }
 static std::atomic<int> g_diff_variant{diff_variant_from_env()};
 static int diff_variant() { return g_diff_variant.load(std::memory_order_relaxed); }
+// Apply geometry, gdsm_tune("apply_variant", v) or GDSM_APPLY_VARIANT=v (same output):
+//   0  default: long lists (> 16384 records) the flat form (apply_flat_kernel: the window's runs
+//      64 at a time, chunks spread over the wave) with a 4 KiB window; short lists apply_kernel
+//      with 4 records per task and a 12 KiB window
+//   1  long lists: apply_kernel (records row by row), 8 KiB window (round 2's default)
+//   2  long lists: apply_kernel, 4 KiB window
+//   3  long lists: flat form, 8 KiB window
+//   4  long lists: flat form, 2 KiB window
+// Same-box, 2M clustered pages (config-3 shard): 0.79 ms (1) -> 0.64 (2) -> 0.55 (0); config 2:
+// 0.250 -> 0.241 ms.
+constexpr int kApplyVariants = 5;
+static int apply_variant_from_env() {
+  const char* e = getenv("GDSM_APPLY_VARIANT");
+  const int v = e ? atoi(e) : 0;
+  return (v >= 0 && v < kApplyVariants) ? v : 0;
+}
+static std::atomic<int> g_apply_variant{apply_variant_from_env()};
+
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 4) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 5) {
     g_diff_variant.store((int)value, std::memory_order_relaxed);
+    return 0;
+  }
+  if (!strcmp(key, "apply_variant") && value >= 0 && value < kApplyVariants) {
+    g_apply_variant.store((int)value, std::memory_order_relaxed);
     return 0;
   }
   return coh_tune(key, value);
 }
 
 // Single-pass diff workspace: the ticket counter and one status granule per unit of the
-// smallest geometry that n may take (2 pages up to kDiffShort, else 16), non-decreasing in n so
-// a workspace reserved for n fits every shorter list.
+// smallest geometry that n may take (2 pages up to kDiffShort, else 16), then the spill pool of
+// the 64-page geometry (a generation word per workgroup slot, then kSpillWGs or
+// fewer workgroup slots of 4 x kDiffSpill bytes). Non-decreasing in n, so a workspace reserved
+// for n fits every shorter list.
 constexpr uint64_t kDiffShort = 32768;
+constexpr uint32_t kDiffSpill = 24576;
+static inline uint64_t up256(uint64_t v) { return (v + 255) & ~255ull; }
+static uint64_t spill_pool_bytes(uint64_t n) {
+  const uint64_t wgs = ((n + 63) / 64 + 3) / 4;
+  return (uint64_t)(wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill;
+}
 uint64_t diff_workspace_bytes(uint64_t n) {
   const uint64_t u16 = (n + 15) / 16, u2 = (min(n, kDiffShort) + 1) / 2;
-  return 8 * (1 + max(u16, u2)) + 64;
+  const uint64_t base = 8 * (1 + max(u16, u2)) + 64;
+  return up256(base) + up256(4 * (uint64_t)kSpillWGs) + spill_pool_bytes(n);
 }
 
 static inline unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap) {
@@ -901,24 +1246,36 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   int v = diff_variant();
-  if (v == 0) v = n <= kDiffShort ? 3 : (cap <= 128 * n) ? 4 : (cap <= 384 * n) ? 2 : 1;
-  const uint32_t U = v == 4 ? 64 : v == 3 ? 2 : v == 2 ? 32 : 16;
+  // the spill pool's place in the workspace (after the largest status area n may need)
+  const uint64_t status_end = up256(8 * (1 + max((n + 15) / 16, (min(n, kDiffShort) + 1) / 2)) + 64);
+  const uint64_t pool_at = status_end + up256(4 * (uint64_t)kSpillWGs);
+  const bool pool_ok = ws_bytes >= pool_at + spill_pool_bytes(n);
+  if (v == 0)
+    v = n <= kDiffShort ? 3 : pool_ok ? 5 : (cap <= 128 * n) ? 4 : (cap <= 384 * n) ? 2 : 1;
+  if (v == 5 && !pool_ok) return hipErrorInvalidValue;
+  const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : v == 2 ? 32 : 16;
   const uint64_t nunits = (n + U - 1) / U;
   if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
-  // ticket counter + status granules, zeroed per launch (outside the timed kernel)
+  // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
+  // (outside the timed kernel)
   hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
+  if (e == hipSuccess && v == 5) e = hipMemsetAsync(ws + status_end, 0, 4 * kSpillWGs, s);
   if (e != hipSuccess) return e;
+  uint32_t* gen = v == 5 ? reinterpret_cast<uint32_t*>(ws + status_end) : nullptr;
+  uint8_t* pool = v == 5 ? ws + pool_at : nullptr;
   ProfScope ps(prof, GDSM_PROF_DIFF, s);
-  auto kern = target ? (v == 4   ? diff_single_kernel<64, 8192, 4, true>
+  auto kern = target ? (v == 5   ? diff_single_kernel<64, 8192, 4, true, kDiffSpill>
+                       : v == 4 ? diff_single_kernel<64, 8192, 4, true>
                        : v == 3 ? diff_single_kernel<2, 8192, 4, true>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, true>
                                 : diff_single_kernel<16, 8192, 4, true>)
-                     : (v == 4   ? diff_single_kernel<64, 8192, 4, false>
+                     : (v == 5   ? diff_single_kernel<64, 8192, 4, false, kDiffSpill>
+                       : v == 4 ? diff_single_kernel<64, 8192, 4, false>
                        : v == 3 ? diff_single_kernel<2, 8192, 4, false>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, n,
-                     rec_off, data, cap, reinterpret_cast<uint64_t*>(ws), target);
+                     rec_off, data, cap, reinterpret_cast<uint64_t*>(ws), target, gen, pool);
   return hipGetLastError();
 }
 
@@ -932,7 +1289,18 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
   // few dense records are spread over waves instead of queueing in one
   const bool short_list = n <= 16384;
   const uint32_t per_task = short_list ? 4u : 64u;
-  auto kern = short_list ? apply_kernel<0, kApplyWinShort> : apply_kernel<0, kApplyWinLong>;
+  const int av = g_apply_variant.load(std::memory_order_relaxed);
+  if (!short_list && (av == 0 || av >= 3)) {
+    auto kf = av == 0 ? apply_flat_kernel<4096>
+              : av == 3 ? apply_flat_kernel<8192>
+                        : apply_flat_kernel<2048>;
+    hipLaunchKernelGGL(kf, dim3(grid_for(n, 4 * 64, 65536)), dim3(256), 0, s, target, ids, n,
+                       rec_off, data, err);
+    return hipGetLastError();
+  }
+  auto kern = short_list ? apply_kernel<0, kApplyWinShort>
+              : av == 2  ? apply_kernel<0, 4096>
+                         : apply_kernel<0, kApplyWinLong>;
   hipLaunchKernelGGL(kern, dim3(grid_for(n, 4 * per_task, 65536)), dim3(256), 0, s, target, ids,
                      n, rec_off, data, err, per_task);
   return hipGetLastError();

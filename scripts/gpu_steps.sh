@@ -15,6 +15,6 @@ for spec in "$@"; do
   echo "=== $name rc=$rc"
   tail -n 4 "$OUT/$name.out"
   if [ $rc -ne 0 ]; then tail -n 15 "$OUT/$name.err"; fi
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 done
 echo "=== done"

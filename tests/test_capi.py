@@ -93,12 +93,19 @@ def test_no_gpu_is_reported_not_crashed():
 
 
 def test_workspace_sizing():
-    """gdsm_diff_workspace_bytes(n) for the single-pass diff."""
+    """gdsm_diff_workspace_bytes(n) for the single-pass diff: a ticket counter and one 8-B
+    look-back granule per 16 pages, then the 64-page geometry's spill pool (a generation word per
+    workgroup slot, up to 1280 workgroup slots of 4 x 24 KiB); non-decreasing in n."""
     from gallocy_amd import _lib
     lib = _lib.load()
-    # single-pass diff: a ticket counter and one 8-B look-back granule per 16 pages
-    assert lib.gdsm_diff_workspace_bytes(1) >= 16
-    assert lib.gdsm_diff_workspace_bytes(1 << 24) == 8 * (1 + (1 << 20)) + 64
+    up = lambda v: (v + 255) // 256 * 256  # noqa: E731
+    slots = lambda n: min(1280, ((n + 63) // 64 + 3) // 4)  # noqa: E731
+    for n in (1, 1000, 1 << 20, 1 << 24):
+        want = up(8 * (1 + max((n + 15) // 16, (min(n, 32768) + 1) // 2)) + 64) + up(4 * 1280) \
+            + slots(n) * 4 * 24576
+        assert lib.gdsm_diff_workspace_bytes(n) == want, n
+    sizes = [lib.gdsm_diff_workspace_bytes(n) for n in range(1, 200000, 997)]
+    assert sizes == sorted(sizes)
 
 
 CALLER = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "legacy_caller"
@@ -123,10 +130,10 @@ def test_tune_rejects_measurement_only_variants():
     from gallocy_amd import _lib
     L = _lib.load()
     for key, bad in ((b"coh_variant", 1), (b"coh_variant", 2), (b"coh_variant", 3),
-                     (b"diff_variant", 5),
-                     (b"apply_variant", 1), (b"no_such_knob", 0)):
+                     (b"diff_variant", 6),
+                     (b"apply_variant", 9), (b"no_such_knob", 0)):
         assert L.gdsm_tune(key, bad) == -22, (key, bad)
     for key, ok in ((b"diff_variant", 1), (b"diff_variant", 2), (b"diff_variant", 3),
-                    (b"diff_variant", 4), (b"coh_variant", 0)):
+                    (b"diff_variant", 4), (b"diff_variant", 5), (b"coh_variant", 0)):
         assert L.gdsm_tune(key, ok) == 0
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0

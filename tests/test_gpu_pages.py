@@ -507,11 +507,12 @@ def _lds_overflow_pages(rng, n):
     return tw, cu
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_diff_variants_bit_exact(variant, golden):
-    """Every diff geometry (gdsm_tune "diff_variant": automatic, 16, 32, 2 or 64 pages per wave) is
-    bit-exact on edge pages, random byte densities (pages past the 64-dirty-chunk fast path),
-    records that overflow the wave's LDS buffer, and clustered and uniform synthetic writes."""
+    """Every diff geometry (gdsm_tune "diff_variant": automatic, 16, 32, 2 or 64 pages per wave,
+    64 pages per wave with the global spill slot) is bit-exact on edge pages, random byte
+    densities (pages past the 64-dirty-chunk fast path), records that overflow the wave's LDS
+    buffer (and, for 5, its spill slot), and clustered and uniform synthetic writes."""
     L = _lib.load()
     assert L.gdsm_tune(b"diff_variant", variant) == 0
     try:
@@ -565,7 +566,7 @@ def test_c1_windows_pinned_by_reference_diff(golden):
         assert zlib.crc32(rep[w].tobytes()) == int(g["crc"][w][1]), w
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_diff_apply_fused_equals_diff_then_apply(variant, golden):
     """gdsm_diff_apply (the diff kernel also applying the runs to a home copy on this GPU) writes
     the same stream as gdsm_diff, and leaves the target exactly as gdsm_apply of that stream
@@ -636,3 +637,99 @@ def test_diff_apply_config2_full_size():
         rc = L.gdsm_diff_raw(c.arena_ptr("replica"), c.arena_ptr("current"), None, n,
                              chk.s.rec_off, chk.s.data, chk.cap, ws.ptr, ws.nbytes, c.stream)
         assert rc == 0 and chk.total() == 0
+
+
+def _long_list_apply_case(rng, n):
+    """A stream of n > 16384 records (the long-list apply path) mixing every record shape: clean
+    pages, 1 % words, clustered 64-B runs, dense random bytes, alternating bytes (many runs), a
+    few long runs, whole-page runs, records larger than a 4 or 8 KiB staging window; and some
+    malformed records (bad run count, unsorted / overlapping / empty / past-the-page runs, a size
+    that does not add up), which must write nothing while the rest is applied."""
+    tw = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    cu = tw.copy()
+    kinds = rng.integers(0, 9, n)
+    for i in np.flatnonzero(kinds == 1):  # 1 % of 8-B words
+        w = np.flatnonzero(rng.random(512) < 0.01)
+        cu[i].reshape(512, 8)[w] ^= 0x11
+    for i in np.flatnonzero(kinds == 2):  # clustered: 10 % of 64-B clusters
+        c = np.flatnonzero(rng.random(64) < 0.1)
+        cu[i].reshape(64, 64)[c] ^= 0x77
+    for i in np.flatnonzero(kinds == 3):  # dense random bytes
+        m = rng.random(4096) < 0.3
+        cu[i, m] ^= 0x0F
+    for i in np.flatnonzero(kinds == 4):  # alternating bytes over part of the page
+        o = int(rng.integers(0, 2048))
+        cu[i, o:o + 1500:2] ^= 0xA5
+    for i in np.flatnonzero(kinds == 5):  # a few long runs
+        for _ in range(3):
+            o = int(rng.integers(0, 3000))
+            cu[i, o:o + int(rng.integers(100, 1000))] ^= 0xFF
+    for i in np.flatnonzero(kinds == 6):  # the whole page
+        cu[i] ^= 0x01
+    for i in np.flatnonzero(kinds == 7):  # > 8 KiB records: alternating bytes everywhere
+        cu[i, ::2] ^= 0x3C
+    ro, data = oracle.diff_pages(tw, cu)
+    data = data.copy()
+    w = data.view("<u4")
+    dirty = np.flatnonzero(np.diff(ro))
+    bad = rng.choice(dirty, 40, replace=False)
+    for t, i in enumerate(bad):
+        b = int(ro[i]) // 4
+        nr = int(w[b])
+        kind = t % 6
+        if kind == 0:
+            w[b] = 5000                              # run count past 2048
+        elif kind == 1 and nr >= 2:                  # unsorted runs
+            w[b + 1], w[b + 2] = w[b + 2], w[b + 1]
+        elif kind == 2:                              # empty run
+            w[b + 1] = w[b + 1] & 0xFFFF
+        elif kind == 3:                              # past the page end
+            w[b + 1] = 4095 | (int(w[b + 1] >> 16) + 2 << 16)
+        elif kind == 4 and nr >= 2:                  # overlapping runs
+            o0, l0 = int(w[b + 1] & 0xFFFF), int(w[b + 1] >> 16)
+            o1, l1 = int(w[b + 2] & 0xFFFF), int(w[b + 2] >> 16)
+            w[b + 2] = (o0 + l0 - 1) | (l1 << 16) if o0 + l0 - 1 < o1 else w[b + 2]
+            if not o0 + l0 - 1 < o1:
+                w[b] = 5000
+        else:                                        # sizes do not add up
+            w[b + 1] = (w[b + 1] & 0xFFFF) | ((int(w[b + 1] >> 16) + 4) << 16)
+    rc = oracle.apply(tw.copy(), ro, data)  # the oracle stops at the first malformed record
+    want = tw.copy()
+    for i in np.flatnonzero(np.diff(ro)):   # the GPU applies every well-formed one (SPEC §4)
+        one = data[int(ro[i]):int(ro[i + 1])]
+        oracle.apply(want, np.array([0, len(one)], np.uint64), one, ids=np.array([i], np.uint32))
+    return tw, ro, data, want, rc
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_apply_variants_long_lists(variant):
+    """Every apply geometry on a long list (gdsm_tune "apply_variant": flat with a 4 KiB window
+    (default), records by rows with an 8 or 4 KiB window, flat with an 8 or 2 KiB window) leaves
+    REPLICA exactly as the oracle's apply of the same stream, malformed records included (nothing
+    of them written, -EINVAL at sync)."""
+    L = _lib.load()
+    rng = np.random.default_rng(900 + variant)
+    n = 20000
+    tw, ro, data, want, rc = _long_list_apply_case(rng, n)
+    assert rc == -22
+    assert L.gdsm_tune(b"apply_variant", variant) == 0
+    try:
+        with ga.Context(n) as c:
+            c.upload("replica", tw)
+            r = Runs.from_host(c, HostRuns(ro, data))
+            c.apply(r)
+            with pytest.raises(GdsmError) as ei:
+                c.sync()
+            assert ei.value.errno == 22
+            got = c.download("replica")
+            diffp = np.flatnonzero((got != want).any(axis=1))
+            assert len(diffp) == 0, diffp[:10]
+            # a permuted id list through the same path
+            perm = rng.permutation(n).astype(np.uint32)
+            ro2, data2 = oracle.diff_pages(tw[perm], want[perm])
+            c.upload("replica", tw)
+            c.apply(Runs.from_host(c, HostRuns(ro2, data2)), "replica", c.ids(perm))
+            c.sync()
+            assert np.array_equal(c.download("replica"), want)
+    finally:
+        L.gdsm_tune(b"apply_variant", 0)
