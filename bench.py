@@ -189,7 +189,7 @@ def read_traffic(pages: int, mode: str, ppm: int, fused: bool):
     from the newest committed PMC summary that measured it on this workload
     (profiles/*traffic*.json, scripts/gpu_prof.sh), else None. Summaries without a workload tag
     are for the default config-2 workload."""
-    suffix = ", true>" if fused else ", false>"
+    flag = ", true" if fused else ", false"  # the kApply template argument
     default = {"pages": 1 << 20, "mode": "uniform", "ppm": 10000}
     for p in sorted((ROOT / "profiles").glob("*traffic*.json"), reverse=True):
         try:
@@ -197,7 +197,7 @@ def read_traffic(pages: int, mode: str, ppm: int, fused: bool):
         except Exception:  # noqa: BLE001
             continue
         if (str(j.get("diff_kernel", "")).startswith(DIFF_KERNEL)
-                and str(j.get("diff_kernel", "")).endswith(suffix)
+                and flag in str(j.get("diff_kernel", ""))
                 and j.get("workload", default) == {"pages": pages, "mode": mode, "ppm": ppm}):
             return j.get("diff_kernel_bytes_per_launch"), p.name
     return None, None

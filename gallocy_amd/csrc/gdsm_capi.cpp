@@ -77,6 +77,10 @@ int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const ui
   return 0;
 }
 
+void note_density(gdsm_ctx* ctx, uint64_t bytes, uint64_t pages) {
+  if (pages) ctx->diff_bpp = (uint32_t)(bytes / pages > 0xFFFFFFFEull ? 0xFFFFFFFEull : bytes / pages) + 1;
+}
+
 int check_and_clear_err(gdsm_ctx* ctx) {
   uint32_t h = 0;
   GDSM_TRY(hipMemcpyAsync(&h, ctx->err, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -569,7 +573,8 @@ static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* 
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
-                             ctx->stream, ctx->P(), target >= 0 ? ctx->arena[target] : nullptr));
+                             ctx->stream, ctx->P(), target >= 0 ? ctx->arena[target] : nullptr,
+                             ctx->diff_bpp));
   return 0;
 }
 
@@ -591,6 +596,7 @@ int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total) {
   GDSM_TRY(hipMemcpyAsync(&t, runs->rec_off + runs->n, 8, hipMemcpyDeviceToHost, ctx->stream));
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
   *total = t;
+  if (runs->n > kDiffShortList) note_density(ctx, t, runs->n);
   return t > runs->cap ? -ENOSPC : 0;
 }
 

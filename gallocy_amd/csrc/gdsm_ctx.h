@@ -24,6 +24,7 @@ struct gdsm_ctx {
   uint64_t* coh_pt = nullptr;      // page table: state | faults << 32 per page
   uint64_t* coh_totals = nullptr;  // device 10 x u64
   uint32_t n_nodes = 0;
+  uint32_t diff_bpp = 0;         // stream bytes per page the host last learned (diff geometry)
   std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks
   // gdsm_apply_async: applies run on `aux`, ordered after everything enqueued on `stream` before
   // them; every other operation joins `aux` first, except gdsm_diff, which only waits for the
@@ -82,6 +83,11 @@ int ensure_aux(gdsm_ctx* ctx);
 // A caller's device id list checked against the arenas on stream `which` (0 main, 1 aux).
 int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const uint32_t** out);
 int check_and_clear_err(gdsm_ctx* ctx);
+// Records the stream density (bytes / pages) the host learned, for the diff's geometry choice
+// (stored + 1, so 0 stays "unknown"). Lists of at most kDiffShortList pages take the short-list
+// geometry anyway and do not count.
+constexpr uint64_t kDiffShortList = 32768;
+void note_density(gdsm_ctx* ctx, uint64_t bytes, uint64_t pages);
 
 struct DeviceGuard {
   int prev = -1;

@@ -499,9 +499,11 @@ int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* c, const gdsm_runs* send,
     if (rc) return rc;
     GDSM_TRY(hipMemcpyAsync(h, c->cnt_dev, 32 * G, hipMemcpyDeviceToHost, s));
     GDSM_TRY(hipStreamSynchronize(s));
-    uint64_t too_small = 0;
+    uint64_t too_small = 0, sent_bytes = 0, sent_recs = 0;
     for (int d = 0; d < G; ++d) {
       sb[d] = h[2 * d + 1];
+      sent_bytes += sb[d];
+      sent_recs += send[d].n;
       too_small |= sb[d] > send[d].cap;  // that diff overflowed its stream (-ENOSPC)
       if (d == me) continue;
       rn[d] = h[2 * G + 2 * d];
@@ -509,6 +511,7 @@ int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* c, const gdsm_runs* send,
       const uint64_t ncap = recv[d].n_cap ? recv[d].n_cap : recv[d].n;
       too_small |= rn[d] > ncap || rb[d] > recv[d].cap;
     }
+    if (sent_recs / G > kDiffShortList) note_density(ctx, sent_bytes, sent_recs);
     // every rank must agree before anyone posts a send
     rc = xp->agree_max(&too_small, s);
     if (rc) return rc;

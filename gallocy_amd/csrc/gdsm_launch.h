@@ -19,11 +19,12 @@ hipError_t launch_gen_pages(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint6
 hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        hipStream_t s, Prof* prof = nullptr);
 // Full diff of n pages in one pass: rec_off[n+1], data[cap]. With `target`, the runs are also
-// applied to target (same page ids) by the same kernel.
+// applied to target (same page ids) by the same kernel. bpp_hint: stream bytes per page the
+// caller saw last time (0 = unknown); it only picks the geometry.
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr,
-                       uint8_t* target = nullptr);
+                       uint8_t* target = nullptr, uint32_t bpp_hint = 0);
 hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         const uint64_t* rec_off, const uint8_t* data, uint32_t* err,
                         hipStream_t s, Prof* prof = nullptr);

@@ -584,45 +584,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     limit = lane_bcast(wave_incl_max(fits ? incl : 0u), 63);
   }
   wave_lds_sync();
+  // The buffered records between two late pages are contiguous both in the wave's logical stream
+  // (slot, then LDS) and in the output: each such run of records is one dword copy, no per-dword
+  // record search.
   uint32_t* dst = reinterpret_cast<uint32_t*>(data + excl);
-  if (!kSpill || spilled == 0) {
-    for (uint32_t g = lane; g < limit / 4u; g += 64) {
-      const uint32_t byte = 4u * g;
-      uint32_t j = 0;
+  // (the slot is read at agent scope: past this CU's L1, which may hold lines of the slot's
+  // previous user)
+  if (kSpill && spilled) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the flushes landed
+  const uint64_t all = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull);
+  for (uint64_t rest = all & ~late; rest;) {  // wave-uniform
+    const uint32_t j0 = (uint32_t)__builtin_ctzll(rest);
+    const uint64_t above = j0 < 63 ? late & ~((2ull << j0) - 1ull) : 0ull;
+    const uint32_t j1 = above ? (uint32_t)__builtin_ctzll(above) : cnt;  // first late page after
+    rest = j1 >= 64 ? 0ull : rest & ~((1ull << j1) - 1ull);
+    const uint32_t o0 = tab[j0], o1 = min(tab[j1], limit);
+    if (o1 <= o0) continue;
+    const uint32_t s0 = tab[kU + 1 + j0] / 4u, d0 = o0 / 4u, nd = (o1 - o0) / 4u;
+    if (!kSpill || spilled == 0) {
+      for (uint32_t g = lane; g < nd; g += 64) __builtin_nontemporal_store(buf[s0 + g], dst + d0 + g);
+    } else {
+      const uint32_t sp = spilled / 4u;
+      for (uint32_t g0 = 0; g0 < nd; g0 += 256) {  // four dwords per lane in flight
+        uint32_t v[4];
 #pragma unroll
-      for (uint32_t step = kU / 2; step; step >>= 1)
-        if (tab[j + step] <= byte) j += step;
-      const uint32_t src = tab[kU + 1 + j];
-      if (src != 0xFFFFFFFFu)
-        __builtin_nontemporal_store(buf[(src + byte - tab[j]) / 4u], dst + g);
-    }
-  } else {
-    // records from the slot and from LDS; four dwords per lane in flight. The slot is read at
-    // agent scope (past this CU's L1, which may hold the slot's previous user's lines).
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the flushes have landed
-    for (uint32_t g0 = 0; g0 < limit / 4u; g0 += 256) {
-      uint32_t v[4];
-      bool ok[4];
+        for (uint32_t q = 0; q < 4; ++q) {
+          const uint32_t g = g0 + 64 * q + lane, lg = s0 + g;
+          v[q] = 0;
+          if (g < nd)
+            v[q] = lg < sp ? __hip_atomic_load(slot + lg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : buf[lg - sp];
+        }
 #pragma unroll
-      for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t g = g0 + 64 * q + lane;
-        const uint32_t byte = 4u * g;
-        uint32_t j = 0;
-#pragma unroll
-        for (uint32_t step = kU / 2; step; step >>= 1)
-          if (tab[j + step] <= byte) j += step;
-        const uint32_t src = tab[kU + 1 + j];
-        ok[q] = g < limit / 4u && src != 0xFFFFFFFFu;
-        const uint32_t lg = (src + byte - tab[j]) / 4u;  // logical dword
-        v[q] = 0;
-        if (ok[q])
-          v[q] = lg < spilled / 4u
-                     ? __hip_atomic_load(slot + lg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                     : buf[lg - spilled / 4u];
+        for (uint32_t q = 0; q < 4; ++q)
+          if (g0 + 64 * q + lane < nd) __builtin_nontemporal_store(v[q], dst + d0 + g0 + 64 * q + lane);
       }
-#pragma unroll
-      for (uint32_t q = 0; q < 4; ++q)
-        if (ok[q]) __builtin_nontemporal_store(v[q], dst + g0 + 64 * q + lane);
     }
   }
   for (uint64_t rem = late; rem;) {  // wave-uniform
@@ -1124,20 +1119,25 @@ __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ t
 // Diff geometry, gdsm_tune("diff_variant", v) or GDSM_DIFF_VARIANT=v; every variant writes the
 // same canonical stream (tests/test_gpu_pages.py checks each):
 //   0  automatic (default): 2 pages per wave for short lists (n <= 32768: a wave walks its
-//      pages one after the other, so a few dozen pages must not share one wave), else 64 pages
-//      per wave with a 24 KiB spill slot per wave (variant 5), whatever the stream's capacity;
-//      a raw caller whose workspace predates the spill pool gets the capacity-based choice of
-//      round 2 (64 / 32 / 16 pages at <= 128 / 384 / more bytes of capacity per page)
+//      pages one after the other, so a few dozen pages must not share one wave); longer lists by
+//      the density the context last saw (gdsm_runs_total, a sized exchange): <= kDense64 B/page
+//      64 pages with the spill slot (5), <= kDense16 16 pages (1), beyond 16 pages with the spill
+//      slot (7); density unknown: 64 pages with the spill slot (5), correct and fast at any
+//      density but 14 % behind 16 pages on dense clustered pages. Never the caller's capacity,
+//      except for a raw caller whose workspace predates the spill pool (round 2's rule:
+//      64 / 32 / 16 pages at <= 128 / 384 / more bytes of capacity per page)
 //   1  16 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 //   2  32 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD
 //   3  2 pages per wave
 //   4  64 pages per wave, 8 KiB LDS record buffer per wave, 4 waves/SIMD (no spill)
 //   5  64 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
+//   6  32 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
+//   7  16 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
 // Measurement-only kernels (invalid output) are not part of the library.
 static int diff_variant_from_env() {
   const char* e = getenv("GDSM_DIFF_VARIANT");
   const int v = e ? atoi(e) : 0;
-  return (v >= 0 && v <= 5) ? v : 0;
+  return (v >= 0 && v <= 7) ? v : 0;
 }
 static std::atomic<int> g_diff_variant{diff_variant_from_env()};
 static int diff_variant() { return g_diff_variant.load(std::memory_order_relaxed); }
@@ -1160,7 +1160,7 @@ static int apply_variant_from_env() {
 static std::atomic<int> g_apply_variant{apply_variant_from_env()};
 
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 5) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 7) {
     g_diff_variant.store((int)value, std::memory_order_relaxed);
     return 0;
   }
@@ -1178,9 +1178,15 @@ int tune(const char* key, int64_t value) {
 // for n fits every shorter list.
 constexpr uint64_t kDiffShort = 32768;
 constexpr uint32_t kDiffSpill = 24576;
+// Densities (stream bytes per page) the automatic geometry switches at: up to kDense64, 64 pages
+// per wave (their records fill the 8 KiB buffer at 128 B); up to kDense16, 16 pages (8 KiB / 16
+// = 512 B fit without spilling); beyond, 16 pages with the spill slot. Measured, 1M pages:
+// 1 % words (66 B/page) 64 pages 1.40 ms vs 16 pages 1.50; clustered 10 % (442 B/page) 16 pages
+// 1.56-1.66 ms vs 64 pages with the spill slot 1.79-1.93 (the spill's write and read-back).
+constexpr uint32_t kDense64 = 112, kDense16 = 480;
 static inline uint64_t up256(uint64_t v) { return (v + 255) & ~255ull; }
-static uint64_t spill_pool_bytes(uint64_t n) {
-  const uint64_t wgs = ((n + 63) / 64 + 3) / 4;
+static uint64_t spill_pool_bytes(uint64_t n) {  // sized for the smaller spill unit (32 pages)
+  const uint64_t wgs = ((n + 31) / 32 + 3) / 4;
   return (uint64_t)(wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill;
 }
 uint64_t diff_workspace_bytes(uint64_t n) {
@@ -1243,33 +1249,45 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
 
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
-                       uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target) {
+                       uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target,
+                       uint32_t bpp_hint) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   int v = diff_variant();
   // the spill pool's place in the workspace (after the largest status area n may need)
   const uint64_t status_end = up256(8 * (1 + max((n + 15) / 16, (min(n, kDiffShort) + 1) / 2)) + 64);
   const uint64_t pool_at = status_end + up256(4 * (uint64_t)kSpillWGs);
   const bool pool_ok = ws_bytes >= pool_at + spill_pool_bytes(n);
-  if (v == 0)
-    v = n <= kDiffShort ? 3 : pool_ok ? 5 : (cap <= 128 * n) ? 4 : (cap <= 384 * n) ? 2 : 1;
-  if (v == 5 && !pool_ok) return hipErrorInvalidValue;
-  const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : v == 2 ? 32 : 16;
+  if (v == 0) {
+    if (n <= kDiffShort)
+      v = 3;
+    else if (bpp_hint)  // the density this context saw last: sparse -> 64 pages, denser -> 16
+      v = bpp_hint <= kDense64 ? (pool_ok ? 5 : 4) : bpp_hint <= kDense16 || !pool_ok ? 1 : 7;
+    else  // unknown density: 64 pages with the spill slot, valid at any density
+      v = pool_ok ? 5 : (cap <= 128 * n) ? 4 : (cap <= 384 * n) ? 2 : 1;
+  }
+  const bool spill = v >= 5;
+  if (spill && !pool_ok) return hipErrorInvalidValue;
+  const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : (v == 2 || v == 6) ? 32 : 16;
   const uint64_t nunits = (n + U - 1) / U;
   if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
   // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
   // (outside the timed kernel)
   hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
-  if (e == hipSuccess && v == 5) e = hipMemsetAsync(ws + status_end, 0, 4 * kSpillWGs, s);
+  if (e == hipSuccess && spill) e = hipMemsetAsync(ws + status_end, 0, 4 * kSpillWGs, s);
   if (e != hipSuccess) return e;
-  uint32_t* gen = v == 5 ? reinterpret_cast<uint32_t*>(ws + status_end) : nullptr;
-  uint8_t* pool = v == 5 ? ws + pool_at : nullptr;
+  uint32_t* gen = spill ? reinterpret_cast<uint32_t*>(ws + status_end) : nullptr;
+  uint8_t* pool = spill ? ws + pool_at : nullptr;
   ProfScope ps(prof, GDSM_PROF_DIFF, s);
   auto kern = target ? (v == 5   ? diff_single_kernel<64, 8192, 4, true, kDiffSpill>
+                       : v == 6 ? diff_single_kernel<32, 8192, 4, true, kDiffSpill>
+                       : v == 7 ? diff_single_kernel<16, 8192, 4, true, kDiffSpill>
                        : v == 4 ? diff_single_kernel<64, 8192, 4, true>
                        : v == 3 ? diff_single_kernel<2, 8192, 4, true>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, true>
                                 : diff_single_kernel<16, 8192, 4, true>)
                      : (v == 5   ? diff_single_kernel<64, 8192, 4, false, kDiffSpill>
+                       : v == 6 ? diff_single_kernel<32, 8192, 4, false, kDiffSpill>
+                       : v == 7 ? diff_single_kernel<16, 8192, 4, false, kDiffSpill>
                        : v == 4 ? diff_single_kernel<64, 8192, 4, false>
                        : v == 3 ? diff_single_kernel<2, 8192, 4, false>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>

@@ -99,7 +99,7 @@ def test_workspace_sizing():
     from gallocy_amd import _lib
     lib = _lib.load()
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
-    slots = lambda n: min(1280, ((n + 63) // 64 + 3) // 4)  # noqa: E731
+    slots = lambda n: min(1280, ((n + 31) // 32 + 3) // 4)  # noqa: E731
     for n in (1, 1000, 1 << 20, 1 << 24):
         want = up(8 * (1 + max((n + 15) // 16, (min(n, 32768) + 1) // 2)) + 64) + up(4 * 1280) \
             + slots(n) * 4 * 24576
@@ -130,10 +130,11 @@ def test_tune_rejects_measurement_only_variants():
     from gallocy_amd import _lib
     L = _lib.load()
     for key, bad in ((b"coh_variant", 1), (b"coh_variant", 2), (b"coh_variant", 3),
-                     (b"diff_variant", 6),
+                     (b"diff_variant", 8),
                      (b"apply_variant", 9), (b"no_such_knob", 0)):
         assert L.gdsm_tune(key, bad) == -22, (key, bad)
     for key, ok in ((b"diff_variant", 1), (b"diff_variant", 2), (b"diff_variant", 3),
-                    (b"diff_variant", 4), (b"diff_variant", 5), (b"coh_variant", 0)):
+                    (b"diff_variant", 4), (b"diff_variant", 5), (b"diff_variant", 6), (b"diff_variant", 7),
+                    (b"coh_variant", 0)):
         assert L.gdsm_tune(key, ok) == 0
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0
