@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 // ---------------------------------------------------------------- launchers
 // Coherence variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = the single-pass fold
 // (coh_fold_kernel), the only one in the product library. Measurement builds (-DGDSM_MEASURE,
-// scripts/build_measure.sh) add 1 = the round-2 four-pass path (tail aggregates, scan, block pass
+// scripts/dev/build_measure.sh) add 1 = the round-2 four-pass path (tail aggregates, scan, block pass
 // C) for same-box A/B, and (output invalid) 2 / 3 = the four-pass path without page-table stores
 // / without any page-table traffic; 4 / 5 / 6 = the fold without its walk / without its
 // look-back / without the ordered look-back.

@@ -68,6 +68,9 @@ void or_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_pag
  * replica equals its current arena. Returns 0, -12 (allocation) or -22. */
 int or_bench_diff_apply(uint64_t n, int mode, uint32_t ppm, uint64_t seed, double seconds,
                         int threads, uint64_t* pages, double* elapsed, int* ok);
+int or_bench_coherence(const uint64_t* events, const uint64_t* page_off, uint64_t n_pages,
+                       uint32_t n_nodes, double seconds, int threads, uint64_t* done,
+                       double* elapsed);
 
 #ifdef __cplusplus
 }

@@ -58,3 +58,47 @@ int or_bench_diff_apply(uint64_t n, int mode, uint32_t ppm, uint64_t seed, doubl
   *ok = all_ok && !failed;
   return failed ? -12 : 0;
 }
+
+/* Batched coherence (or_coherence, docs/SPEC.md §5) over `threads` disjoint page ranges of one
+ * sorted batch: thread t folds the events of pages [t*n_pages/threads, (t+1)*n_pages/threads)
+ * (its slice of `page_off`, the batch's per-page event offsets) into the shared page table,
+ * repeatedly for `seconds`. Pages never cross threads, so the fold is the sequential one. */
+int or_bench_coherence(const uint64_t* events, const uint64_t* page_off, uint64_t n_pages,
+                       uint32_t n_nodes, double seconds, int threads, uint64_t* done,
+                       double* elapsed) {
+  if (n_pages == 0 || threads < 1) return -22;
+  uint32_t* state = malloc(n_pages * sizeof(uint32_t));
+  uint32_t* faults = malloc(n_pages * sizeof(uint32_t));
+  if (!state || !faults) {
+    free(state);
+    free(faults);
+    return -12;
+  }
+  or_coh_init(state, faults, n_pages, n_nodes);
+  uint64_t total = 0;
+  double slowest = 0.0;
+  int failed = 0;
+#pragma omp parallel num_threads(threads) reduction(+ : total) reduction(max : slowest) \
+    reduction(|| : failed)
+  {
+    const uint64_t t = (uint64_t)omp_get_thread_num(), nt = (uint64_t)omp_get_num_threads();
+    const uint64_t p0 = t * n_pages / nt, p1 = (t + 1) * n_pages / nt;
+    const uint64_t e0 = page_off[p0], ne = page_off[p1] - e0;
+    uint64_t tot[10], reps = 0;
+    double dt = 0.0;
+#pragma omp barrier
+    const double t0 = omp_get_wtime();
+    do {
+      if (or_coherence(state, faults, n_pages, n_nodes, events + e0, ne, tot)) failed = 1;
+      ++reps;
+      dt = omp_get_wtime() - t0;
+    } while (dt < seconds && !failed);
+    total = reps * ne;
+    slowest = dt;
+  }
+  free(state);
+  free(faults);
+  *done = total;
+  *elapsed = slowest;
+  return failed ? -22 : 0;
+}

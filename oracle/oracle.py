@@ -37,6 +37,8 @@ def lib():
         L.or_bench_diff_apply.argtypes = [u64, C.c_int, C.c_uint32, u64, C.c_double, C.c_int,
                                           C.POINTER(u64), C.POINTER(C.c_double),
                                           C.POINTER(C.c_int)]
+        L.or_bench_coherence.argtypes = [C.c_void_p, C.c_void_p, u64, C.c_uint32, C.c_double,
+                                         C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -142,6 +144,22 @@ def bench_diff_apply(n, mode, ppm, seed, seconds, threads):
     if rc:
         raise OSError(-rc, "or_bench_diff_apply")
     return pages.value, dt.value, bool(ok.value)
+
+
+def bench_coherence(counts, events, seconds, threads, n_nodes=8):
+    """bench.py's coherence CPU baseline: `threads` OpenMP threads, each folding the events of its
+    own contiguous page range of the batch (page counts `counts`) for `seconds` (timed in C).
+    Returns (events folded, seconds)."""
+    counts = np.ascontiguousarray(counts, np.uint64)
+    offs = np.zeros(len(counts) + 1, np.uint64)
+    np.cumsum(counts, out=offs[1:])
+    ev = np.ascontiguousarray(events, np.uint64)
+    done, dt = C.c_uint64(), C.c_double()
+    rc = lib().or_bench_coherence(_p(ev), _p(offs), len(counts), n_nodes, seconds, threads,
+                                  C.byref(done), C.byref(dt))
+    if rc:
+        raise OSError(-rc, "or_bench_coherence")
+    return done.value, dt.value
 
 
 # ---------------------------------------------------------------- SPEC §5b (multi-GPU coherence)

@@ -3,14 +3,14 @@
 line): per-stage times from HIP events; the batch totals and the final page table must agree
 between variants (the page table is re-initialised before every batch).
 
-    python scripts/ab_coh.py [events] [zipf|uniform] [variants, e.g. 0,1]"""
+    python scripts/dev/ab_coh.py [events] [zipf|uniform] [variants, e.g. 0,1]"""
 import statistics
 import sys
 from pathlib import Path
 
 import numpy as np
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 from gallocy_amd.workloads import event_counts  # noqa: E402

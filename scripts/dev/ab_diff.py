@@ -1,14 +1,14 @@
 """In-process A/B of diff kernel variants (interleaved rounds, one device): per-launch time of
 diff_pages_kernel from HIP events, for BASELINE config 2 (1M pages, 1 % word writes).
 
-    python scripts/ab_diff.py diff_variant 0,1,2
+    python scripts/dev/ab_diff.py diff_variant 0,1,2
 
 Every variant produces the same canonical stream; the totals are checked to agree."""
 import statistics
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 

@@ -2,12 +2,12 @@
 diff alone, apply alone (re-applying the same stream is idempotent), and the serial step
 diff -> apply, so that the cost one kernel leaves to the next shows up.
 
-    AB_MODE=clustered python scripts/ab_step.py"""
+    AB_MODE=clustered python scripts/dev/ab_step.py"""
 import statistics
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 

@@ -1,13 +1,13 @@
 """Apply kernel alone on one workload (re-applying the same stream is idempotent), for rocprofv3
 PMC passes and same-box A/B of apply variants (gdsm_tune "apply_variant").
 
-    APPLY_MODE=clustered APPLY_PAGES=2097152 APPLY_VARIANTS=0,1 python scripts/apply_only.py"""
+    APPLY_MODE=clustered APPLY_PAGES=2097152 APPLY_VARIANTS=0,1 python scripts/dev/apply_only.py"""
 import os
 import statistics
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 

@@ -2,7 +2,7 @@
 # Measurement build of libgdsm (-DGDSM_MEASURE: kernel variants with invalid output, selectable
 # through gdsm_tune) into gallocy_amd/lib_x/; load it with GDSM_LIB=gallocy_amd/lib_x/libgdsm.so.
 set -eu
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gallocy_amd/lib_x
 objs=()
 for s in gallocy_amd/csrc/*.hip gallocy_amd/csrc/*.cpp; do

@@ -2,7 +2,7 @@
 # Stamp build of libgdsm (-DGDSM_COH_STAMPS: kernel variants with invalid output, selectable
 # through gdsm_tune) into gallocy_amd/lib_st/; load it with GDSM_LIB=gallocy_amd/lib_st/libgdsm.so.
 set -eu
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gallocy_amd/lib_st
 objs=()
 for s in gallocy_amd/csrc/*.hip gallocy_amd/csrc/*.cpp; do

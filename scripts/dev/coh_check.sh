@@ -14,6 +14,6 @@ step() {  # name, timeout, cmd...
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 step tests 900 python -u -m pytest tests/test_gpu_coherence.py -x -v --timeout 300 --timeout-method thread ${COH_K:+-k "$COH_K"}
-step ab_uniform 600 python -u scripts/ab_coh.py 1073741824 uniform 0,1
-step ab_zipf 600 python -u scripts/ab_coh.py 1073741824 zipf 0,1
+step ab_uniform 600 python -u scripts/dev/ab_coh.py 1073741824 uniform 0,1
+step ab_zipf 600 python -u scripts/dev/ab_coh.py 1073741824 zipf 0,1
 echo "=== done"

@@ -1,15 +1,15 @@
 """Debug aid for the coherence fold kernel (needs the -DGDSM_COH_STAMPS build,
-scripts/build_stamps.sh, loaded with GDSM_LIB=gallocy_amd/lib_st/libgdsm.so): per-wave phase
+scripts/dev/build_stamps.sh, loaded with GDSM_LIB=gallocy_amd/lib_st/libgdsm.so): per-wave phase
 durations (s_memtime ticks) of every 16th block on a config-4 batch, split by block kind.
 
-    python scripts/coh_fold_stamps.py [events] [zipf|uniform]"""
+    python scripts/dev/coh_fold_stamps.py [events] [zipf|uniform]"""
 import ctypes as C
 import sys
 from pathlib import Path
 
 import numpy as np
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 from gallocy_amd.workloads import event_counts  # noqa: E402

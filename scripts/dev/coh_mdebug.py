@@ -2,13 +2,13 @@
 1..40 events over 1..3 pages) through the GPU and the oracle and saves the smallest batch whose
 results differ to gpurun_out/coh_min.npz.
 
-    python scripts/coh_mdebug.py [variant] [trials]"""
+    python scripts/dev/coh_mdebug.py [variant] [trials]"""
 import sys
 from pathlib import Path
 
 import numpy as np
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 from oracle import oracle  # noqa: E402

@@ -3,7 +3,7 @@
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import gallocy_amd as ga  # noqa: E402
 from gallocy_amd import gdsm  # noqa: E402
 from gallocy_amd.workloads import event_counts  # noqa: E402

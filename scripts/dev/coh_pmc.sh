@@ -11,7 +11,7 @@ for v in ${COH_PMC_VARIANTS:-0}; do
   for d in ${COH_PMC_DISTS:-uniform}; do
     for p in a b c; do
       case $p in a) CT=$A;; b) CT=$B;; c) CT=$C;; esac
-      timeout -s KILL 90 rocprofv3 --pmc $CT --kernel-trace -d $OUT/$p$v$d -o $p --output-format csv -- python3 scripts/coh_pmc.py 268435456 $d $v > $OUT/$p$v$d.log 2>&1 || exit 1
+      timeout -s KILL 90 rocprofv3 --pmc $CT --kernel-trace -d $OUT/$p$v$d -o $p --output-format csv -- python3 scripts/dev/coh_pmc.py 268435456 $d $v > $OUT/$p$v$d.log 2>&1 || exit 1
     done
   done
 done

@@ -21,6 +21,6 @@ if [ -n "${DEV_BENCH:-1}" ]; then
   step bench_unfused 300 python -u bench.py --steps 20 --warmup 3 --no-cpu --fuse off
 fi
 if [ -n "${DEV_PMC:-}" ]; then
-  COH_PMC_VARIANTS=0 bash scripts/coh_pmc.sh > $OUT/cohpmc.log 2>&1; echo "cohpmc rc=$?"; tail -4 $OUT/cohpmc.log
+  COH_PMC_VARIANTS=0 bash scripts/dev/coh_pmc.sh > $OUT/cohpmc.log 2>&1; echo "cohpmc rc=$?"; tail -4 $OUT/cohpmc.log
 fi
 echo "=== done"

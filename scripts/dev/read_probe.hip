@@ -2,7 +2,7 @@
 // CURRENT, 1M x 4 KiB pages) streamed once, one wave per page, XOR-OR reduced to one word per
 // page. Variants: pages per wave, pages in flight per wave, nt vs default loads, grid shape.
 // Not product code: it measures the ceiling the diff kernel is held against.
-//   hipcc --offload-arch=gfx950 -O3 scripts/read_probe.hip -o scripts/read_probe
+//   hipcc --offload-arch=gfx950 -O3 scripts/dev/read_probe.hip -o scripts/dev/read_probe
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -8,7 +8,7 @@
 //   l64     the 64-B line holding the word stored whole (16 lanes x 4 B)
 //   l128    the 128-B line holding the word stored whole (32 lanes x 4 B)
 //   rmw64   the 64-B line read, the word merged in, the line stored whole
-//   hipcc --offload-arch=gfx950 -O3 scripts/scatter_probe.hip -o scripts/scatter_probe
+//   hipcc --offload-arch=gfx950 -O3 scripts/dev/scatter_probe.hip -o scripts/dev/scatter_probe
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
