@@ -1185,8 +1185,8 @@ constexpr uint32_t kDiffSpill = 24576;
 // 1.56-1.66 ms vs 64 pages with the spill slot 1.79-1.93 (the spill's write and read-back).
 constexpr uint32_t kDense64 = 112, kDense16 = 480;
 static inline uint64_t up256(uint64_t v) { return (v + 255) & ~255ull; }
-static uint64_t spill_pool_bytes(uint64_t n) {  // sized for the smaller spill unit (32 pages)
-  const uint64_t wgs = ((n + 31) / 32 + 3) / 4;
+static uint64_t spill_pool_bytes(uint64_t n) {  // sized for the smallest spill unit (16 pages)
+  const uint64_t wgs = ((n + 15) / 16 + 3) / 4;
   return (uint64_t)(wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill;
 }
 uint64_t diff_workspace_bytes(uint64_t n) {
@@ -1270,6 +1270,10 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : (v == 2 || v == 6) ? 32 : 16;
   const uint64_t nunits = (n + U - 1) / U;
   if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
+  // every workgroup's spill slot (ticket % kSpillWGs) lies inside the pool
+  const uint64_t wgs = (nunits + 3) / 4;
+  if (spill && (wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill > spill_pool_bytes(n))
+    return hipErrorInvalidValue;
   // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
   // (outside the timed kernel)
   hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
