@@ -942,7 +942,138 @@ __device__ __forceinline__ void store_chunks_wave(bool valid, uint8_t* dst, uint
 // larger than the window goes through apply_rows from global memory, as in apply_kernel.
 constexpr uint32_t kChunkMap = 512;  // chunks of one run batch mapped through LDS (else: search)
 
-template <uint32_t kWin>
+// One staged window of the flat form: records j..k-1 of the wave's task (lane l's my_off / my_page:
+// record a + l's stream offset and page), their bytes [start, stop) in `win`. Returns 1 when a
+// record of the window is malformed (its runs are not written).
+__device__ __forceinline__ uint32_t flat_window(uint8_t* __restrict__ target,
+                                                const uint32_t* __restrict__ win, uint4* ri,
+                                                uint4* rp, uint8_t* cm, uint64_t my_off,
+                                                uint32_t my_page, uint32_t j, uint32_t k,
+                                                uint64_t start, uint64_t stop) {
+  const uint32_t lane = lane_id();
+  uint32_t bad = 0;
+  // ---- records: lane l = record j + l of the window
+  const uint32_t nrec = k - j;
+  const bool inrec = lane < nrec;
+  const uint32_t r = min(j + lane, 63u);
+  const uint64_t o0 = __shfl(my_off, (int)r, 64);
+  const uint64_t o1n = __shfl(my_off, (int)min(r + 1, 63u), 64);
+  const uint64_t o1 = (j + lane + 1 == k) ? stop : o1n;
+  const uint32_t rs = inrec ? (uint32_t)(o0 - start) : 0u;
+  const uint32_t size = inrec ? (uint32_t)(o1 - o0) : 0u;
+  uint32_t nr = size ? win[rs / 4] : 0u;
+  bool rbad = size && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr);
+  if (rbad) nr = 0;
+  if (nr) {  // the record's run headers, lane-serially: sorted, inside the page, sizes add up
+    // (four independent LDS reads per step, not one dependent read per header)
+    uint32_t prev_end = 0, tot = 0;
+    for (uint32_t i = 0; i < nr; i += 4) {
+      uint32_t hv[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) hv[u] = win[rs / 4 + 1 + min(i + u, nr - 1u)];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        if (i + u < nr) {
+          const uint32_t off = hv[u] & 0xFFFFu, len = hv[u] >> 16;
+          if (len == 0 || off + len > kPage || off < prev_end) rbad = true;
+          prev_end = off + len;
+          tot += len;
+        }
+      }
+    }
+    if (size != 4u + 4u * nr + ((tot + 3u) & ~3u)) rbad = true;
+    if (rbad) nr = 0;
+  }
+  bad |= rbad ? 1u : 0u;
+  const uint32_t rinc = wave_incl_sum(nr);
+  const uint32_t RB = rinc - nr;                 // the record's first run in the window
+  const uint32_t NRW = lane_bcast(rinc, 63);     // runs in the window
+  const uint32_t RBs = inrec ? RB : 0xFFFFFFFFu;  // search key (records past the window: never)
+  ri[lane] = make_uint4(rs, nr, RB, __shfl(my_page, (int)r, 64));
+  wave_lds_sync();
+
+  // ---- runs: 64 at a time
+  uint32_t carry_sum = 0;  // payload bytes of the previous batch's last record so far
+  for (uint32_t q0 = 0; q0 < NRW; q0 += 64) {
+    const uint32_t q = q0 + lane;
+    const bool vq = q < NRW;
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t st = 32; st; st >>= 1) {
+      const uint32_t c = (uint32_t)__shfl((int)RBs, (int)(pos + st), 64);
+      if (c <= q) pos += st;
+    }
+    const uint4 R = ri[pos];  // .x LDS offset, .y runs, .z first run, .w page
+    const uint32_t i = q - R.z;
+    const uint32_t h = vq ? win[R.x / 4 + 1 + i] : 0u;
+    const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
+    // payload offset: lengths summed within the record (segments start at a record's run 0)
+    const uint32_t sg = wave_incl_segsum_dpp(len | ((vq && i == 0) ? kSegStart : 0u));
+    const uint32_t incl = (sg & ~kSegStart) + ((sg & kSegStart) ? 0u : carry_sum);
+    const uint32_t pp = R.x + 4u + 4u * R.y + incl - len;
+    carry_sum = lane_bcast(incl, 63);
+    const uint32_t nch = len ? ((end - 1u) >> 4) - (off >> 4) + 1u : 0u;
+    const uint32_t M = lane_bcast(wave_incl_max(nch), 63);
+    uint8_t* page = target + (uint64_t)R.w * kPage;
+    if (M <= 2) {
+      // short runs (word-sized edits): each lane stores its own run's one or two chunks
+      for (uint32_t c = 0; c < M; ++c) {
+        const uint32_t cs = ((off >> 4) + c) << 4;
+        const uint32_t lo = max(off, cs), hi = min(end, cs + 16u);
+        store_chunks_wave(c < nch, page + cs, lo - cs, hi - cs, win, pp + (lo - off));
+      }
+    } else {
+      // the batch's (run, chunk) pairs spread over the wave, 64 per step: consecutive lanes
+      // store consecutive chunks of a run, so one store instruction writes whole segments
+      // (lane-per-run stores, 16 B into 64 different runs per instruction, measured 1.3x
+      // slower on clustered records)
+      const uint32_t cinc = wave_incl_sum(nch), cex = cinc - nch;
+      const uint32_t T = lane_bcast(cinc, 63);
+      if (T <= kChunkMap) {
+        // chunk -> run through LDS: each run writes its index over its chunks' slots and its
+        // parameters once; a chunk lane then needs two LDS reads (a 6-step search over the
+        // runs' chunk offsets was 6 dependent ds_bpermute round trips per 64 chunks)
+        if (vq) rp[lane] = make_uint4(R.w, off | (end << 16), pp, cex);
+        for (uint32_t c = 0; c < M; ++c)
+          if (c < nch) cm[cex + c] = (uint8_t)lane;
+        wave_lds_sync();
+        for (uint32_t g0 = 0; g0 < T; g0 += 64) {
+          const uint32_t g = g0 + lane;
+          const uint4 P = rp[cm[g < T ? g : 0]];
+          const uint32_t oi = P.y & 0xFFFFu, ei = P.y >> 16;
+          const uint32_t cs = ((oi >> 4) + (g - P.w)) << 4;
+          const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
+          store_chunks_wave(g < T, target + (uint64_t)P.x * kPage + cs, lo - cs, hi - cs, win,
+                            P.z + (lo - oi));
+        }
+        wave_lds_sync();  // the next batch rewrites rp / cm
+        continue;
+      }
+      for (uint32_t g0 = 0; g0 < T; g0 += 64) {
+        const uint32_t g = g0 + lane;
+        uint32_t p2 = 0;
+#pragma unroll
+        for (uint32_t st = 32; st; st >>= 1) {
+          const uint32_t c = (uint32_t)__shfl((int)cex, (int)(p2 + st), 64);
+          if (c <= g) p2 += st;
+        }
+        const uint32_t oi = (uint32_t)__shfl((int)off, (int)p2, 64);
+        const uint32_t ei = (uint32_t)__shfl((int)end, (int)p2, 64);
+        const uint32_t pi = (uint32_t)__shfl((int)pp, (int)p2, 64);
+        const uint32_t ci = (uint32_t)__shfl((int)cex, (int)p2, 64);
+        const uint32_t wi = (uint32_t)__shfl((int)R.w, (int)p2, 64);
+        const uint32_t cs = ((oi >> 4) + (g - ci)) << 4;
+        const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
+        store_chunks_wave(g < T, target + (uint64_t)wi * kPage + cs, lo - cs, hi - cs, win,
+                          pi + (lo - oi));
+      }
+    }
+  }
+  wave_lds_sync();
+  return bad;
+}
+
+template <uint32_t kWin, bool kX4 = true>
 __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ target,
                                                          const uint32_t* __restrict__ ids,
                                                          uint64_t n,
@@ -950,6 +1081,7 @@ __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ t
                                                          const uint8_t* __restrict__ data,
                                                          uint32_t* __restrict__ err) {
   // +4 dwords: an unaligned payload read of the window's last bytes stays inside the buffer
+  // (every fill instruction writes whole 1 KiB / 256-B blocks inside roundup(window, 64 dwords))
   __shared__ __attribute__((aligned(16))) uint32_t win_all[4][kWin / 4 + 4];
   __shared__ uint4 ri_all[4][64];  // per record of the window: LDS offset, runs, first run, page
   __shared__ uint4 rp_all[4][64];  // per run of a batch: page, off | end << 16, payload offset
@@ -989,125 +1121,34 @@ __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ t
       const uint64_t stop = (k == 64) ? end_off : lane_bcast64(my_off, k);
       const uint32_t words = (uint32_t)((stop - start) >> 2);
       const uint32_t* src = reinterpret_cast<const uint32_t*>(data + start);
-      for (uint32_t q0 = 0; q0 < words; q0 += 64) {
+      typedef __attribute__((address_space(1))) void* gptr;
+      typedef __attribute__((address_space(3))) void* lptr;
+      uint32_t q0 = 0;
+      if (kX4) {
+        // 16 B per lane (global_load_lds_dwordx4, gfx950), then the last < 4 dwords. Lanes past
+        // the pieces are switched off, not clamped: an LDS-DMA lane writes only when active, and
+        // a clamped x4 lane would write into the tail's dwords, which the second fill also
+        // writes (two DMA writes of one LDS dword land in no fixed order)
+        const uint32_t n16 = words >> 2;
+        for (; q0 < 4 * n16; q0 += 256) {
+          const uint32_t q = q0 / 4 + lane;
+          if (q < n16)
+            __builtin_amdgcn_global_load_lds((gptr)(src + 4 * q), (lptr)(win + q0), 16, 0, 0);
+        }
+        q0 = 4 * n16;
         const uint32_t q = q0 + lane;
-        __builtin_amdgcn_global_load_lds(
-            (__attribute__((address_space(1))) void*)(src + (q < words ? q : 0)),
-            (__attribute__((address_space(3))) void*)(win + q0), 4, 0, 0);
+        if (q < words) __builtin_amdgcn_global_load_lds((gptr)(src + q), (lptr)(win + q0), 4, 0, 0);
+        q0 = words;
+      }
+      for (; q0 < words; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        __builtin_amdgcn_global_load_lds((gptr)(src + (q < words ? q : 0)), (lptr)(win + q0), 4, 0,
+                                         0);
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed
       wave_lds_sync();
 
-      // ---- records: lane l = record j + l of the window
-      const uint32_t nrec = k - j;
-      const bool inrec = lane < nrec;
-      const uint32_t r = min(j + lane, 63u);
-      const uint64_t o0 = __shfl(my_off, (int)r, 64);
-      const uint64_t o1n = __shfl(my_off, (int)min(r + 1, 63u), 64);
-      const uint64_t o1 = (j + lane + 1 == k) ? stop : o1n;
-      const uint32_t rs = inrec ? (uint32_t)(o0 - start) : 0u;
-      const uint32_t size = inrec ? (uint32_t)(o1 - o0) : 0u;
-      uint32_t nr = size ? win[rs / 4] : 0u;
-      bool rbad = size && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr);
-      if (rbad) nr = 0;
-      if (nr) {  // the record's run headers, lane-serially: sorted, inside the page, sizes add up
-        uint32_t prev_end = 0, tot = 0;
-        for (uint32_t i = 0; i < nr; ++i) {
-          const uint32_t h = win[rs / 4 + 1 + i];
-          const uint32_t off = h & 0xFFFFu, len = h >> 16;
-          if (len == 0 || off + len > kPage || off < prev_end) rbad = true;
-          prev_end = off + len;
-          tot += len;
-        }
-        if (size != 4u + 4u * nr + ((tot + 3u) & ~3u)) rbad = true;
-        if (rbad) nr = 0;
-      }
-      bad |= rbad ? 1u : 0u;
-      const uint32_t rinc = wave_incl_sum(nr);
-      const uint32_t RB = rinc - nr;                 // the record's first run in the window
-      const uint32_t NRW = lane_bcast(rinc, 63);     // runs in the window
-      const uint32_t RBs = inrec ? RB : 0xFFFFFFFFu;  // search key (records past the window: never)
-      ri[lane] = make_uint4(rs, nr, RB, __shfl(my_page, (int)r, 64));
-      wave_lds_sync();
-
-      // ---- runs: 64 at a time
-      uint32_t carry_sum = 0;  // payload bytes of the previous batch's last record so far
-      for (uint32_t q0 = 0; q0 < NRW; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        const bool vq = q < NRW;
-        uint32_t pos = 0;
-#pragma unroll
-        for (uint32_t st = 32; st; st >>= 1) {
-          const uint32_t c = (uint32_t)__shfl((int)RBs, (int)(pos + st), 64);
-          if (c <= q) pos += st;
-        }
-        const uint4 R = ri[pos];  // .x LDS offset, .y runs, .z first run, .w page
-        const uint32_t i = q - R.z;
-        const uint32_t h = vq ? win[R.x / 4 + 1 + i] : 0u;
-        const uint32_t off = h & 0xFFFFu, len = h >> 16, end = off + len;
-        // payload offset: lengths summed within the record (segments start at a record's run 0)
-        const uint32_t sg = wave_incl_segsum_dpp(len | ((vq && i == 0) ? kSegStart : 0u));
-        const uint32_t incl = (sg & ~kSegStart) + ((sg & kSegStart) ? 0u : carry_sum);
-        const uint32_t pp = R.x + 4u + 4u * R.y + incl - len;
-        carry_sum = lane_bcast(incl, 63);
-        const uint32_t nch = len ? ((end - 1u) >> 4) - (off >> 4) + 1u : 0u;
-        const uint32_t M = lane_bcast(wave_incl_max(nch), 63);
-        uint8_t* page = target + (uint64_t)R.w * kPage;
-        if (M <= 2) {
-          // short runs (word-sized edits): each lane stores its own run's one or two chunks
-          for (uint32_t c = 0; c < M; ++c) {
-            const uint32_t cs = ((off >> 4) + c) << 4;
-            const uint32_t lo = max(off, cs), hi = min(end, cs + 16u);
-            store_chunks_wave(c < nch, page + cs, lo - cs, hi - cs, win, pp + (lo - off));
-          }
-        } else {
-          // the batch's (run, chunk) pairs spread over the wave, 64 per step: consecutive lanes
-          // store consecutive chunks of a run, so one store instruction writes whole segments
-          // (lane-per-run stores, 16 B into 64 different runs per instruction, measured 1.3x
-          // slower on clustered records)
-          const uint32_t cinc = wave_incl_sum(nch), cex = cinc - nch;
-          const uint32_t T = lane_bcast(cinc, 63);
-          if (T <= kChunkMap) {
-            // chunk -> run through LDS: each run writes its index over its chunks' slots and its
-            // parameters once; a chunk lane then needs two LDS reads (a 6-step search over the
-            // runs' chunk offsets was 6 dependent ds_bpermute round trips per 64 chunks)
-            if (vq) rp[lane] = make_uint4(R.w, off | (end << 16), pp, cex);
-            for (uint32_t c = 0; c < M; ++c)
-              if (c < nch) cm[cex + c] = (uint8_t)lane;
-            wave_lds_sync();
-            for (uint32_t g0 = 0; g0 < T; g0 += 64) {
-              const uint32_t g = g0 + lane;
-              const uint4 P = rp[cm[g < T ? g : 0]];
-              const uint32_t oi = P.y & 0xFFFFu, ei = P.y >> 16;
-              const uint32_t cs = ((oi >> 4) + (g - P.w)) << 4;
-              const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
-              store_chunks_wave(g < T, target + (uint64_t)P.x * kPage + cs, lo - cs, hi - cs, win,
-                                P.z + (lo - oi));
-            }
-            wave_lds_sync();  // the next batch rewrites rp / cm
-            continue;
-          }
-          for (uint32_t g0 = 0; g0 < T; g0 += 64) {
-            const uint32_t g = g0 + lane;
-            uint32_t p2 = 0;
-#pragma unroll
-            for (uint32_t st = 32; st; st >>= 1) {
-              const uint32_t c = (uint32_t)__shfl((int)cex, (int)(p2 + st), 64);
-              if (c <= g) p2 += st;
-            }
-            const uint32_t oi = (uint32_t)__shfl((int)off, (int)p2, 64);
-            const uint32_t ei = (uint32_t)__shfl((int)end, (int)p2, 64);
-            const uint32_t pi = (uint32_t)__shfl((int)pp, (int)p2, 64);
-            const uint32_t ci = (uint32_t)__shfl((int)cex, (int)p2, 64);
-            const uint32_t wi = (uint32_t)__shfl((int)R.w, (int)p2, 64);
-            const uint32_t cs = ((oi >> 4) + (g - ci)) << 4;
-            const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
-            store_chunks_wave(g < T, target + (uint64_t)wi * kPage + cs, lo - cs, hi - cs, win,
-                              pi + (lo - oi));
-          }
-        }
-      }
-      wave_lds_sync();
+      bad |= flat_window(target, win, ri, rp, cm, my_off, my_page, j, k, start, stop);
       j = k;
     }
   }
@@ -1149,9 +1190,10 @@ static int diff_variant() { return g_diff_variant.load(std::memory_order_relaxed
 //   2  long lists: apply_kernel, 4 KiB window
 //   3  long lists: flat form, 8 KiB window
 //   4  long lists: flat form, 2 KiB window
+//   5  long lists: flat form, 4 KiB window filled by dword LDS-DMA (round 3's first default)
 // Same-box, 2M clustered pages (config-3 shard): 0.79 ms (1) -> 0.64 (2) -> 0.55 (0); config 2:
 // 0.250 -> 0.241 ms.
-constexpr int kApplyVariants = 5;
+constexpr int kApplyVariants = 6;
 static int apply_variant_from_env() {
   const char* e = getenv("GDSM_APPLY_VARIANT");
   const int v = e ? atoi(e) : 0;
@@ -1315,6 +1357,7 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
   if (!short_list && (av == 0 || av >= 3)) {
     auto kf = av == 0 ? apply_flat_kernel<4096>
               : av == 3 ? apply_flat_kernel<8192>
+              : av == 5 ? apply_flat_kernel<4096, false>
                         : apply_flat_kernel<2048>;
     hipLaunchKernelGGL(kf, dim3(grid_for(n, 4 * 64, 65536)), dim3(256), 0, s, target, ids, n,
                        rec_off, data, err);
