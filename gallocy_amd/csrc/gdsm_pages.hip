@@ -892,17 +892,22 @@ __device__ __forceinline__ u32x4 lds_load16(const uint32_t* __restrict__ pay32, 
 //   store, and every other chunk's bytes 16 lanes per chunk, four chunks per step,
 // so no lane walks a byte mask on its own while the others wait (a partial chunk among 64 made
 // every lane of the old per-lane mask walk pay for it).
+// kNT: 1 = half chunks (whole aligned 8-B words) stored nontemporally, 2 = whole chunks too.
+// (Alone, scattered whole 64-B segments are written 1.3x faster nontemporally,
+// scripts/dev/cluster_probe.hip; inside the apply, beside the partial chunks' cached byte stores to
+// the same segments, nontemporal whole chunks measured slower.)
+template <int kNT>
 __device__ __forceinline__ void store_chunks_wave(bool valid, uint8_t* dst, uint32_t lo,
                                                   uint32_t hi, const uint32_t* __restrict__ pay32,
                                                   uint32_t q) {
   const bool full = valid && lo == 0 && hi == 16;
   const bool half = valid && (hi - lo) == 8 && (lo & 7u) == 0;
   if (full) {
-    *reinterpret_cast<u32x4*>(dst) = lds_load16(pay32, q);
+    st<(kNT >= 2)>(reinterpret_cast<u32x4*>(dst), lds_load16(pay32, q));
   } else if (half) {
     const u32x4 v = lds_load16(pay32, q);
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    *reinterpret_cast<u32x2*>(dst + lo) = (u32x2){v.x, v.y};
+    st<(kNT >= 1)>(reinterpret_cast<u32x2*>(dst + lo), (u32x2){v.x, v.y});
   }
   uint64_t G = __ballot(valid && !full && !half);
   const uint32_t lane = lane_id(), r = lane >> 4, b = lane & 15u;
@@ -945,6 +950,7 @@ constexpr uint32_t kChunkMap = 512;  // chunks of one run batch mapped through L
 // One staged window of the flat form: records j..k-1 of the wave's task (lane l's my_off / my_page:
 // record a + l's stream offset and page), their bytes [start, stop) in `win`. Returns 1 when a
 // record of the window is malformed (its runs are not written).
+template <int kNT>
 __device__ __forceinline__ uint32_t flat_window(uint8_t* __restrict__ target,
                                                 const uint32_t* __restrict__ win, uint4* ri,
                                                 uint4* rp, uint8_t* cm, uint64_t my_off,
@@ -1020,7 +1026,7 @@ __device__ __forceinline__ uint32_t flat_window(uint8_t* __restrict__ target,
       for (uint32_t c = 0; c < M; ++c) {
         const uint32_t cs = ((off >> 4) + c) << 4;
         const uint32_t lo = max(off, cs), hi = min(end, cs + 16u);
-        store_chunks_wave(c < nch, page + cs, lo - cs, hi - cs, win, pp + (lo - off));
+        store_chunks_wave<kNT>(c < nch, page + cs, lo - cs, hi - cs, win, pp + (lo - off));
       }
     } else {
       // the batch's (run, chunk) pairs spread over the wave, 64 per step: consecutive lanes
@@ -1043,7 +1049,7 @@ __device__ __forceinline__ uint32_t flat_window(uint8_t* __restrict__ target,
           const uint32_t oi = P.y & 0xFFFFu, ei = P.y >> 16;
           const uint32_t cs = ((oi >> 4) + (g - P.w)) << 4;
           const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
-          store_chunks_wave(g < T, target + (uint64_t)P.x * kPage + cs, lo - cs, hi - cs, win,
+          store_chunks_wave<kNT>(g < T, target + (uint64_t)P.x * kPage + cs, lo - cs, hi - cs, win,
                             P.z + (lo - oi));
         }
         wave_lds_sync();  // the next batch rewrites rp / cm
@@ -1064,7 +1070,7 @@ __device__ __forceinline__ uint32_t flat_window(uint8_t* __restrict__ target,
         const uint32_t wi = (uint32_t)__shfl((int)R.w, (int)p2, 64);
         const uint32_t cs = ((oi >> 4) + (g - ci)) << 4;
         const uint32_t lo = max(oi, cs), hi = min(ei, cs + 16u);
-        store_chunks_wave(g < T, target + (uint64_t)wi * kPage + cs, lo - cs, hi - cs, win,
+        store_chunks_wave<kNT>(g < T, target + (uint64_t)wi * kPage + cs, lo - cs, hi - cs, win,
                           pi + (lo - oi));
       }
     }
@@ -1073,7 +1079,7 @@ __device__ __forceinline__ uint32_t flat_window(uint8_t* __restrict__ target,
   return bad;
 }
 
-template <uint32_t kWin, bool kX4 = true>
+template <uint32_t kWin, bool kX4 = true, int kNT = 0>
 __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ target,
                                                          const uint32_t* __restrict__ ids,
                                                          uint64_t n,
@@ -1148,7 +1154,7 @@ __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ t
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed
       wave_lds_sync();
 
-      bad |= flat_window(target, win, ri, rp, cm, my_off, my_page, j, k, start, stop);
+      bad |= flat_window<kNT>(target, win, ri, rp, cm, my_off, my_page, j, k, start, stop);
       j = k;
     }
   }
@@ -1184,16 +1190,21 @@ static std::atomic<int> g_diff_variant{diff_variant_from_env()};
 static int diff_variant() { return g_diff_variant.load(std::memory_order_relaxed); }
 // Apply geometry, gdsm_tune("apply_variant", v) or GDSM_APPLY_VARIANT=v (same output):
 //   0  default: long lists (> 16384 records) the flat form (apply_flat_kernel: the window's runs
-//      64 at a time, chunks spread over the wave) with a 4 KiB window; short lists apply_kernel
-//      with 4 records per task and a 12 KiB window
+//      64 at a time, chunks spread over the wave) with a 4 KiB window filled 16 B per lane, whole
+//      aligned 8-B words stored nontemporally; short lists apply_kernel with 4 records per task
+//      and a 12 KiB window
 //   1  long lists: apply_kernel (records row by row), 8 KiB window (round 2's default)
 //   2  long lists: apply_kernel, 4 KiB window
 //   3  long lists: flat form, 8 KiB window
 //   4  long lists: flat form, 2 KiB window
 //   5  long lists: flat form, 4 KiB window filled by dword LDS-DMA (round 3's first default)
+//   6  long lists: flat form, whole chunks stored nontemporally too
+//   7  long lists: flat form, every store cached (round 3's first flat default)
+// Same box, 4M pages: uniform 1 % 0.966 ms (7) -> 0.932 (0); clustered 1.058 (7), 1.065 (0),
+// 1.234 (6).
 // Same-box, 2M clustered pages (config-3 shard): 0.79 ms (1) -> 0.64 (2) -> 0.55 (0); config 2:
 // 0.250 -> 0.241 ms.
-constexpr int kApplyVariants = 6;
+constexpr int kApplyVariants = 8;
 static int apply_variant_from_env() {
   const char* e = getenv("GDSM_APPLY_VARIANT");
   const int v = e ? atoi(e) : 0;
@@ -1355,10 +1366,12 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
   const uint32_t per_task = short_list ? 4u : 64u;
   const int av = g_apply_variant.load(std::memory_order_relaxed);
   if (!short_list && (av == 0 || av >= 3)) {
-    auto kf = av == 0 ? apply_flat_kernel<4096>
-              : av == 3 ? apply_flat_kernel<8192>
-              : av == 5 ? apply_flat_kernel<4096, false>
-                        : apply_flat_kernel<2048>;
+    auto kf = av == 0 ? apply_flat_kernel<4096, true, 1>
+              : av == 3 ? apply_flat_kernel<8192, true, 1>
+              : av == 5 ? apply_flat_kernel<4096, false, 1>
+              : av == 6 ? apply_flat_kernel<4096, true, 2>
+              : av == 7 ? apply_flat_kernel<4096, true, 0>
+                        : apply_flat_kernel<2048, true, 1>;
     hipLaunchKernelGGL(kf, dim3(grid_for(n, 4 * 64, 65536)), dim3(256), 0, s, target, ids, n,
                        rec_off, data, err);
     return hipGetLastError();

@@ -8,6 +8,7 @@
 //   write   the same stores, no payload read
 //   read    the payload read alone (stores skipped)
 //   rand    copy with the clusters taken in a random page order (no locality between waves)
+//   copynt / writent   copy / write with nontemporal stores
 //   hipcc --offload-arch=gfx950 -O3 scripts/dev/cluster_probe.hip -o /tmp/cluster_probe
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -62,7 +63,7 @@ __global__ void list_kernel(const uint32_t* __restrict__ off, uint32_t* __restri
   }
 }
 
-template <int kMode>  // 0 copy, 1 write only, 2 read only
+template <int kMode, bool kNT = false>  // 0 copy, 1 write only, 2 read only
 __global__ __launch_bounds__(256) void chunk_kernel(uint8_t* __restrict__ arena,
                                                     const u32x4* __restrict__ pay,
                                                     const uint32_t* __restrict__ list,
@@ -73,8 +74,13 @@ __global__ __launch_bounds__(256) void chunk_kernel(uint8_t* __restrict__ arena,
     const uint32_t cl = list[g >> 2];
     u32x4 v = (u32x4){(uint32_t)g, 1, 2, 3};
     if (kMode != 1) v = __builtin_nontemporal_load(pay + g);
-    if (kMode != 2)
-      *reinterpret_cast<u32x4*>(arena + (uint64_t)cl * 64 + (g & 3) * 16) = v;
+    if (kMode != 2) {
+      u32x4* d = reinterpret_cast<u32x4*>(arena + (uint64_t)cl * 64 + (g & 3) * 16);
+      if (kNT)
+        __builtin_nontemporal_store(v, d);
+      else
+        *d = v;
+    }
     else
       acc ^= v.x ^ v.w;
   }
@@ -114,8 +120,10 @@ int main() {
     const char* name;
     int mode;
     int rnd;
+    bool nt;
   };
-  const V vs[] = {{"copy ", 0, 0}, {"write", 1, 0}, {"read ", 2, 0}, {"rand ", 0, 1}};
+  const V vs[] = {{"copy ", 0, 0, false},  {"write", 1, 0, false},   {"read ", 2, 0, false},
+                  {"copynt", 0, 0, true},  {"writent", 1, 0, true},  {"rand ", 0, 1, false}};
   for (const V& v : vs) {
     hipLaunchKernelGGL(list_kernel, dim3((unsigned)(n / 256)), dim3(256), 0, 0, off, list, n);
     CK(hipDeviceSynchronize());
@@ -137,7 +145,9 @@ int main() {
     std::vector<float> ts;
     for (int r = 0; r < 7; ++r) {
       CK(hipEventRecord(e0, 0));
-      auto k = v.mode == 0 ? chunk_kernel<0> : v.mode == 1 ? chunk_kernel<1> : chunk_kernel<2>;
+      auto k = v.mode == 0 ? (v.nt ? chunk_kernel<0, true> : chunk_kernel<0>)
+               : v.mode == 1 ? (v.nt ? chunk_kernel<1, true> : chunk_kernel<1>)
+                             : chunk_kernel<2>;
       hipLaunchKernelGGL(k, dim3(8192), dim3(256), 0, 0, arena, pay, list, nchunks, sink);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));

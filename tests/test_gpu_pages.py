@@ -701,12 +701,11 @@ def _long_list_apply_case(rng, n):
     return tw, ro, data, want, rc
 
 
-@pytest.mark.parametrize("variant", list(range(6)))
+@pytest.mark.parametrize("variant", list(range(8)))
 def test_apply_variants_long_lists(variant):
     """Every apply geometry on a long list (gdsm_tune "apply_variant": flat with a 4 KiB window
-    filled 16 B per lane (default) or dword by dword, records by rows with an 8 or 4 KiB window,
-    flat with an 8 or 2 KiB window) leaves
-    REPLICA exactly as the oracle's apply of the same stream, malformed records included (nothing
+    filled 16 B per lane (default) or dword by dword, with more or fewer nontemporal stores;
+    records by rows with an 8 or 4 KiB window; flat with an 8 or 2 KiB window) leaves REPLICA exactly as the oracle's apply of the same stream, malformed records included (nothing
     of them written, -EINVAL at sync)."""
     L = _lib.load()
     rng = np.random.default_rng(900 + variant)
