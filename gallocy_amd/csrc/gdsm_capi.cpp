@@ -54,6 +54,13 @@ int ensure_aux(gdsm_ctx* ctx) {
 int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need) {
   if (*have >= need) return 0;
   if (ctx && ctx->capturing) return -EBUSY;  // size workspaces with gdsm_reserve before capturing
+  // kernels queued on the context's streams (main or aux, e.g. an exchange's applies reading the
+  // checked id lists) may still use the old buffer: drain them before it goes (stated here rather
+  // than left to hipFree's own synchronisation)
+  if (*buf && ctx) {
+    if (ctx->stream) GDSM_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->aux) GDSM_TRY(hipStreamSynchronize(ctx->aux));
+  }
   if (*buf) (void)hipFree(*buf);
   *buf = nullptr;
   *have = 0;
