@@ -269,3 +269,31 @@ def test_every_selectable_coherence_variant(variant):
             assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
     finally:
         L.gdsm_tune(b"coh_variant", 0)
+
+
+def test_coherence_at_the_maximum_table_size():
+    """GDSM_MAX_COH_PAGES = 2^28 pages, where the top page's events use every bit of the event's
+    low dword (page << 4): one batch on the lowest and the highest 4096 pages, the top page hot
+    (its events cross many 2048-event blocks), bit-exact against the oracle over the whole
+    2 GiB page table; a table one page larger is refused."""
+    n = 1 << 28
+    rng = np.random.default_rng(28)
+    lo = rng.integers(0, 40, 4096).astype(np.uint64)
+    hi = rng.integers(0, 40, 4096).astype(np.uint64)
+    hi[-1] = 20000
+    ev = np.concatenate([oracle.gen_events(lo, seed=5, write_pct=20),
+                         oracle.gen_events(hi, seed=6, write_pct=20, first_page=n - 4096)])
+    assert int(ev[-1] >> 4) == n - 1
+    with ga.Context(n, arenas=()) as c:
+        c.coh_init(8)
+        tot = c.coherence_batch(ev)
+        gst, gfl = c.coh_download()
+    st, fl = oracle.coh_init(n, 8)
+    rc, otot = oracle.coherence(st, fl, ev)
+    assert rc == 0 and tot == otot
+    assert np.array_equal(gst, st), np.flatnonzero(gst != st)[:10]
+    assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
+    del gst, gfl, st, fl
+    with ga.Context(n + 1, arenas=()) as c:
+        with pytest.raises(GdsmError):
+            c.coh_init(8)
