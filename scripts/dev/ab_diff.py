@@ -14,10 +14,11 @@ from gallocy_amd import gdsm  # noqa: E402
 
 KEY = sys.argv[1] if len(sys.argv) > 1 else "diff_variant"
 VALUES = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1"])]
-ROUNDS, REPS = 6, 10
-n = 1 << 20
-ctx = ga.Context(n)
 import os  # noqa: E402
+
+ROUNDS, REPS = 6, 10
+n = int(os.environ.get("AB_PAGES", 1 << 20))  # pages (default config 2's 1M)
+ctx = ga.Context(n)
 
 if os.environ.get("AB_MODE") == "clustered":  # config-3 density (442 B records)
     ctx.gen_pages(seed=77, mode=ga.GEN_CLUSTERED, ppm=100000)
