@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <vector>
 #include <algorithm>
 
@@ -52,6 +53,81 @@ __global__ __launch_bounds__(256) void rd_pages(const u32x4* __restrict__ a, con
       if (lane == 0) out[p] = (uint32_t)__popcll(m);
     }
   }
+}
+
+// The diff kernel's own shape: PPW pages per wave, the next page's 8 loads issued before the
+// current page is reduced (one page in flight ahead).
+template <int PPW>
+__global__ __launch_bounds__(256) void rd_pipe(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
+                                               uint32_t* __restrict__ out, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wave) * PPW;
+  if (w0 >= n) return;
+  u32x4 t[4], c[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    t[k] = ld<true>(a + w0 * 256 + k * 64 + lane);
+    c[k] = ld<true>(b + w0 * 256 + k * 64 + lane);
+  }
+  for (int j = 0; j < PPW && w0 + j < n; ++j) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32x4 x = t[k] ^ c[k];
+      d |= x.x | x.y | x.z | x.w;
+    }
+    const uint64_t p = w0 + j + 1;
+    if (j + 1 < PPW && p < n) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        t[k] = ld<true>(a + p * 256 + k * 64 + lane);
+        c[k] = ld<true>(b + p * 256 + k * 64 + lane);
+      }
+    }
+    const uint64_t m = __ballot(d != 0);
+    if (lane == 0) out[w0 + j] = (uint32_t)__popcll(m);
+  }
+}
+
+// LDS-DMA: PPW pages per wave, each page's 8 KiB (twin + current) by 8 global_load_lds_dwordx4
+// into one of two per-wave LDS buffers, the next page's DMA issued before the current page is
+// read back from LDS and reduced. 64 KiB of LDS per workgroup: 2 workgroups per CU.
+template <int PPW>
+__global__ __launch_bounds__(256) void rd_dma(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
+                                              uint32_t* __restrict__ out, uint64_t n) {
+  __shared__ __attribute__((aligned(16))) u32x4 buf[4][2][512];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wave) * PPW;
+  if (w0 >= n) return;
+  typedef __attribute__((address_space(1))) void* gptr;
+  typedef __attribute__((address_space(3))) void* lptr;
+#define RD_DMA(p_, s_)                                                                      \
+  do {                                                                                      \
+    for (int k = 0; k < 4; ++k) {                                                           \
+      __builtin_amdgcn_global_load_lds((gptr)(a + (p_) * 256 + k * 64 + lane),              \
+                                       (lptr)(&buf[wave][s_][k * 64]), 16, 0, 0);           \
+      __builtin_amdgcn_global_load_lds((gptr)(b + (p_) * 256 + k * 64 + lane),              \
+                                       (lptr)(&buf[wave][s_][256 + k * 64]), 16, 0, 0);     \
+    }                                                                                       \
+  } while (0)
+  RD_DMA(w0, 0);
+  for (int j = 0; j < PPW && w0 + j < n; ++j) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t p = w0 + j + 1;
+    if (j + 1 < PPW && p < n) RD_DMA(p, (j + 1) & 1);
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32x4 x = buf[wave][j & 1][k * 64 + lane] ^ buf[wave][j & 1][256 + k * 64 + lane];
+      d |= x.x | x.y | x.z | x.w;
+    }
+    const uint64_t m = __ballot(d != 0);
+    if (lane == 0) out[w0 + j] = (uint32_t)__popcll(m);
+  }
+#undef RD_DMA
 }
 
 // Persistent grid-stride over pages, one page per wave iteration.
@@ -104,8 +180,8 @@ __global__ void fill(u32x4* p, uint64_t n, uint32_t s) {
 
 typedef void (*Kern)(const u32x4*, const u32x4*, uint32_t*, uint64_t);
 
-int main() {
-  const uint64_t n = 1 << 20, chunks = n * 256;
+int main(int argc, char** argv) {
+  const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 0) : (1 << 20), chunks = n * 256;
   u32x4 *a, *b;
   uint32_t* out;
   CK(hipMalloc(&a, chunks * 16));
@@ -123,6 +199,10 @@ int main() {
       {"pages ppw4  inf1 nt", rd_pages<4, 1, true>, (unsigned)(n / 16), n},
       {"pages ppw1  inf1 nt", rd_pages<1, 1, true>, (unsigned)(n / 4), n},
       {"pages ppw64 inf2 nt", rd_pages<64, 2, true>, (unsigned)(n / 256), n},
+      {"pipe ppw64 nt      ", rd_pipe<64>, (unsigned)(n / 256), n},
+      {"pipe ppw16 nt      ", rd_pipe<16>, (unsigned)(n / 64), n},
+      {"dma ppw64          ", rd_dma<64>, (unsigned)(n / 256), n},
+      {"dma ppw16          ", rd_dma<16>, (unsigned)(n / 64), n},
       {"persist 2048 nt    ", rd_persist<true>, 2048, n},
       {"persist 4096 nt    ", rd_persist<true>, 4096, n},
       {"persist 8192 nt    ", rd_persist<true>, 8192, n},
