@@ -68,6 +68,12 @@ void or_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_pag
  * replica equals its current arena. Returns 0, -12 (allocation) or -22. */
 int or_bench_diff_apply(uint64_t n, int mode, uint32_t ppm, uint64_t seed, double seconds,
                         int threads, uint64_t* pages, double* elapsed, int* ok);
+/* Tests only: the stream (rec_off[n + 1], data) of the SPEC §6 workload's pages [first, first + n)
+ * equals the oracle's, record by record (each record's size and bytes), regenerating the pages
+ * 4096 at a time on `threads` OpenMP threads. Returns -1 when every record matches, the first
+ * mismatching page index otherwise, -2 on an allocation failure. */
+int64_t or_check_stream(const uint64_t* rec_off, const uint8_t* data, uint64_t first,
+                        uint64_t n, uint64_t seed, int mode, uint32_t ppm, int threads);
 int or_bench_coherence(const uint64_t* events, const uint64_t* page_off, uint64_t n_pages,
                        uint32_t n_nodes, double seconds, int threads, uint64_t* done,
                        double* elapsed);

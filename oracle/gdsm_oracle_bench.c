@@ -102,3 +102,55 @@ int or_bench_coherence(const uint64_t* events, const uint64_t* page_off, uint64_
   *elapsed = slowest;
   return failed ? -22 : 0;
 }
+
+int64_t or_check_stream(const uint64_t* rec_off, const uint8_t* data, uint64_t first,
+                        uint64_t n, uint64_t seed, int mode, uint32_t ppm, int threads) {
+  if (threads < 1) threads = 1;
+  const uint64_t kB = 4096;  // pages per work item
+  const uint64_t nitems = (n + kB - 1) / kB;
+  int64_t bad = -1;
+  int failed = 0;
+  if (n && rec_off[0] != 0) return 0;
+#pragma omp parallel num_threads(threads) reduction(|| : failed)
+  {
+    uint8_t* twin = malloc(kB * OR_PAGE_SZ);
+    uint8_t* cur = malloc(kB * OR_PAGE_SZ);
+    uint64_t* ro = malloc((kB + 1) * sizeof(uint64_t));
+    uint8_t* buf = NULL;
+    uint64_t bcap = 0;
+    if (!twin || !cur || !ro) failed = 1;
+#pragma omp for schedule(dynamic, 1)
+    for (uint64_t it = 0; it < nitems; ++it) {
+      if (failed) continue;
+      const uint64_t p0 = it * kB, m = n - p0 < kB ? n - p0 : kB;
+      or_gen_pages(twin, cur, NULL, first + p0, 1, m, seed, mode, ppm);
+      const uint64_t need = or_diff_pages(twin, cur, NULL, m, ro, NULL, 0);
+      if (need > bcap) {
+        free(buf);
+        bcap = need;
+        buf = malloc(bcap ? bcap : 1);
+        if (!buf) {
+          failed = 1;
+          continue;
+        }
+      }
+      or_diff_pages(twin, cur, NULL, m, ro, buf, bcap);
+      for (uint64_t i = 0; i < m; ++i) {
+        const uint64_t a = rec_off[p0 + i], b = rec_off[p0 + i + 1];
+        if (b - a != ro[i + 1] - ro[i] || b < a ||
+            memcmp(data + a, buf + ro[i], (size_t)(ro[i + 1] - ro[i])) != 0) {
+#pragma omp critical
+          {
+            if (bad < 0 || (int64_t)(p0 + i) < bad) bad = (int64_t)(p0 + i);
+          }
+          break;
+        }
+      }
+    }
+    free(twin);
+    free(cur);
+    free(ro);
+    free(buf);
+  }
+  return failed ? -2 : bad;
+}

@@ -39,6 +39,8 @@ def lib():
                                           C.POINTER(C.c_int)]
         L.or_bench_coherence.argtypes = [C.c_void_p, C.c_void_p, u64, C.c_uint32, C.c_double,
                                          C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
+        L.or_check_stream.restype = C.c_int64
+        L.or_check_stream.argtypes = [vp, vp, u64, u64, u64, C.c_int, C.c_uint32, C.c_int]
         _lib = L
     return _lib
 
@@ -133,6 +135,20 @@ def ref_nw_batch(cases):
         out.append((raw[i:i + L], raw[i + L:i + 2 * L]))
         i += 2 * L
     return out
+
+
+def check_stream(rec_off, data, first, n, seed, mode, ppm, threads=16):
+    """The stream (rec_off[n + 1], data) of the SPEC §6 workload's pages [first, first + n)
+    against the oracle, record by record, on `threads` OpenMP threads (tests only). Returns -1
+    when it matches everywhere, else the first mismatching page index."""
+    ro = np.ascontiguousarray(rec_off, np.uint64)
+    d = np.ascontiguousarray(data, np.uint8)
+    assert len(ro) == n + 1
+    rc = lib().or_check_stream(_p(ro), _p(d) if len(d) else None, first, n, seed, mode, ppm,
+                               threads)
+    if rc == -2:
+        raise MemoryError("or_check_stream")
+    return int(rc)
 
 
 def bench_diff_apply(n, mode, ppm, seed, seconds, threads):

@@ -231,3 +231,18 @@ def test_coherence_rejects_node_outside_the_table():
     st, fl = oracle.coh_init(8, 3)
     rc, _ = oracle.coherence(st, fl, np.array([(1 << 4) | (2 << 1)], np.uint64), n_nodes=3)
     assert rc == 0
+
+
+def test_check_stream_finds_the_first_bad_record():
+    """oracle.check_stream (the whole-stream checker of the full-size GPU tests) accepts the
+    oracle's own stream of a workload slice and names the page of the first corrupted record."""
+    n = 5000
+    for mode, ppm in ((0, 10000), (1, 100000)):
+        tw, cu = oracle.gen_pages(n, seed=3, mode=mode, ppm=ppm, first_page=777)
+        ro, data = oracle.diff_pages(tw, cu)
+        assert oracle.check_stream(ro, data, 777, n, 3, mode, ppm, threads=4) == -1
+        assert oracle.check_stream(ro, data, 778, n, 3, mode, ppm, threads=4) != -1
+        bad = data.copy()
+        p = 3210 + int(np.flatnonzero(np.diff(ro[3210:].astype(np.int64)) > 8)[0])
+        bad[int(ro[p]) + 5] ^= 0x40
+        assert oracle.check_stream(ro, bad, 777, n, 3, mode, ppm, threads=4) == p
