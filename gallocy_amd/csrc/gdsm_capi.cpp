@@ -595,6 +595,44 @@ int gdsm_diff_apply(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* o
   return diff_impl(ctx, ids, n, out, target);
 }
 
+int gdsm_diff_split(gdsm_ctx* ctx, const uint64_t* bounds, uint32_t G, gdsm_runs* out) {
+  if (!ctx || !bounds || !out || G < 1 || G > gdsm::kMaxSplit) return -EINVAL;
+  if (!ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
+  if (bounds[G] > ctx->n_pages) return -EINVAL;
+  gdsm::DiffSplit sp{};
+  sp.G = G;
+  for (uint32_t d = 0; d < G; ++d) {
+    gdsm_runs& o = out[d];
+    if (bounds[d + 1] < bounds[d] || !o.rec_off || (!o.data && o.cap)) return -EINVAL;
+    const uint64_t n = bounds[d + 1] - bounds[d];
+    if (o.n_cap ? n > o.n_cap : (o.owned && n > o.n)) return -EINVAL;
+    for (uint32_t e = 0; e < d; ++e)
+      if (out[e].rec_off == o.rec_off) return -EINVAL;  // every stream its own buffers
+    sp.rec_off[d] = o.rec_off;
+    sp.data[d] = o.data;
+    sp.cap[d] = o.cap;
+    sp.first[d] = bounds[d];
+  }
+  sp.first[G] = bounds[G];
+  DeviceGuard g(ctx->device);
+  if (ctx->aux_targets & ((1u << GDSM_TWIN) | (1u << GDSM_CURRENT))) {
+    int rc = join_aux(ctx);  // a pending apply writes an arena this call reads
+    if (rc) return rc;
+  }
+  for (uint32_t d = 0; d < G; ++d) {
+    auto busy = ctx->runs_busy.find(out[d].rec_off);
+    if (busy != ctx->runs_busy.end()) GDSM_TRY(hipStreamWaitEvent(ctx->stream, busy->second, 0));
+  }
+  int rc = ensure(ctx, &ctx->diff_ws, &ctx->diff_ws_bytes,
+                  gdsm::diff_workspace_bytes(bounds[G] - bounds[0]));
+  if (rc) return rc;
+  for (uint32_t d = 0; d < G; ++d) out[d].n = bounds[d + 1] - bounds[d];
+  GDSM_TRY(gdsm::launch_diff_split(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], sp,
+                                   ctx->diff_ws, ctx->diff_ws_bytes, ctx->stream, ctx->P(),
+                                   ctx->diff_bpp));
+  return 0;
+}
+
 int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total) {
   if (!ctx || !runs || !total || !runs->rec_off) return -EINVAL;
   CtxGuard g(ctx);

@@ -25,6 +25,21 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr,
                        uint8_t* target = nullptr, uint32_t bpp_hint = 0);
+// The diff kernel's output streams: list entries [first[d], first[d+1]) go to stream d (record
+// i of stream d = entry first[d] + i); ustart: the first work unit of each stream (set by the
+// launcher). One launch serves them all, each stream with its own look-back chain.
+constexpr uint32_t kMaxSplit = 8;
+struct DiffSplit {
+  uint64_t* rec_off[kMaxSplit];
+  uint8_t* data[kMaxSplit];
+  uint64_t cap[kMaxSplit];
+  uint64_t first[kMaxSplit + 1];
+  uint64_t ustart[kMaxSplit + 1];
+  uint32_t G;
+};
+// One diff launch over arena pages [first[0], first[G]) (ids = identity) into sp's G streams.
+hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
+                             uint64_t ws_bytes, hipStream_t s, Prof* prof, uint32_t bpp_hint);
 hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
                         const uint64_t* rec_off, const uint8_t* data, uint32_t* err,
                         hipStream_t s, Prof* prof = nullptr);

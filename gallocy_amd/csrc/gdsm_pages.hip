@@ -419,8 +419,7 @@ constexpr uint32_t kSpillWGs = 1280;  // > the workgroups of this kernel one MI3
 template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
-    const uint32_t* __restrict__ ids, uint64_t n, uint64_t* __restrict__ rec_off,
-    uint8_t* __restrict__ data, uint64_t cap, uint64_t* __restrict__ ws,
+    const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool) {
   static_assert(kU <= 64 && (kU & (kU - 1)) == 0, "unit size");
   __shared__ uint32_t sel_tab[16];
@@ -435,7 +434,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   uint4* dat = dat_all[wave];
   uint32_t* buf = buf_all[wave];
   uint32_t* tab = tab_all[wave];
-  const uint64_t nunits = (n + kU - 1) / kU;
+  const uint64_t nunits = sp.ustart[sp.G];
   // one ticket per workgroup (a single counter takes ~88 returning atomics per us, so per-wave
   // tickets would queue on it); unit = 4 * ticket + wave
   __shared__ uint32_t ticket, done_waves;
@@ -453,13 +452,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   __syncthreads();
   const uint64_t u = (uint64_t)ticket * 4 + wave;
   if (u >= nunits) return;  // wave-uniform: the grid's spare waves
+  // the output stream this unit belongs to (units never straddle two of them) and its place in it
+  uint32_t d = 0;
+#pragma unroll
+  for (uint32_t t = 1; t < kMaxSplit; ++t)
+    if (t < sp.G && sp.ustart[t] <= u) d = t;
+  const uint64_t u0 = sp.ustart[d];            // the stream's first unit
+  uint64_t* __restrict__ rec_off = sp.rec_off[d];
+  uint8_t* __restrict__ data = sp.data[d];
+  const uint64_t cap = sp.cap[d];
   uint32_t* slot = kSpill ? reinterpret_cast<uint32_t*>(
                                 pool + ((uint64_t)(ticket % kSpillWGs) * 4 + wave) * kSpill)
                           : nullptr;
   uint32_t spilled = 0;  // bytes of this wave's records flushed to its slot
   uint64_t* status = ws + 1;
-  const uint64_t i0 = u * kU;
-  const uint32_t cnt = (uint32_t)min((uint64_t)kU, n - i0);
+  const uint64_t l0 = (u - u0) * kU;              // first record of the unit in its stream
+  const uint64_t i0 = sp.first[d] + l0;           // ... and its list entry
+  const uint32_t cnt = (uint32_t)min((uint64_t)kU, sp.first[d + 1] - i0);
 
   uint32_t acc = 0;       // LDS bytes used by buffered records
   uint64_t late = 0;      // bit j: page j is emitted from the arenas after the look-back
@@ -541,15 +550,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   const uint32_t incl = wave_incl_sum(my_size);  // lanes >= cnt hold 0
   const uint32_t agg = lane_bcast(incl, 63);
   if (lane == 0)
-    __hip_atomic_store(status + u, (u == 0 ? kStIncl : kStAgg) | agg, __ATOMIC_RELAXED,
+    __hip_atomic_store(status + u, (u == u0 ? kStIncl : kStAgg) | agg, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   uint64_t excl = 0;
-  if (u > 0) {
+  if (u > u0) {
     int64_t pos = (int64_t)u - 1;
     for (;;) {
       const int64_t q = pos - (int64_t)lane;
-      uint64_t st = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : kStIncl;  // before unit 0: an inclusive prefix of 0
+      uint64_t st = q >= (int64_t)u0
+                        ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : kStIncl;  // before the stream's first unit: an inclusive prefix of 0
       while (__ballot((st >> 62) == 0)) {  // a predecessor has not published yet
         __builtin_amdgcn_s_sleep(1);
         if ((st >> 62) == 0)
@@ -570,8 +580,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   }
 
   // ---- rec_off, then the records: buffered ones from LDS, late ones from the arenas
-  if (lane < cnt) rec_off[i0 + lane + 1] = excl + incl;
-  if (u == 0 && lane == 0) rec_off[0] = 0;
+  if (lane < cnt) rec_off[l0 + lane + 1] = excl + incl;
+  if (u == u0 && lane == 0) rec_off[0] = 0;
   if (lane < kU) {
     tab[lane] = lane < cnt ? incl - my_size : agg;
     tab[kU + 1 + lane] = ((late >> lane) & 1ull) ? 0xFFFFFFFFu : my_src;
@@ -1238,8 +1248,10 @@ constexpr uint32_t kDiffSpill = 24576;
 // 1.56-1.66 ms vs 64 pages with the spill slot 1.79-1.93 (the spill's write and read-back).
 constexpr uint32_t kDense64 = 112, kDense16 = 480;
 static inline uint64_t up256(uint64_t v) { return (v + 255) & ~255ull; }
-static uint64_t spill_pool_bytes(uint64_t n) {  // sized for the smallest spill unit (16 pages)
-  const uint64_t wgs = ((n + 15) / 16 + 3) / 4;
+// Sized for the smallest spill unit (16 pages), plus the partial units of up to kMaxSplit output
+// streams (launch_diff_split: each stream's last unit may be partial): two more workgroups.
+static uint64_t spill_pool_bytes(uint64_t n) {
+  const uint64_t wgs = ((n + 15) / 16 + 3) / 4 + 2;
   return (uint64_t)(wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill;
 }
 uint64_t diff_workspace_bytes(uint64_t n) {
@@ -1300,11 +1312,47 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
   return hipGetLastError();
 }
 
+static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
+                                   DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
+                                   Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap);
+
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target,
                        uint32_t bpp_hint) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
+  DiffSplit sp{};
+  sp.G = 1;
+  sp.rec_off[0] = rec_off;
+  sp.data[0] = data;
+  sp.cap[0] = cap;
+  sp.first[0] = 0;
+  sp.first[1] = n;
+  return launch_diff_impl(twin, cur, ids, sp, ws, ws_bytes, s, prof, target, bpp_hint, cap);
+}
+
+hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
+                             uint64_t ws_bytes, hipStream_t s, Prof* prof, uint32_t bpp_hint) {
+  if (sp.G < 1 || sp.G > kMaxSplit) return hipErrorInvalidValue;
+  uint64_t mincap = ~0ull;
+  for (uint32_t d = 0; d < sp.G; ++d) {
+    if (sp.first[d + 1] < sp.first[d]) return hipErrorInvalidValue;
+    mincap = sp.cap[d] < mincap ? sp.cap[d] : mincap;
+    if (sp.first[d + 1] == sp.first[d]) {  // an empty stream: rec_off[0] = 0, no work unit
+      const hipError_t e = hipMemsetAsync(sp.rec_off[d], 0, sizeof(uint64_t), s);
+      if (e != hipSuccess) return e;
+    }
+  }
+  if (sp.first[sp.G] == sp.first[0]) return hipSuccess;
+  return launch_diff_impl(twin, cur, nullptr, sp, ws, ws_bytes, s, prof, nullptr, bpp_hint,
+                          mincap);
+}
+
+// `cap` (the smallest stream capacity) only matters to workspaces that predate the spill pool.
+static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
+                                   DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
+                                   Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap) {
+  const uint64_t n = sp.first[sp.G] - sp.first[0];
   int v = diff_variant();
   // the spill pool's place in the workspace (after the largest status area n may need)
   const uint64_t status_end = up256(8 * (1 + max((n + 15) / 16, (min(n, kDiffShort) + 1) / 2)) + 64);
@@ -1321,7 +1369,10 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   const bool spill = v >= 5;
   if (spill && !pool_ok) return hipErrorInvalidValue;
   const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : (v == 2 || v == 6) ? 32 : 16;
-  const uint64_t nunits = (n + U - 1) / U;
+  sp.ustart[0] = 0;
+  for (uint32_t d = 0; d < sp.G; ++d)
+    sp.ustart[d + 1] = sp.ustart[d] + (sp.first[d + 1] - sp.first[d] + U - 1) / U;
+  const uint64_t nunits = sp.ustart[sp.G];
   if ((1 + nunits) * 8 > ws_bytes) return hipErrorInvalidValue;
   // every workgroup's spill slot (ticket % kSpillWGs) lies inside the pool
   const uint64_t wgs = (nunits + 3) / 4;
@@ -1349,8 +1400,8 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        : v == 3 ? diff_single_kernel<2, 8192, 4, false>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, n,
-                     rec_off, data, cap, reinterpret_cast<uint64_t*>(ws), target, gen, pool);
+  hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,
+                     reinterpret_cast<uint64_t*>(ws), target, gen, pool);
   return hipGetLastError();
 }
 

@@ -271,6 +271,17 @@ class Context:
         n = self._count(ids, n)
         check(lib().gdsm_twin(self.handle, self._ptr(ids), n), "gdsm_twin")
 
+    def diff_split(self, bounds, outs) -> None:
+        """One diff launch for several destinations (gdsm_diff_split): arena pages
+        [bounds[d], bounds[d+1]) into outs[d], each stream exactly what diff() of that range
+        writes."""
+        G = len(outs)
+        b = (C.c_uint64 * (G + 1))(*[int(x) for x in bounds])
+        arr = (GdsmRuns * G)(*[o.s for o in outs])
+        check(lib().gdsm_diff_split(self.handle, b, G, arr), "gdsm_diff_split")
+        for d, o in enumerate(outs):
+            o.s.n = arr[d].n
+
     def diff(self, ids=None, n: Optional[int] = None, out: Optional[Runs] = None, cap: int = 0,
              apply_to: Optional[str] = None) -> Runs:
         """TWIN vs CURRENT -> Runs; with apply_to (normally "replica"), the same kernel also

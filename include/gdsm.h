@@ -163,6 +163,12 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out);
  * gdsm_runs_total). Replaces the local-home half of gallocy's described release
  * (resources/NUTSHELL.md:59-69): the home applies what the writer diffed. */
 int gdsm_diff_apply(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out, int target);
+/* One diff launch for a release with several destinations: arena pages [bounds[d],
+ * bounds[d+1]) are diffed into out[d] (G <= 8 streams, each with its own buffers; record i of
+ * out[d] is page bounds[d] + i; out[d].n is set). Every stream is exactly what gdsm_diff of that
+ * range would write, but the G ranges share one launch instead of G (gdsm_exchange's per-home
+ * streams). */
+int gdsm_diff_split(gdsm_ctx* ctx, const uint64_t* bounds, uint32_t G, gdsm_runs* out);
 /* Synchronises, returns rec_off[n] in *total; -ENOSPC if it exceeded runs->cap. */
 int gdsm_runs_total(gdsm_ctx* ctx, const gdsm_runs* runs, uint64_t* total);
 /* Applies `in` to arena `target` (normally GDSM_REPLICA) for the listed pages (ids unique). */

@@ -95,12 +95,13 @@ def test_no_gpu_is_reported_not_crashed():
 def test_workspace_sizing():
     """gdsm_diff_workspace_bytes(n) for the single-pass diff: a ticket counter and one 8-B
     look-back granule per 16 pages, then the spill pool sized for the smallest spill geometry
-    (16 pages per wave: a generation word per workgroup slot, up to 1280 workgroup slots of
-    4 x 24 KiB); non-decreasing in n."""
+    (16 pages per wave, plus two workgroups for the partial units of split streams: a
+    generation word per workgroup slot, up to 1280 workgroup slots of 4 x 24 KiB); non-decreasing
+    in n."""
     from gallocy_amd import _lib
     lib = _lib.load()
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
-    slots = lambda n: min(1280, ((n + 15) // 16 + 3) // 4)  # noqa: E731
+    slots = lambda n: min(1280, ((n + 15) // 16 + 3) // 4 + 2)  # noqa: E731
     for n in (1, 1000, 1 << 20, 1 << 24):
         want = up(8 * (1 + max((n + 15) // 16, (min(n, 32768) + 1) // 2)) + 64) + up(4 * 1280) \
             + slots(n) * 4 * 24576

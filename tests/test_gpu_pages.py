@@ -7,6 +7,7 @@ import pytest
 
 import gallocy_amd as ga
 from gallocy_amd import _lib
+from gallocy_amd._lib import GdsmRuns
 from gallocy_amd.gdsm import GdsmError, HostRuns, Runs
 from oracle import oracle
 from tests.helpers import c1_windows, np_diff, runs_positions
@@ -758,3 +759,54 @@ def test_apply_variants_long_lists(variant):
             assert np.array_equal(c.download("replica"), want)
     finally:
         L.gdsm_tune(b"apply_variant", 0)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 6, 7])
+def test_diff_split_equals_per_range_diffs(variant):
+    """gdsm_diff_split (one launch, G <= 8 streams, each with its own look-back chain) writes
+    exactly the stream gdsm_diff writes for each range, in every diff geometry: ranges that are
+    not unit multiples, empty ranges, a single page, uniform and clustered pages, and the
+    largest-record pages; bad arguments are refused."""
+    L = _lib.load()
+    assert L.gdsm_tune(b"diff_variant", variant) == 0
+    rng = np.random.default_rng(1200 + variant)
+    try:
+        n = 40000
+        tw, cu = oracle.gen_pages(n, seed=12, mode=1, ppm=100000)
+        tw[:300] = rng.integers(0, 256, (300, 4096), dtype=np.uint8)
+        cu[:300] = tw[:300]
+        cu[:300, ::2] ^= 0x5A  # 2048 runs per page: the largest records
+        cu[300:20000] = tw[300:20000]
+        w = rng.random((19700, 512)) < 0.01
+        cu[300:20000].reshape(19700, 512, 8)[w] ^= 0x11
+        with ga.Context(n) as c:
+            c.upload("twin", tw)
+            c.upload("current", cu)
+            for G, bounds in [(1, [0, n]), (2, [0, 17, n]), (8, None), (5, [0, 0, 1, 1, 30000, n]),
+                              (3, [100, 100, 100, 100])]:
+                if bounds is None:
+                    bounds = [0] + sorted(rng.integers(0, n, G - 1).tolist()) + [n]
+                outs = [Runs(c, max(1, bounds[d + 1] - bounds[d]),
+                             cap=max(64, 11000 * (bounds[d + 1] - bounds[d]))) for d in range(G)]
+                c.diff_split(bounds, outs)
+                for d in range(G):
+                    a, b = bounds[d], bounds[d + 1]
+                    got = outs[d].to_host()
+                    assert outs[d].n == b - a
+                    ro, data = oracle.diff_pages(tw[a:b], cu[a:b])
+                    _eq_runs(got, ro, data)
+                for o in outs:
+                    o.free()
+            one = [Runs(c, 10, cap=4096) for _ in range(2)]
+            b = (C.c_uint64 * 3)(0, 10, 5)  # decreasing
+            arr = (GdsmRuns * 2)(*[o.s for o in one])
+            assert L.gdsm_diff_split(c.handle, b, 2, arr) == -22
+            b = (C.c_uint64 * 3)(0, 5, n + 1)  # past the arenas
+            assert L.gdsm_diff_split(c.handle, b, 2, arr) == -22
+            arr = (GdsmRuns * 2)(one[0].s, one[0].s)  # one stream twice
+            b = (C.c_uint64 * 3)(0, 5, 10)
+            assert L.gdsm_diff_split(c.handle, b, 2, arr) == -22
+            b = (C.c_uint64 * 10)(*range(10))
+            assert L.gdsm_diff_split(c.handle, b, 9, (GdsmRuns * 9)()) == -22
+    finally:
+        L.gdsm_tune(b"diff_variant", 0)
