@@ -641,7 +641,14 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
 // has published its inclusive prefix, and every wave publishes only after its loads landed, so
 // the head's wave has read the word before anyone stores it. Page ids are taken from the low
 // dword (n_pages <= 2^28; any high-dword bit rejects the batch).
-constexpr uint32_t kFK = 32;                // events per lane
+// Events per lane: 32 (2048-event blocks). A -DGDSM_FOLD_K=16 build (1024-event blocks, 64 VGPRs
+// and 16 KiB of LDS per workgroup: 8 waves/SIMD instead of 5) is bit-exact and measured slower,
+// 3.18 / 3.03 ms against 2.42 / 2.43 (uniform / Zipf, same box): twice the blocks, twice the
+// per-block prologue, look-back and tail.
+#ifndef GDSM_FOLD_K
+#define GDSM_FOLD_K 32
+#endif
+constexpr uint32_t kFK = GDSM_FOLD_K;       // events per lane (16 or 32: hm is one 32-bit mask)
 constexpr uint32_t kFH = 16;                // of them held in registers at a time
 constexpr uint32_t kFBlock = 64 * kFK;
 constexpr uint32_t kHE = 0x10000u, kHW = 0x20000u, kPRE = 0x40000u, kHRead = 0xFFu;
@@ -816,7 +823,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     }
     xp = X[kFH - 1];
   }
-  if (kFull) hm = __brev(hm);
+  if (kFull) hm = __brev(hm) >> (32u - kFK);
   const uint32_t hc = (uint32_t)__popc(hm);
   uint32_t xf = 0, xl = 0;  // the lane's first and last head events
   if (hc) {
