@@ -3,6 +3,7 @@
 // page. Variants: pages per wave, pages in flight per wave, nt vs default loads, grid shape.
 // Not product code: it measures the ceiling the diff kernel is held against.
 //   hipcc --offload-arch=gfx950 -O3 scripts/dev/read_probe.hip -o scripts/dev/read_probe
+//   read_probe <pages> [w]   (w: the record-stream variants only)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -86,6 +87,66 @@ __global__ __launch_bounds__(256) void rd_pipe(const u32x4* __restrict__ a, cons
     }
     const uint64_t m = __ballot(d != 0);
     if (lane == 0) out[w0 + j] = (uint32_t)__popcll(m);
+  }
+}
+
+// rd_pipe plus a record stream: WB bytes per page stored to out_w (dword stores, the diff's
+// coalesced copy shape), either right after each page (kEnd false) or for the whole unit after its
+// last page (kEnd true, the diff's order: records leave after the unit's look-back). The ceiling
+// for a diff whose records are not small (config 3: ~850 B per page).
+template <int PPW, uint32_t WB, bool kNT, bool kEnd, bool kX4 = false>
+__global__ __launch_bounds__(256) void rd_pipe_w(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
+                                                 uint32_t* __restrict__ out, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wave) * PPW;
+  if (w0 >= n) return;
+  uint32_t* ow = out + n;  // the record stream, after the per-page words
+  u32x4 t[4], c[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    t[k] = ld<true>(a + w0 * 256 + k * 64 + lane);
+    c[k] = ld<true>(b + w0 * 256 + k * 64 + lane);
+  }
+  uint32_t acc = 0;
+  for (int j = 0; j < PPW && w0 + j < n; ++j) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32x4 x = t[k] ^ c[k];
+      d |= x.x | x.y | x.z | x.w;
+    }
+    const uint64_t p = w0 + j + 1;
+    if (j + 1 < PPW && p < n) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        t[k] = ld<true>(a + p * 256 + k * 64 + lane);
+        c[k] = ld<true>(b + p * 256 + k * 64 + lane);
+      }
+    }
+    acc ^= d;
+    if (!kEnd) {
+      uint32_t* dst = ow + (w0 + j) * (WB / 4);
+      for (uint32_t g = lane; g < WB / 4; g += 64) {
+        if (kNT) __builtin_nontemporal_store(d ^ g, dst + g); else dst[g] = d ^ g;
+      }
+    }
+    const uint64_t m = __ballot(d != 0);
+    if (lane == 0) out[w0 + j] = (uint32_t)__popcll(m);
+  }
+  if (kEnd) {
+    const uint64_t np = min((uint64_t)PPW, n - w0);
+    uint32_t* dst = ow + w0 * (WB / 4);
+    if (kX4) {  // 16-B stores (the unit's stream starts 16-B aligned here: 832 = 52 * 16)
+      u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+      for (uint32_t g = lane; g < np * (WB / 16); g += 64) {
+        const u32x4 v = (u32x4){acc ^ g, acc, g, 1u};
+        if (kNT) __builtin_nontemporal_store(v, d4 + g); else d4[g] = v;
+      }
+    } else {
+      for (uint32_t g = lane; g < np * (WB / 4); g += 64) {
+        if (kNT) __builtin_nontemporal_store(acc ^ g, dst + g); else dst[g] = acc ^ g;
+      }
+    }
   }
 }
 
@@ -186,7 +247,8 @@ int main(int argc, char** argv) {
   uint32_t* out;
   CK(hipMalloc(&a, chunks * 16));
   CK(hipMalloc(&b, chunks * 16));
-  CK(hipMalloc(&out, n * 4));
+  const bool wmode = argc > 2 && argv[2][0] == 'w';  // record-stream variants only
+  CK(hipMalloc(&out, n * 4 + (wmode ? n * 832 : 0)));
   hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, a, chunks, 1u);
   hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, b, chunks, 1u);
   CK(hipDeviceSynchronize());
@@ -211,6 +273,16 @@ int main(int argc, char** argv) {
       {"flat 8192 nt       ", rd_flat<true>, 8192, chunks},
       {"flat 8192          ", rd_flat<false>, 8192, chunks},
   };
+  if (wmode)
+    vs = {
+        {"pipe ppw16 nt      ", rd_pipe<16>, (unsigned)(n / 64), n},
+        {"pipe16 +832 end nt ", rd_pipe_w<16, 832, true, true>, (unsigned)(n / 64), n},
+        {"pipe16 +832 end    ", rd_pipe_w<16, 832, false, true>, (unsigned)(n / 64), n},
+        {"pipe16 +832 page nt", rd_pipe_w<16, 832, true, false>, (unsigned)(n / 64), n},
+        {"pipe64 +832 end nt ", rd_pipe_w<64, 832, true, true>, (unsigned)(n / 256), n},
+        {"pipe16 +832 end nt x4", rd_pipe_w<16, 832, true, true, true>, (unsigned)(n / 64), n},
+        {"pipe16 +832 end x4 ", rd_pipe_w<16, 832, false, true, true>, (unsigned)(n / 64), n},
+    };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -231,8 +303,9 @@ int main(int argc, char** argv) {
   for (size_t v = 0; v < vs.size(); ++v) {
     std::sort(ms[v].begin(), ms[v].end());
     const double med = ms[v][R / 2];
-    printf("%s  median %.4f ms  min %.4f ms  %.0f GB/s\n", vs[v].name, med, ms[v][0],
-           2.0 * chunks * 16 / (med * 1e-3) / 1e9);
+    const double wb = (wmode && v > 0) ? 832.0 * n : 0.0;
+    printf("%s  median %.4f ms  min %.4f ms  %.0f GB/s (read + written)\n", vs[v].name, med,
+           ms[v][0], (2.0 * chunks * 16 + wb) / (med * 1e-3) / 1e9);
   }
   return 0;
 }
