@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
     ap.add_argument("--coh-pages", type=int, default=16 << 20, help="coherence: pages")
     ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
+    ap.add_argument("--coh-nodes", type=int, default=8,
+                    help="coherence: DSM nodes of the batch (BASELINE config 4: 8)")
     return ap.parse_args()
 
 
@@ -229,9 +231,12 @@ def run_coherence(args):
     n, E = args.coh_pages, args.events
     counts = event_counts(n, E, args.dist, seed=args.seed)
     ctx = ga.Context(n, arenas=())
-    ev = ctx.gen_events(counts, seed=args.seed, n_nodes=8, write_pct=20)
+    nn = args.coh_nodes
+    if not 1 <= nn <= 8:
+        raise SystemExit("--coh-nodes must be 1-8")
+    ev = ctx.gen_events(counts, seed=args.seed, n_nodes=nn, write_pct=20)
     touched = int((counts > 0).sum())
-    ctx.coh_init(8)
+    ctx.coh_init(nn)
     tot_dev = ctx.buffer(80)
     L = ga.gdsm.lib()
 
@@ -263,7 +268,7 @@ def run_coherence(args):
            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
            "data": f"synthetic ({args.dist} page popularity, SPEC §6 events)",
-           "config": {"workload": f"{n} pages, 8 nodes, {ev.count} events/batch, {args.dist}, 20% writes",
+           "config": {"workload": f"{n} pages, {nn} nodes, {ev.count} events/batch, {args.dist}, 20% writes",
                       "touched_pages": touched},
            "roofline": {"bound": "hbm", "kernel": "gdsm::coh_fold_kernel", "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -812,7 +812,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   // ---- heads (a new page), validity. (Sortedness inside a lane is checked where the walk meets
   // a head; the first / last head events are read back from LDS.)
   uint32_t X[kFH];
-  uint32_t hm = 0, nodes = 0;
+  uint32_t hm = 0;
   uint32_t bad = hib ? 1u : 0u;
 #pragma unroll
   for (uint32_t h = 0; h < kFK / kFH; ++h) {
@@ -830,7 +830,6 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
           hm = shl1_add(hm, __ballot(head));  // bit 31 - k, one v_addc per event
         else
           hm |= (head ? 1u : 0u) << k;
-        if (kNodes) nodes = max(nodes, x & 14u);  // 2 * the largest node
       }
     }
     xp = X[kFH - 1];
@@ -844,8 +843,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   }
   // opaque from here on: the walk re-derives its per-event head flags from these words instead
   // of the compiler keeping the prologue's 32 masks live
-  asm volatile("" : "+v"(hm), "+v"(xf), "+v"(xl), "+v"(nodes));
-  if (kNodes && (nodes >> 1) >= n_nodes) bad = 1;
+  asm volatile("" : "+v"(hm), "+v"(xf), "+v"(xl));
   if (nv && (xlast >> 4) >= n_pages) bad = 1;
   // does the lane's last event end its segment? (the next lane's first event is a head, or the
   // next wave's, or the batch ends there)
@@ -980,6 +978,18 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   }
   if (nv && last_end) COH_END_SEG(xlast >> 4);
   if (hasS) COH_FLUSH_S();
+  if (kNodes) {
+    // a node outside the group fails the batch: checked from the LDS copy once the walk's
+    // registers are free (taken in the heads pass, it kept the fold at 103 VGPRs, 4 waves/SIMD)
+    uint32_t nodes = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kFK / 4; ++r) {
+      const uint4 w = *reinterpret_cast<const uint4*>(tr + fold_slot(kFK * lane + 4 * r));
+      nodes = max(nodes, max(max(w.x & 14u, w.y & 14u), max(w.z & 14u, w.w & 14u)));
+    }
+    // (slots past the block's end in a partial block hold the zero events written for them)
+    if ((nodes >> 1) >= n_nodes) bad = 1;
+  }
 #undef COH_END_SEG
 #undef COH_FLUSH_S
 
