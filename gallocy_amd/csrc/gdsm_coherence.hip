@@ -655,6 +655,12 @@ __global__ __launch_bounds__(256) void coh_apply_block_kernel(
 // so without the raise its loads queue behind the older waves' walks, and its whole block
 // starts late. Measured, same box, alternating (uniform / Zipf ms): 0: 2.41 / 2.42-2.43,
 // 1: 2.29-2.32 / 2.41-2.43, 5: 2.30-2.31 / 2.42-2.43, 2: 2.40-2.41 / 2.42-2.44, 3: 2.29-2.30.
+// GDSM_FOLD_PRE2 (default 1): the words of a lane's first GDSM_FOLD_PRE2 middle heads (its
+// second, third head when it has more) are loaded with the first and last heads' words, before
+// the walk, instead of inside it.
+#ifndef GDSM_FOLD_PRE2
+#define GDSM_FOLD_PRE2 1
+#endif
 #ifndef GDSM_FOLD_PRIO
 #define GDSM_FOLD_PRIO 5
 #endif
@@ -853,16 +859,26 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   if (!kFull && nv > 0 && g0 + nv == n) last_end = true;
 
   // ---- page-table words of the lane's last and first heads (one gathered load each)
-  uint64_t Wl = 0, Wf = 0;  // last and first heads (a lane's other heads load in the walk)
+  uint64_t Wl = 0, Wf = 0, Ws = 0, Wt = 0;  // last, first, second, third heads (others: walk)
   {
     const uint32_t pl = xl >> 4, pf = xf >> 4;
     if (hc && pl < n_pages) Wl = pt[pl];
     if (hc > 1 && pf < n_pages) Wf = pt[pf];
+    if (GDSM_FOLD_PRE2 && hc > 2) {  // a middle head: its page lies inside this lane
+      const uint32_t h2 = hm & (hm - 1u);
+      const uint32_t p2 = tr[fold_slot(kFK * lane + (uint32_t)__builtin_ctz(h2))] >> 4;
+      if (p2 < n_pages) Ws = pt[p2];
+      if (GDSM_FOLD_PRE2 > 1 && hc > 3) {
+        const uint32_t h3 = h2 & (h2 - 1u);
+        const uint32_t p3 = tr[fold_slot(kFK * lane + (uint32_t)__builtin_ctz(h3))] >> 4;
+        if (p3 < n_pages) Wt = pt[p3];
+      }
+    }
   }
   const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
   const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
   if ((GDSM_FOLD_PRIO & 5) == 5) __builtin_amdgcn_s_setprio(0);
-  asm volatile("" : "+v"(Wf));  // waited for here, not inside the walk
+  asm volatile("" : "+v"(Wf), "+v"(Ws), "+v"(Wt));  // waited for here, not inside the walk
   // Early publication (see above): the words of every lane's first and last heads have landed
   // (the wave's last head's word is the only one another wave may store), so the head flag goes
   // out with it and ordered successors need not wait for this walk either.
@@ -934,7 +950,13 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
             // walk; a middle head (lanes with >= 3 heads) loads its word here. A word prefetched
             // one head ahead instead made every head step wait: the wave's one vmcnt counter also
             // counts the walk's stores, and some lane is at a head at most steps.
-            if (hs != 0) {
+            if (GDSM_FOLD_PRE2 && hs == 1) {
+              B = (uint32_t)Ws & 0x7FFFFu;
+              Bfo = (uint32_t)(Ws >> 32);
+            } else if (GDSM_FOLD_PRE2 > 1 && hs == 2) {
+              B = (uint32_t)Wt & 0x7FFFFu;
+              Bfo = (uint32_t)(Wt >> 32);
+            } else if (hs != 0) {
               const uint32_t pg = x >> 4;  // a page >= n_pages fails the batch (clamped load)
               const uint64_t w = pt[pg < n_pages ? pg : 0u];
               B = (uint32_t)w & 0x7FFFFu;
