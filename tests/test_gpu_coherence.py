@@ -116,6 +116,31 @@ def test_node_outside_the_table_is_rejected():
         c.coherence_batch(np.array([(1 << 4) | (2 << 1)], np.uint64))
 
 
+def test_node_outside_the_table_is_rejected_in_whole_blocks():
+    """The same rejection when the bad event sits in a whole 2048-event block (the vector-load
+    instance, whose node check reads the block's LDS copy after the walk) — its first, middle and
+    last events, a later block, and the partial block at the end — and a clean batch still folds
+    like the oracle."""
+    n = 4096
+    counts = zipf_counts(n, 3 * 2048 + 5, seed=7)
+    good = oracle.gen_events(counts, seed=11, n_nodes=5, write_pct=25)
+    with ga.Context(n, arenas=()) as c:
+        for pos in (0, 1000, 2047, 2048, 4095, 6143, 6146):
+            ev = good.copy()
+            ev[pos] = (ev[pos] & ~np.uint64(14)) | np.uint64(6 << 1)  # node 6 of 5
+            c.coh_init(5)
+            with pytest.raises(GdsmError) as ei:
+                c.coherence_batch(ev)
+            assert ei.value.errno == 22, pos
+        c.coh_init(5)
+        tot = c.coherence_batch(good)
+        st, fl = oracle.coh_init(n, 5)
+        rc, otot = oracle.coherence(st, fl, good, n_nodes=5)
+        assert rc == 0 and tot == otot
+        gst, gfl = c.coh_download()
+        assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+
+
 def _batch_from(c, host, unaligned):
     """Device copy of a host event batch: 16-B aligned, or one u64 in (8-B aligned only), which
     takes the scalar-load instance of pass C."""
