@@ -67,10 +67,13 @@ def parse():
                          "then gdsm_apply of the stream")
     ap.add_argument("--compare-overlap", action="store_true",
                     help="also time the other overlap mode (reported beside the measured one)")
-    ap.add_argument("--workload", choices=["pages", "coherence", "mmult", "nw"], default="pages",
+    ap.add_argument("--workload", choices=["pages", "coherence", "mmult", "nw", "twin"],
+                    default="pages",
                     help="pages: BASELINE configs[1]/[2] (the headline); coherence: configs[3]; "
                          "mmult: configs[4] trace replay; nw: the reference diff() (NW alignment) "
-                         "on the GPU over configs[0]-shaped page pairs")
+                         "on the GPU over configs[0]-shaped page pairs; twin: the twin step "
+                         "(TWIN := CURRENT) of the north-star pages, beside the writer-side "
+                         "re-twin of only the dirty bytes (the release's stream applied to TWIN)")
     ap.add_argument("--nw-pairs", type=int, default=512, help="nw: 4 KiB page pairs per batch")
     ap.add_argument("--ndim", type=int, default=1000, help="mmult: matrix size (<= 1021)")
     ap.add_argument("--nodes", type=int, default=4, help="mmult: simulated DSM nodes (1-8)")
@@ -142,6 +145,29 @@ def efficiency_ref(pages_total: int, mode: str, ppm: int):
 XGMI_LINK_GBS = 153.0  # per xGMI link, one direction (MI355X_MICROARCH.md); 7 links per GPU
 
 
+def host_info() -> dict:
+    """nproc, the CPU model and the host RAM (BASELINE.md timing rules), next to CPU numbers."""
+    out = {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
+    try:
+        out["host_cpu"] = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
+    except Exception:  # noqa: BLE001
+        pass
+    try:
+        kb = int([ln for ln in open("/proc/meminfo") if ln.startswith("MemTotal")][0].split()[1])
+        out["host_ram_gib"] = round(kb / (1 << 20), 1)
+    except Exception:  # noqa: BLE001
+        pass
+    return out
+
+
+def cpu_threads() -> int:
+    """The CPU share this process may use: OMP_NUM_THREADS when set (the GPU box exports its
+    share there; os.cpu_count() is the whole machine), else the affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(int(env), aff) if env and env.isdigit() else aff)
+
+
 def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
     """The C oracle (oracle/liboracle.so, -O3, OpenMP, timed in C) on a bounded sample of the
     workload: one thread, then all of this process's CPU share (single-core and
@@ -150,9 +176,7 @@ def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
     n1, nper = 32768, 16384
     pages1, dt1, ok1 = oracle.bench_diff_apply(n1, mode, ppm, seed, seconds / 2, 1)
     assert ok1
-    # The box exports OMP_NUM_THREADS = its CPU share; os.cpu_count() is the whole machine.
-    nt = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
-    nt = max(1, min(nt, len(os.sched_getaffinity(0)), 16))
+    nt = cpu_threads()
     pages, dt, ok = oracle.bench_diff_apply(nper, mode, ppm, seed, seconds / 2, nt)
     assert ok
     out = {"value": round(pages / dt, 1), "unit": "pages/s", "cores": nt, "kind": "port",
@@ -174,12 +198,7 @@ def cpu_baseline(mode: int, ppm: int, seed: int, seconds: float):
                         "sources (oracle/_ref); extrapolated, the reference crashes at 4 KiB"}
         except Exception as e:  # noqa: BLE001
             out["reference_nw_diff"] = {"error": str(e)[:200]}
-    try:
-        import platform
-        out["host_cpu"] = (open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0]
-                           .strip(": \t") or platform.processor())
-    except Exception:  # noqa: BLE001
-        pass
+    out.update(host_info())
     return out
 
 
@@ -220,21 +239,57 @@ def read_coh_traffic(dist: str, pages: int, events: int):
     return None, None
 
 
+def ranks_setup():
+    """(rank, world, local device) under a launcher (gloo carries barriers and the max-over-ranks
+    time; nothing of the data path), or (0, 1, 0)."""
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    return rank, world, local
+
+
+def max_over_ranks(dt: float, world: int) -> float:
+    if world == 1:
+        return dt
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world: int):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
 def run_coherence(args):
     """BASELINE configs[3]: batched coherence, 16M pages, 8 nodes, 1B events (Zipf 0.8 or
-    uniform pages, 20 % writes), one GPU. A step = one whole batch through the page table."""
+    uniform pages, 20 % writes), one GPU. A step = one whole batch through the page table.
+    N > 1 GPUs: the page table is sharded by home (SPEC §5b: rank r holds pages [r n/N,
+    (r+1) n/N)) and every home folds the batch of its own pages (n/N pages, E/N events, the
+    events as gdsm_route_events delivers them); no collective in the timed region (strong
+    scaling, the same 16M pages and 1B events in all)."""
     import torch
 
     import gallocy_amd as ga
     from gallocy_amd.workloads import event_counts
-    torch.cuda.set_device(0)
-    n, E = args.coh_pages, args.events
-    counts = event_counts(n, E, args.dist, seed=args.seed)
-    ctx = ga.Context(n, arenas=())
+    rank, world, local = ranks_setup()
+    if args.coh_pages % world or args.events % world:
+        raise SystemExit("--coh-pages and --events must be multiples of the GPU count")
+    n, E = args.coh_pages // world, args.events // world
+    counts = event_counts(n, E, args.dist, seed=args.seed + rank)
+    ctx = ga.Context(n, arenas=(), device=local)
     nn = args.coh_nodes
     if not 1 <= nn <= 8:
         raise SystemExit("--coh-nodes must be 1-8")
-    ev = ctx.gen_events(counts, seed=args.seed, n_nodes=nn, write_pct=20)
+    ev = ctx.gen_events(counts, seed=args.seed + rank, n_nodes=nn, write_pct=20)
     touched = int((counts > 0).sum())
     ctx.coh_init(nn)
     tot_dev = ctx.buffer(80)
@@ -249,26 +304,40 @@ def run_coherence(args):
         step()
     ctx.sync()
     torch.cuda.synchronize()
+    barrier(world)
     ctx.prof_enable(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     ctx.sync()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = max_over_ranks(time.perf_counter() - t0, world)
     prof = ctx.prof_read()
     totals = tot_dev.download(np.uint64, 10)
-    main_ms = prof["coh_fold"][0] / max(1, prof["coh_fold"][1])
+    main_ms = max_over_ranks(prof["coh_fold"][0] / max(1, prof["coh_fold"][1]), world)
     alg = ev.count * 8 + touched * 16  # events read + state/faults words read and written
     achieved = alg / (main_ms * 1e-3) / 1e9
     traffic, traffic_src = read_coh_traffic(args.dist, n, E)
     stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]} for k, v in prof.items() if v[1]}
-    res = {"metric": "coherence events/sec", "value": round(ev.count * args.steps / dt, 1),
-           "unit": "events/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+    all_events = ev.count
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([ev.count, touched], dtype=torch.int64)
+        dist.all_reduce(t)
+        all_events = int(t[0])
+    if rank != 0:
+        ctx.close()
+        barrier(world)
+        return
+    res = {"metric": "coherence events/sec", "value": round(all_events * args.steps / dt, 1),
+           "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "u64",
            "data": f"synthetic ({args.dist} page popularity, SPEC §6 events)",
-           "config": {"workload": f"{n} pages, {nn} nodes, {ev.count} events/batch, {args.dist}, 20% writes",
+           "config": {"workload": f"{n * world} pages, {nn} nodes, {all_events} events/batch, "
+                                  f"{args.dist}, 20% writes"
+                                  + (f", page table sharded over {world} GPUs (rank 0's shard: "
+                                     f"{n} pages, {ev.count} events)" if world > 1 else ""),
                       "touched_pages": touched},
            "roofline": {"bound": "hbm", "kernel": "gdsm::coh_fold_kernel", "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -279,13 +348,12 @@ def run_coherence(args):
            "last_batch_totals": {"invalidations": int(totals[0]), "transfers": int(totals[1]),
                                  "node_faults": [int(x) for x in totals[2:]]},
            "cpu_baseline": None}
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
         from oracle import oracle
         m = 1 << 20
         sub = event_counts(m, 1 << 26, args.dist, seed=args.seed)
         hev = oracle.gen_events(sub, seed=args.seed)
-        nt = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
-        nt = max(1, min(nt, len(os.sched_getaffinity(0)), 16))
+        nt = cpu_threads()
         d1, t1 = oracle.bench_coherence(sub, hev, args.cpu_seconds / 2, 1)
         dn, tn = oracle.bench_coherence(sub, hev, args.cpu_seconds / 2, nt)
         res["cpu_baseline"] = {
@@ -295,9 +363,155 @@ def run_coherence(args):
                       f"{args.cpu_seconds / 2:.1f} s, oracle or_coherence -O3, timed in C",
             "single_thread": {"value": round(d1 / t1, 1), "cores": 1,
                               "sample": f"the same batch, {d1 // max(1, len(hev))} passes, "
-                                        f"{t1:.1f} s"}}
+                                        f"{t1:.1f} s"}, **host_info()}
     print(json.dumps(res), flush=True)
     ctx.close()
+    barrier(world)
+
+
+def run_twin(args):
+    """The twin step of north_star ("page twin/diff creation") on the north-star pages (16M x 4
+    KiB, 1 % word writes), one GPU per rank (replicas at N > 1, weak scaling). A step =
+    gdsm_twin of every page (TWIN := CURRENT, the copy that opens a write interval: 8192 B of
+    HBM per page). Reported beside it: the writer-side re-twin a release can do instead, the
+    release's own diff stream applied to TWIN (gdsm_apply, |D| + |P| bytes per page), which
+    leaves TWIN == CURRENT too (checked)."""
+    import torch
+
+    import gallocy_amd as ga
+    rank, world, local = ranks_setup()
+    n = args.pages or (16 << 20)
+    mode = ga.GEN_UNIFORM if (args.mode or "uniform") == "uniform" else ga.GEN_CLUSTERED
+    ppm = args.ppm if args.ppm is not None else (10000 if mode == ga.GEN_UNIFORM else 100000)
+    ctx = ga.Context(n, device=local, arenas=("twin", "current"))
+    ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n,
+                  arenas=("twin", "current"))
+    runs = ctx.diff(cap=n * (128 if mode == ga.GEN_UNIFORM else 1024))
+    total = runs.total()
+    host = runs.to_host()
+    pay = payload_bytes(host.rec_off, host.data)
+    del host
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        ctx.sync()
+        torch.cuda.synchronize()
+        barrier(world)
+        ctx.prof_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        ctx.sync()
+        torch.cuda.synchronize()
+        dt = max_over_ranks(time.perf_counter() - t0, world)
+        return dt, ctx.prof_read()
+
+    dt, prof = timed(lambda: ctx.twin())
+    twin_ms = max_over_ranks(prof["twin"][0] / max(1, prof["twin"][1]), world)
+    ok_full = ctx.diff(cap=1 << 20).total() == 0
+    # re-twin by the stream: TWIN back to its generated state, then the stream applied to it
+    ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n, arenas=("twin",))
+    dt_a, prof_a = timed(lambda: ctx.apply(runs, "twin"))
+    apply_ms = max_over_ranks(prof_a["apply"][0] / max(1, prof_a["apply"][1]), world)
+    ok_apply = ctx.diff(cap=1 << 20).total() == 0
+    alg = 8192 * n
+    achieved = alg / (twin_ms * 1e-3) / 1e9
+    res = None
+    if rank == 0:
+        res = {"metric": "pages twinned/sec (4 KiB)", "value": round(world * n * args.steps / dt, 1),
+               "unit": "pages/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+               "data": "synthetic (counter-hash pages, docs/SPEC.md §6)",
+               "config": {"workload": f"{n} x 4 KiB pages per GPU, gdsm_twin of every page"
+                                      + (f", {world} replicas" if world > 1 else ""),
+                          "pages_per_gpu": n, "seed": args.seed},
+               "roofline": {"bound": "hbm", "kernel": "gdsm::twin_kernel",
+                            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                            "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(twin_ms, 4)},
+               "twin_equals_current": bool(ok_full),
+               "retwin_by_stream": {
+                   "kernel": "gdsm::apply_flat_kernel (target TWIN)",
+                   "ms_per_launch": round(apply_ms, 4),
+                   "algorithmic_bytes_per_launch": int(total + pay),
+                   "achieved_gbs": round((total + pay) / (apply_ms * 1e-3) / 1e9, 1),
+                   "speedup_vs_full_twin": round(twin_ms / apply_ms, 2),
+                   "twin_equals_current": bool(ok_apply),
+                   "note": "the release's diff stream applied to the writer's TWIN re-twins only "
+                           "the dirty bytes; it needs the stream the release computes anyway"},
+               "cpu_baseline": None}
+        if not args.no_cpu and world == 1:
+            m = 1 << 18
+            src = np.random.default_rng(args.seed).integers(0, 256, (m, 4096), dtype=np.uint8)
+            dst = np.empty_like(src)
+            reps, t1 = 0, time.perf_counter()
+            while time.perf_counter() - t1 < min(args.cpu_seconds, 6.0) or reps == 0:
+                np.copyto(dst, src)
+                reps += 1
+            ct = time.perf_counter() - t1
+            res["cpu_baseline"] = {"value": round(reps * m / ct, 1), "unit": "pages/s", "cores": 1,
+                                   "kind": "port",
+                                   "sample": f"{m} pages (1 GiB) copied {reps} times with "
+                                             "numpy.copyto (memcpy), one thread (or_twin's "
+                                             "per-page memcpy, oracle/gdsm_oracle.c)",
+                                   **host_info()}
+        print(json.dumps(res), flush=True)
+    runs.free()
+    ctx.close()
+    barrier(world)
+
+
+def mmult_cpu_baseline(ndim: int, nodes: int, seed: int) -> dict:
+    """Config 5 on the host: the same trace replayed round by round on one thread through the C
+    oracle (or_coherence of the round's events, the twin of the written pages, the row writes,
+    or_diff_pages of those pages, or_apply of the stream to the home copies), P node views side
+    by side as on the GPU. The home copies are checked against the product afterwards."""
+    from gallocy_amd.trace import PAGE_SZ, MmultTrace, c_row_values, mmult_layout, zone_image
+    from oracle import oracle
+    L = mmult_layout(ndim)
+    T = MmultTrace(L, nodes, seed)
+    Z = L.n_pages
+    img = zone_image(L).reshape(Z, PAGE_SZ)
+    cur = np.tile(img, (nodes, 1))
+    twin = cur.copy()
+    rep = img.copy()
+    flat = cur.reshape(-1)
+    st, fl = oracle.coh_init(Z, nodes)
+    rowvals = np.stack([c_row_values(L, i) for i in range(L.ndim)]).view(np.uint8)
+    plan = []
+    for r in range(T.rounds):
+        rows = T.round_rows(r)
+        ids, home = [], []
+        for t, i in rows:
+            wp = np.arange(int(L.c_rows[i]) // PAGE_SZ, (int(L.c_rows[i]) + 8 * ndim - 1) // PAGE_SZ + 1)
+            ids.append(t * Z + wp)
+            home.append(wp)
+        plan.append((T.round_events(r), rows, np.concatenate(ids).astype(np.uint32),
+                     np.concatenate(home).astype(np.uint32)))
+    rb = 8 * ndim
+    t0 = time.perf_counter()
+    for ev, rows, ids, home in plan:
+        oracle.coherence(st, fl, ev, n_nodes=nodes)
+        twin[ids] = cur[ids]
+        for t, i in rows:
+            o = t * Z * PAGE_SZ + int(L.c_rows[i])
+            flat[o:o + rb] = rowvals[i]
+        ro, data = oracle.diff_pages(twin, cur, ids, cap=len(ids) * 10244)
+        oracle.apply(rep, ro, data, home)
+    dt = time.perf_counter() - t0
+    z = img.copy().reshape(-1)
+    f64 = z.view("<f8")
+    for i in range(ndim):
+        o = int(L.c_rows[i]) // 8
+        f64[o:o + ndim] = c_row_values(L, i)
+    ok = bool(np.array_equal(rep.reshape(-1), z))
+    return {"value": round(T.rounds / dt, 1), "unit": "rounds/s", "cores": 1, "kind": "port",
+            "sample": f"the whole NDIM={ndim} trace ({T.rounds} rounds, {nodes} nodes) replayed "
+                      f"once through the C oracle (coherence, twin, row writes, diff, apply) in "
+                      f"{dt:.3f} s, Python driving the rounds",
+            "home_copy_equals_product": ok, **host_info()}
 
 
 def run_mmult_ranks(args, rank: int, world: int):
@@ -364,6 +578,34 @@ def run_mmult(args):
     R = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed)
     dt = R.run(graph=args.graph)
     ok = bool(np.array_equal(R.home_copy(), R.final_image()))
+    # latency breakdown: the same replay again on a fresh state with per-launch HIP events (a
+    # separate run, so the events do not weigh on `value`)
+    R2 = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed)
+    R2.data.prof_enable(True)
+    R2.pt.prof_enable(True)
+    dt2 = R2.run(graph=False)
+    pd, pp = R2.data.prof_read(), R2.pt.prof_read()
+    R2.close()
+    rounds = R.T.rounds
+    stages = {}
+    for k, v in list(pd.items()) + list(pp.items()):
+        if v[1]:
+            stages[k] = {"ms_per_launch": round(v[0] / v[1], 5),
+                         "launches_per_round": round(v[1] / rounds, 2)}
+    kern_ms = sum(v[0] for v in pd.values()) + sum(v[0] for v in pp.values())
+    launches = sum(v[1] for v in pd.values()) + sum(v[1] for v in pp.values())
+    copies = sum(len(R.rows[r]) for r in range(rounds))  # one row write (d2d copy) per row
+    latency = {"bound": "latency",
+               "kernel_launches_per_round": round(launches / rounds, 2),
+               "row_copies_per_round": round(copies / rounds, 2),
+               "host_syncs_per_round": 0,
+               "kernel_ms_per_round": round(kern_ms / rounds, 5),
+               "wall_ms_per_round_profiled": round(dt2 / rounds * 1e3, 5),
+               "stages": stages,
+               "note": "a round is ~12 dense pages: the kernels' own time is a fraction of the "
+                       "round, the rest is the device-side issue cost of ~10 dependent tiny "
+                       "operations on two streams; one HIP graph of every round (--graph) "
+                       "measured no faster (replay.py). No HBM or MFMA roofline applies."}
     res = {"metric": "mmult trace replay rounds/sec", "value": round(R.T.rounds / dt, 1),
            "unit": "rounds/s", "n_gpus": 1, "steps": R.T.rounds, "warmup": 0,
            "ms_per_step": round(dt / R.T.rounds * 1e3, 4), "higher_is_better": True,
@@ -379,7 +621,10 @@ def run_mmult(args):
            "rows_per_s": round(args.ndim / dt, 1),
            "home_copy_equals_product": ok,
            "totals": {"invalidations": int(R.totals[0]), "transfers": int(R.totals[1]),
-                      "node_faults": [int(x) for x in R.totals[2:]]}}
+                      "node_faults": [int(x) for x in R.totals[2:]]},
+           "roofline": None, "latency": latency,
+           "cpu_baseline": None if args.no_cpu else mmult_cpu_baseline(args.ndim, args.nodes,
+                                                                       args.seed)}
     print(json.dumps(res), flush=True)
     R.close()
 
@@ -393,19 +638,20 @@ def run_nw(args):
     pairs (twin, current with 1 % of 8-byte words rewritten: BASELINE configs[0]'s shape, which
     the reference itself cannot align: it crashes from 1181 bytes) through gdsm_nw_diff_batch.
     A step = one batch: DP fill + traceback + alignment strings. VALU-bound (no HBM or MFMA
-    roofline applies: 2 bits of traceback per cell are the only HBM traffic)."""
+    roofline applies: 2 bits of traceback per cell are the only HBM traffic). N > 1 GPUs:
+    replicas only (every rank aligns its own batch; nothing is exchanged), weak scaling."""
     import torch
 
     import gallocy_amd as ga
     from gallocy_amd import _lib
-    torch.cuda.set_device(0)
+    rank, world, local = ranks_setup()
     n, ln = args.nw_pairs, 4096
-    rng = np.random.default_rng(args.seed)
+    rng = np.random.default_rng(args.seed + rank)
     a = rng.integers(0, 256, (n, ln), dtype=np.uint8)
     b = a.copy()
     b.reshape(n, -1, 8)[rng.random((n, ln // 8)) < 0.01] ^= 0x5A
     off = np.arange(n + 1, dtype=np.uint64) * ln
-    ctx = ga.Context(1, arenas=())
+    ctx = ga.Context(1, arenas=(), device=local)
     da, doff, db = (ctx.buffer(x.nbytes).upload(x) for x in (a, off, b))
     ob = 2 * n * ln + n
     o1, o2, ol = ctx.buffer(ob), ctx.buffer(ob), ctx.buffer(8 * n)
@@ -419,6 +665,7 @@ def run_nw(args):
         step()
     ctx.sync()
     torch.cuda.synchronize()
+    barrier(world)
     ctx.prof_enable(True)
     ctx.prof_read()
     t0 = time.perf_counter()
@@ -426,35 +673,41 @@ def run_nw(args):
         step()
     ctx.sync()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = max_over_ranks(time.perf_counter() - t0, world)
     prof = ctx.prof_read()
     cells = n * (ln + 1) ** 2
-    fill_ms = prof["nw_fill"][0] / max(1, prof["nw_fill"][1])
+    fill_ms = max_over_ranks(prof["nw_fill"][0] / max(1, prof["nw_fill"][1]), world)
     # spot check against the oracle (first pair)
     from oracle import oracle
     L0 = int(ol.download(np.uint64, 1)[0])
     g1 = o1.download(np.uint8, L0)
     want = oracle.nw_diff(a[0].tobytes(), b[0].tobytes())
     assert g1.tobytes() == want[0], "GPU alignment differs from the oracle"
+    if rank != 0:
+        ctx.close()
+        barrier(world)
+        return
     achieved = cells * NW_OPS_PER_CELL / (fill_ms * 1e-3) / 1e12
     peak = VALU_PEAK_OPS / 1e12
     stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
               for k, v in prof.items() if v[1]}
     res = {"metric": "NW alignment DP cells/sec (reference diff() on GPU)",
-           "value": round(cells * args.steps / dt, 1), "unit": "cells/s", "n_gpus": 1,
+           "value": round(world * cells * args.steps / dt, 1), "unit": "cells/s",
+           "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "i32",
            "data": "synthetic 4 KiB page pairs, 1 % of 8-byte words rewritten",
-           "config": {"workload": f"{n} pairs x 4096 x 4096 bytes, diff() alignment",
-                      "pairs_per_s": round(n * args.steps / dt, 1)},
+           "config": {"workload": f"{n} pairs x 4096 x 4096 bytes per GPU, diff() alignment"
+                                  + (f", {world} replicas" if world > 1 else ""),
+                      "pairs_per_s": round(world * n * args.steps / dt, 1)},
            "roofline": {"bound": "valu", "kernel": "gdsm::nw_fill_kernel",
                         "achieved": round(achieved, 2), "peak": round(peak, 1),
                         "unit": "Tops/s", "frac": round(achieved / peak, 4), "traffic": None,
                         "ops_per_cell": NW_OPS_PER_CELL, "cells_per_launch": cells,
                         "avg_launch_ms": round(fill_ms, 4)},
            "stages": stages, "cpu_baseline": None}
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
         base = {}
         drv = oracle.REF_DRIVER
         if drv.exists():
@@ -478,16 +731,48 @@ def run_nw(args):
             res["cpu_baseline"]["oracle_port"] = port
     print(json.dumps(res), flush=True)
     ctx.close()
+    barrier(world)
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: this GPU-free parent starts the N ranks itself
+    (torch.distributed.run on 127.0.0.1, one process per GPU), before anything touches a GPU,
+    and returns their exit code; rank 0's JSON line goes to this process's stdout. Under a
+    launcher (WORLD_SIZE set) --gpus must equal the rank count. None: run here as one rank."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} "
+                             f"ranks (WORLD_SIZE)")
+        return None
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus == 1:
+        return None
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           str(ROOT / "bench.py"), *sys.argv[1:]]
+    log("bench.py: launching", args.gpus, "ranks:", " ".join(cmd[2:]))
+    return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
 
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     if args.workload == "coherence":
         return run_coherence(args)
     if args.workload == "nw":
         return run_nw(args)
     if args.workload == "mmult":
         return run_mmult(args)
+    if args.workload == "twin":
+        return run_twin(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -603,6 +888,20 @@ def main():
     # same launches the HIP events time
     dt_other = timed(not pipelined, False)[0] if args.compare_overlap else None
     dt, prof = timed(pipelined, True)
+    # The xGMI link alone: the same releases again (untimed for `value`) with GDSM_XCHG_TIMED, a
+    # device-side barrier before each transfer, so the exchange stage starts once every rank's
+    # streams are ready and times the RCCL group, not the wait for the peers' diffs.
+    link = None
+    if shard is not None and shard.comm is not None:
+        shard.flags |= exchange.XCHG_TIMED
+        try:
+            _, plink = timed(pipelined, True)
+        finally:
+            shard.flags &= ~exchange.XCHG_TIMED
+        link = [plink["exchange"][0] / args.steps, plink["exchange_wait"][0] / args.steps]
+        t = torch.tensor(link, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        link = t.tolist()
 
     # correctness of the measured work: REPLICA == CURRENT afterwards (diff of the two is empty)
     if shard is None:
@@ -640,20 +939,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         stage_ms = dict(zip(("diff", "exchange", "apply"), t.tolist()))
     xgmi = None
-    if shard is not None and stage_ms["exchange"] > 0:
+    if link is not None and link[0] > 0:
         moved = shard.moved_remote  # bytes this rank's exchange hands the transport per step
-        ach = moved / (stage_ms["exchange"] * 1e-3) / 1e9
+        ach = moved / (link[0] * 1e-3) / 1e9
         peak_node, peak_used = 7 * XGMI_LINK_GBS, (world - 1) * XGMI_LINK_GBS
         xgmi = {"bound": "xgmi", "achieved": round(ach, 2), "unit": "GB/s",
                 "peak": peak_node, "frac": round(ach / peak_node, 4),
                 "peak_links_used": peak_used, "frac_links_used": round(ach / peak_used, 4),
                 "bytes_per_step": int(moved),
-                "exchange_ms_per_step": round(stage_ms["exchange"], 4),
+                "link_ms_per_step": round(link[0], 4),
+                "exchange_ms_incl_wait": round(stage_ms["exchange"], 4),
+                "timed_run_exchange_ms_incl_wait": round(link[1], 4),
                 "note": "bytes one rank sends to its N-1 peers per step (rec_off + page indices + "
-                        "the byte budget of each stream) / the RCCL group's time on the exchange "
-                        "stream (HIP events; it includes waiting for the peers' diffs, so it is a "
-                        "lower bound on the link rate). peak: 7 links x 153 GB/s (all of an "
-                        "MI355X's xGMI); peak_links_used: the N-1 links one rank's peers use"}
+                        "the byte budget of each stream) / link_ms_per_step: the RCCL group's "
+                        "time on the exchange stream (HIP events, max over ranks) in a second run "
+                        "of the same K releases with GDSM_XCHG_TIMED, where a one-word device "
+                        "all-to-all before each transfer makes it start once every rank's "
+                        "streams are ready. exchange_ms_incl_wait: the measured run's exchange "
+                        "stage, which includes waiting for the peers' diffs. peak: 7 links x 153 "
+                        "GB/s (all of an MI355X's xGMI); peak_links_used: the N-1 links one "
+                        "rank's peers use"}
     ref_ms, ref_src = efficiency_ref(world * n, mode_name, ppm) if world > 1 else (None, None)
 
     if rank == 0:
@@ -701,6 +1006,7 @@ def main():
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "exchange": None if shard is None else {
                 "transport": shard.transport, "fixed_budgets": bool(shard.flags),
+                "comm_ranks": shard.comm.size()[0] if shard.comm is not None else None,
                 "recoveries": shard.recoveries,
                 "sent_remote_bytes_per_step": shard.sent_remote,
                 "received_bytes_per_step": shard.received},

@@ -37,6 +37,7 @@ class GdsmRuns(C.Structure):
 SIGNATURES = {
     "gdsm_version": (C.c_char_p, []),
     "gdsm_tune": (C.c_int, [C.c_char_p, C.c_int64]),
+    "gdsm_debug_fail_alloc": (C.c_int, [vp, C.c_int]),
     "gdsm_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "gdsm_init": (C.c_int, [C.POINTER(vp), C.c_int, C.c_uint64, C.c_uint32]),
     "gdsm_fini": (C.c_int, [vp]),

@@ -54,6 +54,7 @@ int ensure_aux(gdsm_ctx* ctx) {
 int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need) {
   if (*have >= need) return 0;
   if (ctx && ctx->capturing) return -EBUSY;  // size workspaces with gdsm_reserve before capturing
+  if (ctx && ctx->fail_alloc > 0 && --ctx->fail_alloc == 0) return -ENOMEM;  // test hook
   // kernels queued on the context's streams (main or aux, e.g. an exchange's applies reading the
   // checked id lists) may still use the old buffer: drain them before it goes (stated here rather
   // than left to hipFree's own synchronisation)
@@ -448,6 +449,12 @@ int gdsm_prof_enable(gdsm_ctx* ctx, int on) {
   ctx->prof.resolve();
   ctx->prof.clear();
   ctx->prof.on = on != 0;
+  return 0;
+}
+
+int gdsm_debug_fail_alloc(gdsm_ctx* ctx, int nth) {
+  if (!ctx || nth < 0) return -EINVAL;
+  ctx->fail_alloc = nth;
   return 0;
 }
 

@@ -59,6 +59,9 @@ struct gdsm_ctx {
   bool capture_origin = false;  // this context began the capture (only it may end it)
   std::vector<gdsm_ctx*> capture_joined;
   std::vector<hipEvent_t> capture_events;
+  // gdsm_debug_fail_alloc: the fail_alloc-th next workspace growth fails with -ENOMEM (tests of
+  // the collective refusals); 0 = off
+  mutable int fail_alloc = 0;
 };
 
 namespace gdsm {

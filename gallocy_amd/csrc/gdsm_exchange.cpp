@@ -194,6 +194,7 @@ struct LoopbackTransport final : Transport {
   int rank = 0;
   std::vector<LoopGroup::Msg> sends, recvs;
   ~LoopbackTransport() override {
+    if (!g) return;  // never joined a group
     LoopGroup::Post& me = g->post[rank];
     if (me.ready) (void)hipEventDestroy(me.ready);
     if (me.done) (void)hipEventDestroy(me.done);
@@ -379,7 +380,7 @@ int gdsm_comm_init_loopback(gdsm_comm** comms, gdsm_ctx* const* ctxs, int nranks
   if (!grp) return -ENOMEM;
   grp->nranks = nranks;
   grp->post.resize(nranks);
-  int rc = 0;
+  int rc = 0, joined = 0;  // joined: transports holding a reference to grp
   for (int r = 0; r < nranks && !rc; ++r) {
     DeviceGuard g(ctxs[r]->device);
     gdsm_comm* c = new (std::nothrow) gdsm_comm;
@@ -396,6 +397,7 @@ int gdsm_comm_init_loopback(gdsm_comm** comms, gdsm_ctx* const* ctxs, int nranks
       std::lock_guard<std::mutex> lk(grp->mu);
       ++grp->refs;
     }
+    ++joined;
     c->xp = xp;
     c->nranks = nranks;
     c->rank = r;
@@ -407,17 +409,13 @@ int gdsm_comm_init_loopback(gdsm_comm** comms, gdsm_ctx* const* ctxs, int nranks
       rc = -ENOMEM;
   }
   if (rc) {
+    // the last transport's destructor deletes grp; with none joined nobody else will
     for (int r = 0; r < nranks; ++r)
       if (comms[r]) {
         gdsm_comm_fini(comms[r]);
         comms[r] = nullptr;
       }
-    bool orphan = false;
-    {
-      std::lock_guard<std::mutex> lk(grp->mu);
-      orphan = grp->refs == 0;
-    }
-    if (orphan) delete grp;
+    if (joined == 0) delete grp;
   }
   return rc;
 }
@@ -456,7 +454,9 @@ int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* c, const gdsm_runs* send,
                   const uint32_t* const* send_ids, gdsm_runs* recv, uint32_t* const* recv_ids,
                   int target, uint32_t flags) {
   if (!ctx || !c || !send || !send_ids || !recv || !recv_ids) return -EINVAL;
-  if (target < 0 || target > 2 || !ctx->arena[target] || (flags & ~GDSM_XCHG_FIXED)) return -EINVAL;
+  if (target < 0 || target > 2 || !ctx->arena[target] ||
+      (flags & ~(GDSM_XCHG_FIXED | GDSM_XCHG_TIMED)))
+    return -EINVAL;
   if (c->device != ctx->device) return -EINVAL;
   const int G = c->nranks, me = c->rank;
   const bool fixed = flags & GDSM_XCHG_FIXED;
@@ -520,19 +520,34 @@ int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* c, const gdsm_runs* send,
 
   // ---- move: one grouped point-to-point transfer per peer pair
   {
-    gdsm::ProfScope ps(ctx->P(), GDSM_PROF_EXCHANGE, s);
-    rc = xp->group_start();
-    for (int p = 0; p < G && !rc; ++p) {
-      if (p == me) continue;
-      const uint64_t ns = send[p].n;
-      rc = xp->send(send[p].rec_off, 8 * (ns + 1), p, s);
-      if (!rc && ns) rc = xp->send(send_ids[p], 4 * ns, p, s);
-      if (!rc && sb[p]) rc = xp->send(send[p].data, sb[p], p, s);
-      if (!rc) rc = xp->recv(recv[p].rec_off, 8 * (rn[p] + 1), p, s);
-      if (!rc && rn[p]) rc = xp->recv(recv_ids[p], 4 * rn[p], p, s);
-      if (!rc && rb[p]) rc = xp->recv(recv[p].data, rb[p], p, s);
+    gdsm::Prof* P = ctx->P();
+    hipEvent_t w0 = P ? P->mark(s) : nullptr;  // this rank's streams are ready
+    if (flags & GDSM_XCHG_TIMED) {
+      // every rank's streams are ready once this one-word all-to-all completes (the exchange
+      // counters are free here: exact mode read them back above)
+      rc = xp->all_to_all_u64(c->cnt_dev, c->cnt_dev + G, 1, s);
+      if (rc) {
+        if (P) P->span(GDSM_PROF_EXCHANGE_WAIT, w0, nullptr);
+        return rc;
+      }
     }
-    const int rc2 = xp->group_end(s);
+    int rc2 = 0;
+    {
+      gdsm::ProfScope ps(P, GDSM_PROF_EXCHANGE, s);
+      rc = xp->group_start();
+      for (int p = 0; p < G && !rc; ++p) {
+        if (p == me) continue;
+        const uint64_t ns = send[p].n;
+        rc = xp->send(send[p].rec_off, 8 * (ns + 1), p, s);
+        if (!rc && ns) rc = xp->send(send_ids[p], 4 * ns, p, s);
+        if (!rc && sb[p]) rc = xp->send(send[p].data, sb[p], p, s);
+        if (!rc) rc = xp->recv(recv[p].rec_off, 8 * (rn[p] + 1), p, s);
+        if (!rc && rn[p]) rc = xp->recv(recv_ids[p], 4 * rn[p], p, s);
+        if (!rc && rb[p]) rc = xp->recv(recv[p].data, rb[p], p, s);
+      }
+      rc2 = xp->group_end(s);
+    }
+    if (P) P->span(GDSM_PROF_EXCHANGE_WAIT, w0, P->mark(s));
     if (rc || rc2) return rc ? rc : rc2;
   }
   for (int p = 0; p < G; ++p)
@@ -577,6 +592,15 @@ int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* c, const gdsm_runs* send,
 }
 
 // ---- coherence across GPUs (SPEC §5b) ----------------------------------------------------
+// Both calls are collective: once the arguments are accepted, a rank's own failure (a workspace it
+// cannot allocate, a launch error) is folded into the next agreement instead of being returned
+// alone, so no peer is left waiting in a transfer. Every workspace is grown before the agreement
+// that precedes its use.
+namespace {
+constexpr uint64_t kVerdictLocal = 4;  // some rank failed on its own (bits 0-1: the call's own)
+inline int refused(int local) { return local ? local : -ECANCELED; }
+}  // namespace
+
 int gdsm_route_events(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* events, uint64_t n,
                       uint64_t total_pages, uint64_t* batch, uint64_t cap, uint64_t* n_batch) {
   if (!ctx || !c || !n_batch || (n && !events) || (cap && !batch)) return -EINVAL;
@@ -592,9 +616,17 @@ int gdsm_route_events(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* events, uint6
   const uint64_t base = (uint64_t)me * per < total_pages ? (uint64_t)me * per : total_pages;
   uint64_t* cnt = c->rcnt_dev;  // [0,G) sent, [G,2G) received, [2G,3G+1) bounds, [4G] flag
   uint32_t* flag = reinterpret_cast<uint32_t*>(cnt + 4 * G);
-  GDSM_TRY(hipMemsetAsync(flag, 0, 8, s));
-  GDSM_TRY(gdsm::launch_route_split(events, n, total_pages, per, (uint32_t)G, cnt, cnt + 2 * G,
-                                    flag, s));
+  int local = 0;
+  {
+    hipError_t e = hipMemsetAsync(flag, 0, 8, s);
+    if (e == hipSuccess)
+      e = gdsm::launch_route_split(events, n, total_pages, per, (uint32_t)G, cnt, cnt + 2 * G,
+                                   flag, s);
+    if (e != hipSuccess) {  // send nothing; the agreement below refuses everywhere
+      local = map_err(e);
+      (void)hipMemsetAsync(cnt, 0, 8 * (4 * (size_t)G + 1), s);
+    }
+  }
   int rc = xp->all_to_all_u64(cnt, cnt + G, 1, s);
   if (rc) return rc;
   uint64_t* h = c->rcnt_host;
@@ -602,16 +634,17 @@ int gdsm_route_events(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* events, uint6
   GDSM_TRY(hipStreamSynchronize(s));
   std::vector<uint64_t> off(G + 1, 0);
   for (int p = 0; p < G; ++p) off[p + 1] = off[p] + h[G + p];
-  // every rank agrees before anything moves: 2 = some node's events are invalid, 1 = some
-  // home's batch buffer is too small
-  uint64_t verdict = ((reinterpret_cast<uint32_t*>(h + 4 * G)[0] & 1u) ? 2u : 0u) |
-                     (off[G] > cap ? 1u : 0u);
+  const bool fits = off[G] <= cap;
+  if (!local && fits) local = ensure(ctx, &c->route_buf, &c->route_bytes, 8 * (off[G] ? off[G] : 1));
+  // every rank agrees before anything moves: 4 = some rank failed, 2 = some node's events are
+  // invalid, 1 = some home's batch buffer is too small
+  uint64_t verdict = (local ? kVerdictLocal : 0u) |
+                     ((reinterpret_cast<uint32_t*>(h + 4 * G)[0] & 1u) ? 2u : 0u) | (fits ? 0u : 1u);
   rc = xp->agree_max(&verdict, s);
   if (rc) return rc;
+  if (verdict & kVerdictLocal) return refused(local);
   if (verdict & 2) return -EINVAL;
   if (verdict & 1) return -ENOSPC;
-  rc = ensure(ctx, &c->route_buf, &c->route_bytes, 8 * (off[G] ? off[G] : 1));
-  if (rc) return rc;
   uint64_t* runs = reinterpret_cast<uint64_t*>(c->route_buf);
   {
     gdsm::ProfScope ps(ctx->P(), GDSM_PROF_ROUTE, s);
@@ -645,55 +678,83 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
   if (g.rc) return g.rc;
   hipStream_t s = ctx->stream;
   const uint64_t nb = gdsm::notice_blocks(n);
-  int rc = ensure(ctx, &c->pre, &c->pre_bytes, 4 * (n ? n : 1));
-  if (!rc) rc = ensure(ctx, &c->blk, &c->blk_bytes, 4 * GDSM_MAX_NODES * (nb ? nb : 1));
-  if (!rc) rc = ensure(ctx, &c->blk_off, &c->blk_off_bytes, 8 * GDSM_MAX_NODES * (nb ? nb : 1));
-  if (rc) return rc;
-  uint32_t* pre = reinterpret_cast<uint32_t*>(c->pre);
+  uint32_t* pre = nullptr;
   uint64_t* cnt = c->rcnt_dev;  // [0,G) notices per node, [G,2G) received, [2G,3G) bases
   uint64_t* h = c->rcnt_host;
+  // every workspace of the call, the fold's included, before the first agreement
+  int local = ensure(ctx, &c->pre, &c->pre_bytes, 4 * (n ? n : 1));
+  if (!local) local = ensure(ctx, &c->blk, &c->blk_bytes, 4 * GDSM_MAX_NODES * (nb ? nb : 1));
+  if (!local)
+    local = ensure(ctx, &c->blk_off, &c->blk_off_bytes, 8 * GDSM_MAX_NODES * (nb ? nb : 1));
+  if (!local) local = ensure(ctx, &ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n));
+  pre = reinterpret_cast<uint32_t*>(c->pre);
   // capacity first, before the page table changes: a node gets at most one notice per page that
   // any home's batch touches, so every node needs cap >= the sum of the homes' distinct pages
-  GDSM_TRY(gdsm::launch_notice_pre(ctx->coh_pt, ctx->n_pages, batch, n, pre, cnt + 4 * G, s));
+  if (!local) {
+    const hipError_t e = gdsm::launch_notice_pre(ctx->coh_pt, ctx->n_pages, batch, n, pre,
+                                                 cnt + 4 * G, s);
+    if (e != hipSuccess) local = map_err(e);
+  }
   GDSM_TRY(hipMemcpyAsync(h + 4 * G, cnt + 4 * G, 8, hipMemcpyDeviceToHost, s));
+  GDSM_TRY(hipMemcpyAsync(h + 4 * G + 1, ctx->err, 4, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipStreamSynchronize(s));
-  for (int p = 0; p < G; ++p) h[p] = h[4 * G];
+  const uint64_t distinct = local ? 0 : h[4 * G];
+  // an error bit an earlier batch left (kept for gdsm_sync, restored below): only this fold's
+  // rejection may refuse the call
+  const uint32_t stale = reinterpret_cast<uint32_t*>(h + 4 * G + 1)[0] & gdsm::detail::kErrEvents;
+  if (stale) {
+    reinterpret_cast<uint32_t*>(h + 4 * G + 1)[0] &= ~stale;
+    GDSM_TRY(hipMemcpyAsync(ctx->err, h + 4 * G + 1, 4, hipMemcpyHostToDevice, s));
+  }
+  for (int p = 0; p < G; ++p) h[p] = distinct;
   GDSM_TRY(hipMemcpyAsync(cnt, h, 8 * (size_t)G, hipMemcpyHostToDevice, s));
-  rc = xp->all_to_all_u64(cnt, cnt + G, 1, s);
+  int rc = xp->all_to_all_u64(cnt, cnt + G, 1, s);
   if (rc) return rc;
   GDSM_TRY(hipMemcpyAsync(h + G, cnt + G, 8 * (size_t)G, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipStreamSynchronize(s));
   uint64_t bound = 0;
   for (int p = 0; p < G; ++p) bound += h[G + p];
-  uint64_t small = bound > cap ? 1u : 0u;
-  rc = xp->agree_max(&small, s);
+  // this home sends at most one notice per (distinct page of its batch, node)
+  if (!local) local = ensure(ctx, &c->staging, &c->staging_bytes, 8 * G * (distinct ? distinct : 1));
+  uint64_t verdict = (local ? kVerdictLocal : 0u) | (bound > cap ? 1u : 0u);
+  rc = xp->agree_max(&verdict, s);
   if (rc) return rc;
-  if (small) return -ENOSPC;
-  rc = gdsm_coherence_batch_async(ctx, batch, n, totals_dev);
-  if (rc) return rc;
+  if (verdict & kVerdictLocal) return refused(local);
+  if (verdict & 1) return -ENOSPC;
+  // from here a failure leaves the page tables unspecified (as a rejected batch does)
+  local = gdsm_coherence_batch_async(ctx, batch, n, totals_dev);
   uint32_t* blk = reinterpret_cast<uint32_t*>(c->blk);
   uint64_t* blk_off = reinterpret_cast<uint64_t*>(c->blk_off);
-  GDSM_TRY(gdsm::launch_notice_count(ctx->coh_pt, ctx->n_pages, batch, n, pre, (uint32_t)G, blk,
-                                     blk_off, cnt, cnt + 2 * G, s));
+  if (!local) {
+    const hipError_t e = gdsm::launch_notice_count(ctx->coh_pt, ctx->n_pages, batch, n, pre,
+                                                   (uint32_t)G, blk, blk_off, cnt, cnt + 2 * G, s);
+    if (e != hipSuccess) local = map_err(e);
+  }
+  if (local) GDSM_TRY(hipMemsetAsync(cnt, 0, 8 * 3 * (size_t)G, s));
   rc = xp->all_to_all_u64(cnt, cnt + G, 1, s);
   if (rc) return rc;
   GDSM_TRY(hipMemcpyAsync(h, cnt, 8 * 3 * (size_t)G, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipMemcpyAsync(h + 4 * G, ctx->err, 4, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipStreamSynchronize(s));
+  const uint32_t err_now = reinterpret_cast<uint32_t*>(h + 4 * G)[0];
+  if (stale) {  // the earlier batch's bit goes back for gdsm_sync to report
+    reinterpret_cast<uint32_t*>(h + 4 * G + 1)[0] = err_now | stale;
+    GDSM_TRY(hipMemcpyAsync(ctx->err, h + 4 * G + 1, 4, hipMemcpyHostToDevice, s));
+    GDSM_TRY(hipStreamSynchronize(s));
+  }
   std::vector<uint64_t> off(G + 1, 0);
   uint64_t sent = 0;
   for (int p = 0; p < G; ++p) {
     off[p + 1] = off[p] + h[G + p];
     sent += h[p];
   }
-  // some home's batch was rejected by the fold (its page table is unspecified): all refuse
-  uint64_t verdict = (reinterpret_cast<uint32_t*>(h + 4 * G)[0] & gdsm::detail::kErrEvents) ||
-                     off[G] > cap;  // (cannot exceed the bound checked above)
+  // some home's batch was rejected by this fold (its page table is unspecified): all refuse
+  verdict = (local ? kVerdictLocal : 0u) | ((err_now & gdsm::detail::kErrEvents) ? 1u : 0u) |
+            (off[G] > cap || sent > 8 * G * (distinct ? distinct : 1) ? 1u : 0u);
   rc = xp->agree_max(&verdict, s);
   if (rc) return rc;
+  if (verdict & kVerdictLocal) return refused(local);
   if (verdict) return -EINVAL;
-  rc = ensure(ctx, &c->staging, &c->staging_bytes, 8 * (sent ? sent : 1));
-  if (rc) return rc;
   uint64_t* stg = reinterpret_cast<uint64_t*>(c->staging);
   GDSM_TRY(gdsm::launch_notice_emit(ctx->coh_pt, ctx->n_pages, batch, n, pre, (uint32_t)G, base,
                                     blk_off, cnt + 2 * G, stg, s));

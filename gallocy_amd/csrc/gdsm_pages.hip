@@ -975,10 +975,13 @@ __device__ __forceinline__ uint32_t flat_window(uint8_t* __restrict__ target,
   const uint64_t o0 = __shfl(my_off, (int)r, 64);
   const uint64_t o1n = __shfl(my_off, (int)min(r + 1, 63u), 64);
   const uint64_t o1 = (j + lane + 1 == k) ? stop : o1n;
-  const uint32_t rs = inrec ? (uint32_t)(o0 - start) : 0u;
-  const uint32_t size = inrec ? (uint32_t)(o1 - o0) : 0u;
+  // offsets out of order (an unchecked caller stream) can put a record of the window outside
+  // [start, stop): it is malformed and writes nothing (its bytes are not in the window)
+  const bool outside = inrec && (o0 < start || o1 < o0 || o1 > stop);
+  const uint32_t rs = inrec && !outside ? (uint32_t)(o0 - start) : 0u;
+  const uint32_t size = inrec && !outside ? (uint32_t)(o1 - o0) : 0u;
   uint32_t nr = size ? win[rs / 4] : 0u;
-  bool rbad = size && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr);
+  bool rbad = outside || (size && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr));
   if (rbad) nr = 0;
   if (nr) {  // the record's run headers, lane-serially: sorted, inside the page, sizes add up
     // (four independent LDS reads per step, not one dependent read per header)
@@ -1249,8 +1252,10 @@ constexpr uint32_t kDiffSpill = 24576;
 constexpr uint32_t kDense64 = 112, kDense16 = 480;
 static inline uint64_t up256(uint64_t v) { return (v + 255) & ~255ull; }
 // Sized for the smallest spill unit (16 pages), plus the partial units of up to kMaxSplit output
-// streams (launch_diff_split: each stream's last unit may be partial): two more workgroups.
+// streams (launch_diff_split: each stream's last unit may be partial): two more workgroups. None
+// for short lists, which take the 2-page geometry, unless a spill geometry is forced (gdsm_tune).
 static uint64_t spill_pool_bytes(uint64_t n) {
+  if (n <= kDiffShort && diff_variant() < 5) return 0;
   const uint64_t wgs = ((n + 15) / 16 + 3) / 4 + 2;
   return (uint64_t)(wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill;
 }

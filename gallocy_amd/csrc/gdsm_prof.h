@@ -42,6 +42,20 @@ struct Prof {
     }
     open_stage = -1;
   }
+  // An event recorded on s now (nullptr when off); span() pairs two of them into a stage.
+  hipEvent_t mark(hipStream_t s) {
+    if (!on) return nullptr;
+    hipEvent_t e = take();
+    if (e) (void)hipEventRecord(e, s);
+    return e;
+  }
+  void span(int stage, hipEvent_t a, hipEvent_t b) {
+    if (a && b) pending.push_back({stage, a, b});
+    else {
+      if (a) pool.push_back(a);
+      if (b) pool.push_back(b);
+    }
+  }
   // Caller synchronised the stream.
   void resolve() {
     for (auto& m : pending) {

@@ -26,6 +26,7 @@ from . import gdsm
 from ._lib import GdsmRuns, check
 
 XCHG_FIXED = 1
+XCHG_TIMED = 2  # a device barrier before each transfer: the exchange stage times the link alone
 
 
 def dest_bounds(rank: int, world: int, n: int) -> list[int]:
@@ -126,6 +127,12 @@ class Comm:
         cs = (C.c_void_p * G)(*[c.handle for c in ctxs])
         check(gdsm.lib().gdsm_comm_init_loopback(hs, cs, G), "gdsm_comm_init_loopback")
         return [cls(ctxs[r], r, G, handle=hs[r]) for r in range(G)]
+
+    def size(self) -> tuple[int, int]:
+        """gdsm_comm_size: (ranks, this rank) as the communicator itself reports them."""
+        nr, me = C.c_int(0), C.c_int(-1)
+        check(gdsm.lib().gdsm_comm_size(self.handle, C.byref(nr), C.byref(me)), "gdsm_comm_size")
+        return nr.value, me.value
 
     def agree(self, ctx: gdsm.Context, value: int) -> int:
         """gdsm_comm_agree: the maximum of every rank's value (collective, synchronous)."""

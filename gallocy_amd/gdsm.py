@@ -220,7 +220,7 @@ class Context:
         return Graph(g.value)
 
     PROF_STAGES = ("diff", "apply", "twin", "coh_fold", "coh_reduce", "nw_fill", "nw_trace",
-                   "exchange", "route")
+                   "exchange", "route", "exchange_wait")
 
     def prof_enable(self, on: bool = True):
         check(lib().gdsm_prof_enable(self.handle, int(on)), "gdsm_prof_enable")

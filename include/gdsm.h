@@ -69,6 +69,7 @@ enum gdsm_prof_stage {
   GDSM_PROF_NW_TRACE,   /* GPU diff(): traceback + alignment strings */
   GDSM_PROF_EXCHANGE,   /* gdsm_exchange: the transfer of the record streams (RCCL group) */
   GDSM_PROF_ROUTE,      /* gdsm_route_events / gdsm_coherence_notify: the transfers */
+  GDSM_PROF_EXCHANGE_WAIT, /* gdsm_exchange: the transfer plus the wait for the peers' streams */
   GDSM_PROF_STAGES
 };
 
@@ -334,6 +335,12 @@ enum gdsm_exchange_flags {
    * one host read, and agrees on capacity with every rank (all return -ENOSPC when any stream
    * is too small). */
   GDSM_XCHG_FIXED = 1u << 0,
+  /* Measurement: before the transfer, a device-side barrier (a one-word all-to-all on the
+   * exchange stream), so the transfer starts once every rank's streams are ready. With profiling
+   * on, GDSM_PROF_EXCHANGE then times the RCCL group alone (the link) and
+   * GDSM_PROF_EXCHANGE_WAIT the group plus the wait for the peers; without the flag both time the
+   * group from when this rank's own streams are ready. */
+  GDSM_XCHG_TIMED = 1u << 1,
 };
 /* Collective: every rank of `comm` calls it with arrays of nranks entries.
  *   send[d], send_ids[d]: this rank's stream for home rank d and, per record, the page's index
@@ -373,7 +380,9 @@ int gdsm_exchange(gdsm_ctx* ctx, gdsm_comm* comm, const gdsm_runs* send,
  * rank's home block, from every node, merged by (page, seq) and packed as SPEC §5 events with the
  * LOCAL page, are being written to `batch` (device, cap entries) on ctx's stream. All ranks return
  * -EINVAL if any node's list is unsorted or names a page >= total_pages or a node >= nranks, and
- * -ENOSPC if any home's cap is too small; nothing moves then. */
+ * -ENOSPC if any home's cap is too small; nothing moves then. A rank whose own step fails after
+ * the arguments were accepted (a workspace it cannot allocate, a launch error) returns that error
+ * and every other rank -ECANCELED, together; nothing moves either. */
 int gdsm_route_events(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* events, uint64_t n,
                       uint64_t total_pages, uint64_t* batch, uint64_t cap, uint64_t* n_batch);
 /* Home side: folds `batch` (n events, local pages, e.g. from gdsm_route_events) into ctx's page
@@ -388,7 +397,11 @@ int gdsm_route_events(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* events, ui
  * node never gets more notices than there are distinct pages in all homes' batches: every rank
  * returns -ENOSPC, before any page table changes, when some node's cap is below that count. All
  * ranks return -EINVAL if any home's batch was rejected by the fold (that page table is then
- * unspecified, as after a rejected gdsm_coherence_batch). */
+ * unspecified, as after a rejected gdsm_coherence_batch). A rank whose own step fails (a workspace
+ * it cannot allocate, a launch error) returns that error and every other rank -ECANCELED,
+ * together: before the fold (every workspace is sized then) no page table changes; a launch
+ * failure of the fold itself leaves the page tables unspecified, as above. Only this fold's
+ * rejection counts: an error bit an earlier unsynchronised batch left is kept for gdsm_sync. */
 int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* batch, uint64_t n,
                           uint64_t base, uint64_t* totals_dev, uint64_t* notices, uint64_t cap,
                           uint64_t* n_notices);
@@ -396,6 +409,9 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* batch,
 const char* gdsm_version(void);
 /* Process-wide kernel-variant knobs for measurement, e.g. ("diff_variant", 0..4). */
 int gdsm_tune(const char* key, int64_t value);
+/* Test hook: the nth next growth of one of ctx's internal workspaces fails with -ENOMEM (0 = off).
+ * Used to show that a collective call refuses on every rank together when one rank fails. */
+int gdsm_debug_fail_alloc(gdsm_ctx* ctx, int nth);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -27,3 +27,68 @@ def test_payload_bytes_matches_run_lengths():
             want += sum(int(h) >> 16 for h in w[a + 1:a + 1 + int(w[a])])
     assert bench.payload_bytes(ro, data) == want
     assert want == int(np.count_nonzero(twin != cur))  # runs cover exactly the changed bytes
+
+
+def test_cpu_baseline_reports_host(monkeypatch):
+    """BASELINE.md timing rules: nproc, the CPU model and the host RAM next to CPU numbers; the
+    thread count is the process's CPU share (OMP_NUM_THREADS), with no fixed cap."""
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.cpu_threads() == min(3, len(__import__("os").sched_getaffinity(0)))
+    h = bench.host_info()
+    assert h["nproc"] >= 1 and h["host_ram_gib"] > 0 and h["host_cpu"]
+
+
+def _bench(args, env_extra):
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, str(bench.ROOT / "bench.py"), *args], env=env,
+                          capture_output=True, text=True, timeout=120)
+
+
+def test_gpus_mismatch_with_launcher_exits_nonzero():
+    """Under a launcher (WORLD_SIZE set) --gpus must equal the rank count: a mismatch exits
+    non-zero before anything touches a GPU, instead of printing a line for the wrong N."""
+    r = _bench(["--gpus", "1", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and "--gpus 1" in r.stderr and "WORLD_SIZE" in r.stderr
+    r = _bench(["--gpus", "8", "--steps", "1"], {"WORLD_SIZE": "4", "RANK": "0"})
+    assert r.returncode != 0
+    r = _bench(["--gpus", "0"], {})
+    assert r.returncode != 0
+
+
+def test_gpus_n_without_launcher_spawns_n_ranks(monkeypatch):
+    """`bench.py --gpus N` with no launcher: the parent (no GPU call) starts torch.distributed.run
+    with N processes on 127.0.0.1 and returns their exit code; --gpus 1 runs in-process."""
+    import argparse
+    import subprocess
+    calls = []
+
+    class R:
+        returncode = 7
+
+    def fake_run(cmd, env=None, **kw):
+        calls.append((cmd, env))
+        return R()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(bench.sys, "argv", ["bench.py", "--gpus", "4", "--steps", "2"])
+    assert bench.launch_ranks(argparse.Namespace(gpus=4)) == 7
+    cmd, env = calls[0]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"] and cmd[-5].endswith("bench.py")
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert bench.launch_ranks(argparse.Namespace(gpus=1)) is None
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.launch_ranks(argparse.Namespace(gpus=4)) is None  # already a rank
+
+
+def test_mmult_cpu_baseline_replays_the_trace():
+    """Config 5's CPU baseline: the test_mmult trace through the C oracle round by round; the
+    home copies equal the product zone afterwards."""
+    out = bench.mmult_cpu_baseline(96, 3, 7)
+    assert out["home_copy_equals_product"] is True
+    assert out["value"] > 0 and out["unit"] == "rounds/s" and out["kind"] == "port"

@@ -97,17 +97,25 @@ def test_workspace_sizing():
     look-back granule per 16 pages, then the spill pool sized for the smallest spill geometry
     (16 pages per wave, plus two workgroups for the partial units of split streams: a
     generation word per workgroup slot, up to 1280 workgroup slots of 4 x 24 KiB); non-decreasing
-    in n."""
+    in n. Short lists (<= 32768 pages, the 2-page geometry) get no spill pool unless a spill
+    geometry is forced (gdsm_tune "diff_variant" 5-7)."""
     from gallocy_amd import _lib
     lib = _lib.load()
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
     slots = lambda n: min(1280, ((n + 15) // 16 + 3) // 4 + 2)  # noqa: E731
-    for n in (1, 1000, 1 << 20, 1 << 24):
-        want = up(8 * (1 + max((n + 15) // 16, (min(n, 32768) + 1) // 2)) + 64) + up(4 * 1280) \
-            + slots(n) * 4 * 24576
-        assert lib.gdsm_diff_workspace_bytes(n) == want, n
-    sizes = [lib.gdsm_diff_workspace_bytes(n) for n in range(1, 200000, 997)]
-    assert sizes == sorted(sizes)
+    for forced in (0, 7):
+        assert lib.gdsm_tune(b"diff_variant", forced) == 0
+        try:
+            for n in (1, 1000, 32768, 32769, 1 << 20, 1 << 24):
+                pool = slots(n) * 4 * 24576 if (n > 32768 or forced) else 0
+                want = up(8 * (1 + max((n + 15) // 16, (min(n, 32768) + 1) // 2)) + 64) \
+                    + up(4 * 1280) + pool
+                assert lib.gdsm_diff_workspace_bytes(n) == want, (n, forced)
+            sizes = [lib.gdsm_diff_workspace_bytes(n) for n in range(1, 200000, 997)]
+            assert sizes == sorted(sizes)
+        finally:
+            lib.gdsm_tune(b"diff_variant", 0)
+    assert lib.gdsm_diff_workspace_bytes(32768) < 1 << 20  # was ~50 MB with the pool
 
 
 CALLER = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "legacy_caller"

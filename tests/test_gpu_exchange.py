@@ -111,3 +111,39 @@ def test_bench_multi_rank_rehearsal_gloo(ranks, overlap):
     assert d["exchange"]["received_bytes_per_step"] > 0
     assert d["pipelined"] is (overlap == "on")
     assert d["scaling"] == "strong" and d["config"]["total_pages"] == ranks * ranks * 8192
+
+
+def _bench_no_launcher(args, backend="gloo"):
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["GDSM_BENCH_BACKEND"] = backend
+    r = subprocess.run([sys.executable, str(root / "bench.py"), *args], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    return json.loads(line[0])
+
+
+def test_bench_gpus_2_without_launcher():
+    """`bench.py --gpus 2` with no launcher (how a user or the driver may call it): the GPU-free
+    parent spawns the two ranks itself, and rank 0's line reports n_gpus 2 (ranks share cuda:0
+    over the gloo rehearsal transport here; RCCL on a multi-GPU node)."""
+    d = _bench_no_launcher(["--gpus", "2", "--steps", "2", "--warmup", "1", "--total-pages",
+                            str(4 * 8192), "--no-cpu"])
+    assert d["n_gpus"] == 2 and d["replica_equals_current"] is True
+    assert d["config"]["total_pages"] == 4 * 8192 and d["config"]["pages_per_gpu"] == 2 * 8192
+
+
+def test_bench_coherence_sharded_gpus_2_without_launcher():
+    """The coherence workload at N = 2: the page table sharded by home, each rank folding its own
+    pages' batch; one line with n_gpus 2 and the events of both shards."""
+    d = _bench_no_launcher(["--gpus", "2", "--workload", "coherence", "--coh-pages",
+                            str(1 << 20), "--events", str(1 << 22), "--steps", "2", "--warmup",
+                            "1", "--no-cpu"])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["value"] > 0 and "sharded over 2 GPUs" in d["config"]["workload"]

@@ -87,3 +87,22 @@ def test_capture_refuses_workspace_growth_and_host_sync():
         with pytest.raises(GdsmError) as ei:
             c.capture_end()
         assert ei.value.errno == errno.EINVAL
+
+
+def test_capture_end_on_joined_context_is_refused():
+    """Only the context that began a capture may end it: gdsm_capture_end on a context that was
+    joined into another's capture returns -EINVAL and leaves the recording open, which the
+    originating context then ends (round-2 advice, gdsm_capi.cpp capture_origin)."""
+    import ctypes as C
+    L = ga.gdsm.lib()
+    with ga.Context(64) as a, ga.Context(64) as b:
+        a.sync()
+        b.sync()
+        a.capture_begin(b)
+        g = C.c_void_p()
+        assert L.gdsm_capture_end(b.handle, C.byref(g)) == -errno.EINVAL
+        assert not g.value
+        a.capture_end().destroy()
+        # both contexts work eagerly again
+        a.sync()
+        b.sync()

@@ -70,7 +70,7 @@ def homes_equal_writers(ctxs, n):
                for d, ctx in enumerate(ctxs))
 
 
-@pytest.mark.parametrize("G", [2, 3, 4])
+@pytest.mark.parametrize("G", [2, 3, 4, 8])
 def test_loopback_shard_exact_then_fixed(G):
     """Release 0 with exact sizes (all-to-all of sizes, agreement, grouped moves), calibrate(),
     then pipelined fixed-budget releases with no host synchronisation: every home REPLICA equals
@@ -99,12 +99,13 @@ def test_loopback_shard_exact_then_fixed(G):
         close_group(ctxs, comms)
 
 
-def test_loopback_over_budget_is_rejected_then_recovered():
+@pytest.mark.parametrize("G", [3, 8])
+def test_loopback_over_budget_is_rejected_then_recovered(G):
     """After calibrate(), rank 0 writes 4x as many words: its fixed-budget streams (n/G > 256
     records each) no longer fit their budgets. The homes reject them whole (nothing of rank 0's
     release applied, -EOVERFLOW on the homes and on rank 0), drain() has every rank agree and redo
     the release with exact sizes, and every home ends equal to the writers' CURRENT."""
-    G, n = 3, 3 * 4096
+    n = G * 4096
     ctxs, comms = make_group(G, n)
     shards = [exchange.Shard(ctxs[r], r, G, n, 1024, transport="loopback", comm=comms[r])
               for r in range(G)]
@@ -288,3 +289,78 @@ def test_loopback_agree():
         assert got == [15, 15]
     finally:
         close_group(ctxs, comms)
+
+
+@pytest.mark.parametrize("G", [4, 8])
+def test_loopback_bench_step_pipelined_timed(G):
+    """bench.py's N > 1 step at the production group size, reduced total: every rank diffs its
+    pages into one stream per home (one gdsm_diff_split launch), release 0 exact, calibrate(),
+    then pipelined fixed-budget releases with profiling on, then the same releases with
+    GDSM_XCHG_TIMED (the device barrier before each transfer that bench.py uses to time the link
+    alone): both runs record the exchange and exchange_wait stages, nothing recovers, and every
+    home REPLICA equals its pages' CURRENT (checked on the device by Shard.verify and on the host)."""
+    n = 8192 * G // 4 * 4
+    ctxs, comms = make_group(G, n)
+    shards = [exchange.Shard(ctxs[r], r, G, n, 128, transport="loopback", comm=comms[r])
+              for r in range(G)]
+    profs = [None] * G
+    try:
+        def rank(r):
+            s = shards[r]
+            s.run(1, pipelined=False)
+            s.drain()
+            s.calibrate()
+            s.run(2, pipelined=True)
+            s.drain()
+            out = []
+            for timed in (False, True):
+                if timed:
+                    s.flags |= exchange.XCHG_TIMED
+                ctxs[r].prof_enable(True)
+                s.run(3, pipelined=True)
+                s.drain()
+                out.append(ctxs[r].prof_read())
+                s.flags &= ~exchange.XCHG_TIMED
+            assert s.recoveries == 0
+            profs[r] = out
+        run_ranks(G, rank)
+        for r in range(G):
+            for p in profs[r]:
+                assert p["diff"][1] == 3 and p["exchange"][1] == 3 and p["exchange_wait"][1] == 3
+                # the wait-inclusive span contains the transfer
+                assert p["exchange_wait"][0] >= p["exchange"][0] * 0.999
+        assert all(shards[r].verify(SEED, ga.GEN_UNIFORM, 10000) for r in range(G))
+        assert homes_equal_writers(ctxs, n)
+    finally:
+        for s in shards:
+            s.close()
+        close_group(ctxs, comms)
+
+
+def test_exchange_rejects_unknown_flags():
+    G, n = 2, 1024
+    ctxs, comms = make_group(G, n)
+    try:
+        runs = [ga.Runs(ctxs[0], 1, cap=16) for _ in range(G)]
+        rids = [None] * G
+        assert _exchange(ctxs[0], comms[0], runs, [0] * G, runs, rids, flags=4) == -errno.EINVAL
+    finally:
+        close_group(ctxs, comms)
+
+
+def test_loopback_init_failure_frees_the_group():
+    """gdsm_comm_init_loopback with a NULL context among valid ones: -EINVAL, nothing leaked or
+    double-freed (the group is deleted by whoever holds the last reference)."""
+    lib = ga.gdsm.lib()
+    ctx = ga.Context(64)
+    try:
+        hs = (C.c_void_p * 3)()
+        cs = (C.c_void_p * 3)(ctx.handle, None, ctx.handle)
+        assert lib.gdsm_comm_init_loopback(hs, cs, 3) == -errno.EINVAL
+        assert all(h is None for h in hs)
+        for _ in range(3):  # repeated builds and teardowns of a valid group
+            comms = exchange.Comm.loopback([ctx])
+            for c in comms:
+                c.close()
+    finally:
+        ctx.close()

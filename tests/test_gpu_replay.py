@@ -69,7 +69,7 @@ def test_rank_replay_single_rank_rccl():
         R.close()
 
 
-@pytest.mark.parametrize("ranks,ndim", [(2, 300), (3, 257), (4, 1000)])
+@pytest.mark.parametrize("ranks,ndim", [(2, 300), (3, 257), (4, 1000), (8, 1000)])
 def test_rank_replay_multi_rank_loopback(ranks, ndim):
     """MmultRankReplay with `ranks` DSM nodes as threads on cuda:0 over the loopback communicator:
     every round routes each node's own fault events to the homes (gdsm_route_events), folds them

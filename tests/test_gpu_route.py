@@ -67,7 +67,8 @@ class Shard:
                                 np.zeros(self.nh, np.uint32))
 
 
-@pytest.mark.parametrize("G,Z,n,hot", [(2, 5000, 3000, 0), (3, 4099, 20000, 500), (4, 777, 4000, 0)])
+@pytest.mark.parametrize("G,Z,n,hot", [(2, 5000, 3000, 0), (3, 4099, 20000, 500), (4, 777, 4000, 0),
+                                       (8, 9001, 3000, 300), (8, 64, 2000, 0)])
 def test_route_notify_equal_sequential_fold(G, Z, n, hot):
     rng = np.random.default_rng(G * 1000 + Z)
     shards = [Shard(r, G, Z) for r in range(G)]
@@ -167,6 +168,183 @@ def test_route_refusals_are_collective():
             st, fl = s.ctx.coh_download()
             assert np.array_equal(st, gst[s.base:s.base + s.nh])
             assert np.array_equal(fl, gfl[s.base:s.base + s.nh])
+    finally:
+        for c in comms:
+            c.close()
+        for s in shards:
+            s.ctx.close()
+
+
+def test_route_notify_8_nodes_full_copyset():
+    """The production group size, GDSM_MAX_NODES = 8 ranks: in batch 0 every node reads pages
+    0-99 (their copysets become all 8 nodes), in batch 1 every node writes some of them (a write
+    to a page all 8 share invalidates 7 copies), then a random batch. Shards, totals and every
+    node's notices equal the oracle's sequential fold."""
+    G, Z = 8, 4096
+    rng = np.random.default_rng(88)
+    shards = [Shard(r, G, Z) for r in range(G)]
+    comms = exchange.Comm.loopback([s.ctx for s in shards])
+    gst, gfl = oracle.coh_init(Z, G)
+    try:
+        def batch_of(pages_per_node, rw_of):
+            tot = sum(len(p) for p in pages_per_node)
+            clock = rng.permutation(tot).astype(np.uint64)
+            out, k = [], 0
+            for t, pages in enumerate(pages_per_node):
+                m = len(pages)
+                rw = rw_of(t, m)
+                e = (np.asarray(pages, np.uint64) << np.uint64(36)) \
+                    | (clock[k:k + m] << np.uint64(4)) | np.uint64(t << 1) | rw
+                k += m
+                out.append(np.sort(e))
+            return out
+        reads = batch_of([np.arange(100)] * G, lambda t, m: np.zeros(m, np.uint64))
+        writes = batch_of([rng.choice(100, 10, replace=False) for _ in range(G)],
+                          lambda t, m: np.ones(m, np.uint64))
+        mixed = batch_of([rng.integers(0, Z, 3000) for _ in range(G)],
+                         lambda t, m: (rng.random(m) < 0.2).astype(np.uint64))
+        for bi, stamped in enumerate((reads, writes, mixed)):
+            rc_ref, tot_ref, want = oracle.route_round(gst, gfl, stamped, G, Z)
+            assert rc_ref == 0
+            if bi == 0:
+                assert np.all(gst[:100] & 0xFF == 0xFF)  # every page shared by all 8 nodes
+            if bi == 1:
+                assert tot_ref["invalidations"] >= 7
+            got, tots = [None] * G, [None] * G
+
+            def rank(r):
+                s, c = shards[r], comms[r]
+                ev = s.ctx.buffer(max(8, 8 * len(stamped[r]))).upload(stamped[r])
+                cap = sum(len(x) for x in stamped) + 1
+                bt, nt, tot = s.ctx.buffer(8 * cap), s.ctx.buffer(8 * (Z + 1)), s.ctx.buffer(80)
+                nb = exchange.route_events(s.ctx, c, ev.ptr, len(stamped[r]), Z, bt.ptr, cap)
+                k = exchange.coherence_notify(s.ctx, c, bt.ptr, nb, s.base, tot.ptr, nt.ptr, Z + 1)
+                s.ctx.sync()
+                got[r] = nt.download(np.uint64, k) if k else np.zeros(0, np.uint64)
+                tots[r] = tot.download(np.uint64, 10).astype(np.int64)
+                for b in (ev, bt, nt, tot):
+                    b.free()
+            run_ranks(G, rank)
+            for r in range(G):
+                assert np.array_equal(got[r], want[r]), (bi, r)
+            assert np.sum(tots, axis=0).tolist() == [tot_ref["invalidations"],
+                                                     tot_ref["transfers"], *tot_ref["node_faults"]]
+        for s in shards:
+            st, fl = s.ctx.coh_download()
+            assert np.array_equal(st, gst[s.base:s.base + s.nh])
+            assert np.array_equal(fl, gfl[s.base:s.base + s.nh])
+    finally:
+        for c in comms:
+            c.close()
+        for s in shards:
+            s.ctx.close()
+
+
+def test_route_notify_local_failure_is_collective():
+    """One rank's own failure (a workspace it cannot allocate, forced by gdsm_debug_fail_alloc)
+    inside gdsm_route_events or gdsm_coherence_notify: that rank returns -ENOMEM and every other
+    rank -ECANCELED, together (no peer is left waiting in a transfer), nothing changes, and the
+    group works afterwards. notify grows five workspaces (pre-fold words, per-block counts and
+    offsets, the fold's workspace, the notice staging); a failure is forced at each in turn."""
+    import ctypes as C
+    G, Z = 3, 3000
+    rng = np.random.default_rng(6)
+    shards = [Shard(r, G, Z) for r in range(G)]
+    comms = exchange.Comm.loopback([s.ctx for s in shards])
+    lib = ga.gdsm.lib()
+    try:
+        stamped = stamped_batch(rng, G, Z, 2000)
+        cap = sum(len(x) for x in stamped) + 1
+        bufs = []
+        for r, s in enumerate(shards):
+            bufs.append((s.ctx.buffer(8 * len(stamped[r])).upload(stamped[r]),
+                         s.ctx.buffer(8 * cap), s.ctx.buffer(8 * Z), s.ctx.buffer(80)))
+        nbs = [C.c_uint64(0) for _ in range(G)]
+
+        def route_all():
+            rcs = [None] * G
+
+            def rank(r):
+                s, c = shards[r], comms[r]
+                ev, bt, _, _ = bufs[r]
+                rcs[r] = lib.gdsm_route_events(s.ctx.handle, c.handle, ev.ptr, len(stamped[r]), Z,
+                                               bt.ptr, cap, C.byref(nbs[r]))
+            run_ranks(G, rank)
+            return rcs
+
+        def notify_all():
+            rcs = [None] * G
+
+            def rank(r):
+                s, c = shards[r], comms[r]
+                _, bt, nt, tot = bufs[r]
+                nn = C.c_uint64(0)
+                rcs[r] = lib.gdsm_coherence_notify(s.ctx.handle, c.handle, bt.ptr, nbs[r].value,
+                                                   s.base, tot.ptr, nt.ptr, Z, C.byref(nn))
+                s.ctx.sync()
+            run_ranks(G, rank)
+            return rcs
+
+        assert lib.gdsm_debug_fail_alloc(shards[1].ctx.handle, 1) == 0
+        assert route_all() == [-errno.ECANCELED, -errno.ENOMEM, -errno.ECANCELED]
+        assert route_all() == [0, 0, 0]
+        init = [s.ctx.coh_download() for s in shards]
+        fails = 0
+        for _ in range(8):
+            assert lib.gdsm_debug_fail_alloc(shards[2].ctx.handle, 1) == 0
+            rcs = notify_all()
+            if rcs == [0, 0, 0]:
+                break
+            assert rcs == [-errno.ECANCELED, -errno.ECANCELED, -errno.ENOMEM], rcs
+            fails += 1
+            for s, (st0, fl0) in zip(shards, init):  # no page table changed
+                st, fl = s.ctx.coh_download()
+                assert np.array_equal(st, st0) and np.array_equal(fl, fl0)
+        assert fails == 5 and rcs == [0, 0, 0]
+        assert lib.gdsm_debug_fail_alloc(shards[2].ctx.handle, 0) == 0
+        gst, gfl = oracle.coh_init(Z, G)
+        assert oracle.route_round(gst, gfl, stamped, G, Z)[0] == 0
+        for s in shards:
+            st, fl = s.ctx.coh_download()
+            assert np.array_equal(st, gst[s.base:s.base + s.nh])
+            assert np.array_equal(fl, gfl[s.base:s.base + s.nh])
+    finally:
+        for c in comms:
+            c.close()
+        for s in shards:
+            s.ctx.close()
+
+
+def test_notify_ignores_a_stale_event_error_bit():
+    """An error bit an earlier, never-synchronised gdsm_coherence_batch_async left behind (an
+    unsorted batch) does not make the next gdsm_coherence_notify refuse: only its own fold's
+    rejection counts. The stale bit is still reported by the next gdsm_sync."""
+    G, Z = 2, 2000
+    rng = np.random.default_rng(7)
+    shards = [Shard(r, G, Z) for r in range(G)]
+    comms = exchange.Comm.loopback([s.ctx for s in shards])
+    lib = ga.gdsm.lib()
+    try:
+        # rank 0: an unsorted local batch folded asynchronously, never synchronised
+        bad = np.array([(5 << 4) | 1, (3 << 4)], np.uint64)
+        s0 = shards[0]
+        evb, tb = s0.ctx.buffer(16).upload(bad), s0.ctx.buffer(80)
+        assert lib.gdsm_coherence_batch_async(s0.ctx.handle, evb.ptr, 2, tb.ptr) == 0
+        stamped = stamped_batch(rng, G, Z, 1000)
+        got = [None] * G
+
+        def rank(r):
+            s, c = shards[r], comms[r]
+            ev = s.ctx.buffer(8 * len(stamped[r])).upload(stamped[r])
+            cap = sum(len(x) for x in stamped) + 1
+            bt, nt, tot = s.ctx.buffer(8 * cap), s.ctx.buffer(8 * (Z + 1)), s.ctx.buffer(80)
+            nb = exchange.route_events(s.ctx, c, ev.ptr, len(stamped[r]), Z, bt.ptr, cap)
+            got[r] = exchange.coherence_notify(s.ctx, c, bt.ptr, nb, s.base, tot.ptr, nt.ptr,
+                                               Z + 1)
+        run_ranks(G, rank)
+        assert all(k is not None for k in got)
+        assert lib.gdsm_sync(s0.ctx.handle) == -errno.EINVAL  # the earlier batch's error
+        assert lib.gdsm_sync(shards[1].ctx.handle) == 0
     finally:
         for c in comms:
             c.close()
