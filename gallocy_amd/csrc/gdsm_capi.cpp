@@ -194,7 +194,13 @@ int gdsm_init(gdsm_ctx** out, int device, uint64_t n_pages, uint32_t flags) {
       rc = -ENOMEM;
       break;
     }
-    (void)hipMemset(ctx->err, 0, 256);
+    // on the context's own stream: a non-blocking stream does not wait for the null stream,
+    // so a hipMemset there could land after the first read of the word (a recycled allocation
+    // still holding an earlier context's error bits)
+    if (hipMemsetAsync(ctx->err, 0, 256, ctx->stream) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
     for (int a = 0; a < 3 && !rc; ++a) {
       if (!(flags & (1u << a)) || n_pages == 0) continue;
       // + one guard page (index n_pages): where a checked id list sends out-of-range ids
@@ -1054,8 +1060,9 @@ int nw_host(gdsm_ctx* ctx, const char* m1, size_t n1, const char* m2, size_t n2,
   const uint32_t max_len = (uint32_t)(n1 > n2 ? n1 : n2);
   rc = gdsm_nw_diff_batch(ctx, da, offs, db, offs + 2, 1, max_len, d1, d2, dlen);
   if (rc) return rc;
-  uint64_t L = 0;
-  GDSM_TRY(hipMemcpy(&L, dlen, 8, hipMemcpyDeviceToHost));
+  uint64_t L = 0;  // on the context's stream: the null stream does not wait for a non-blocking one
+  GDSM_TRY(hipMemcpyAsync(&L, dlen, 8, hipMemcpyDeviceToHost, ctx->stream));
+  GDSM_TRY(hipStreamSynchronize(ctx->stream));
   char* a1 = static_cast<char*>(alloc(L + 1));
   char* a2 = static_cast<char*>(alloc(L + 1));
   if (!a1 || !a2) {
@@ -1063,8 +1070,9 @@ int nw_host(gdsm_ctx* ctx, const char* m1, size_t n1, const char* m2, size_t n2,
     if (a2) release(a2);
     return -ENOMEM;
   }
-  hipError_t e = hipMemcpy(a1, d1, L + 1, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipMemcpy(a2, d2, L + 1, hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpyAsync(a1, d1, L + 1, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(a2, d2, L + 1, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     release(a1);
     release(a2);

@@ -675,6 +675,385 @@ __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt
                                      n_nodes, tr_all[threadIdx.x >> 6]);
 }
 
+// ---------------------------------------------------------------- S: streaming fold
+// One wave = one span of kSpan = 4096 events, walked as 64 chunks of 64 CONSECUTIVE events (lane
+// l = event 64c + l of the span), with no LDS copy: the chunk's events come straight from a
+// coalesced 8-B load issued kSD chunks ahead, and the page-table words of the chunk's heads from
+// a gather issued kSG chunks ahead, so a wave never stops to load a block.
+//
+// Inside a chunk the fold is a segmented OR scan over the lanes (DPP): a lane's scan value is
+// (F | base word) for a CONST event (a write, or a head: its page-table word, then the head's own
+// read), or its reader bit in the R field for a read; a lane with F keeps its value, others OR in
+// what precedes them. The exclusive value is the state the event meets: base word + the readers
+// since it (s_state applies them: copyset |= R, EXCLUSIVE -> SHARED when R leaves the copyset).
+// The last lane's inclusive value carries to the next chunk.
+//
+// The span's first segment (opened in an earlier span) starts from PROBE (no F, empty base): its
+// reads before the first write (P8, the prefix) count one fault per node and its first write is
+// left out; both are corrected after the decoupled look-back has given the incoming state, which
+// is also when that segment's state word is stored (the low dword; its fault count is added to
+// the high dword atomically, as is the count of a segment that continues past the span). A
+// segment that starts and ends inside the span is stored whole (state | old count + faults).
+// Status granules, tickets and ordering are the fold's (F above): a wave publishes after its
+// loads landed; a wave that stores the state of a segment opened before it looks back to a span
+// that holds a head.
+constexpr uint32_t kSC = 64;              // chunks per span
+constexpr uint32_t kSpan = 64 * kSC;      // events per span
+constexpr uint32_t kSD = 6;               // event loads in flight (chunks ahead)
+constexpr uint32_t kSG = 3;               // head-word gathers in flight (chunks ahead)
+static_assert(kSD % kSG == 0 && kSG < kSD, "ring geometry");
+constexpr uint32_t kSF = 1u << 31;        // scan value: a CONST at or before this lane
+constexpr uint32_t kSProbe = 1u << 28;    // scan value: the span's incoming state (unknown)
+
+// state word (bits 0-18) of base word `base` after the readers R since it
+__device__ __forceinline__ uint32_t s_state(uint32_t v) {
+  const uint32_t base = v & 0x7FFFFu, R = (v >> 20) & 0xFFu;
+  const bool flip = ((base >> 16) & 3u) == 2u && (R & ~base & 0xFFu);
+  return (base | R) ^ (flip ? 0x30000u : 0u);
+}
+
+// Segmented OR scan (inclusive) over the 64 lanes: a lane with kSF keeps its value.
+__device__ __forceinline__ uint32_t sor_scan(uint32_t v) {
+#define GDSM_SOR(ctrl, rm)                                                  \
+  do {                                                                      \
+    const uint32_t t_ = dpp0<ctrl, rm>(v);                                  \
+    v = v | (t_ & ~(uint32_t)((int32_t)v >> 31));                           \
+  } while (0)
+  GDSM_SOR(0x111, 0xF);
+  GDSM_SOR(0x112, 0xF);
+  GDSM_SOR(0x114, 0xF);
+  GDSM_SOR(0x118, 0xF);
+  GDSM_SOR(0x142, 0xA);
+  GDSM_SOR(0x143, 0xC);
+#undef GDSM_SOR
+  return v;
+}
+
+__device__ __forceinline__ uint64_t le_mask(uint32_t lane) {  // lanes 0..lane
+  return lane == 63 ? ~0ull : (2ull << lane) - 1ull;
+}
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+
+template <bool kFull>
+__device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
+                                                const uint64_t* __restrict__ ev, uint64_t n,
+                                                uint64_t b, uint64_t* __restrict__ status,
+                                                uint32_t* __restrict__ partial,
+                                                uint32_t* __restrict__ err, uint32_t n_nodes) {
+  const uint32_t lane = lane_id();
+  const uint64_t lo = b * kSpan;
+  const uint64_t hi = lo + kSpan;
+  const uint32_t nev = kFull ? kSpan : (uint32_t)min((uint64_t)kSpan, n - lo);
+  const uint32_t nch = kFull ? kSC : (nev + 63u) / 64u;
+  const uint64_t lem = le_mask(lane);
+  // the event before the span and the one after it (uniform scalar loads)
+  const uint32_t xprev = lo > 0 ? (uint32_t)ev[lo - 1] : 0u;
+  const bool has_next = hi < n;
+  const uint32_t xnext = has_next ? (uint32_t)ev[hi] : 0u;
+
+  uint64_t X[kSD];       // events of chunks c .. c + kSD - 1 (ring)
+  uint64_t Wg[kSG];      // page-table words of the heads of chunks c .. c + kSG - 1 (ring)
+  uint64_t Hg[kSG];      // their head masks
+#define GDSM_SLOAD(c_, slot_)                                                        \
+  do {                                                                               \
+    const uint64_t g_ = lo + 64ull * (c_) + lane;                                    \
+    X[slot_] = ((c_) < nch && (kFull || g_ < n)) ? __builtin_nontemporal_load(ev + g_) \
+                                                 : ~0ull;                            \
+  } while (0)
+  uint32_t bad = 0, pprev = xprev >> 4;  // page of the event before chunk (gathers' view)
+  const bool batch_first = lo == 0;
+  // heads of chunk c (events in X[slot]) and their words; pprev = page of the event before it
+#define GDSM_SGATHER(c_, slot_, gslot_)                                              \
+  do {                                                                               \
+    const uint64_t x_ = X[slot_];                                                    \
+    const bool v_ = (c_) < nch && (kFull || lo + 64ull * (c_) + lane < n);           \
+    const uint32_t xl_ = (uint32_t)x_, p_ = xl_ >> 4;                                \
+    uint32_t pp_ = (uint32_t)__builtin_amdgcn_update_dpp((int)pprev, (int)p_, 0x138, 0xF, 0xF, false); \
+    const bool first_ = batch_first && (c_) == 0 && lane == 0;                       \
+    const bool h_ = v_ && (first_ || p_ != pp_);                                     \
+    bad |= (v_ && ((uint32_t)(x_ >> 32) != 0u || p_ >= n_pages || (!first_ && p_ < pp_) || \
+                   ((xl_ >> 1) & 7u) >= n_nodes)) ? 1u : 0u;                         \
+    Hg[gslot_] = __ballot(h_);                                                       \
+    uint64_t w_ = 0;                                                                 \
+    if (h_ && p_ < n_pages) w_ = pt[p_];                                             \
+    Wg[gslot_] = w_;                                                                 \
+    pprev = (uint32_t)__builtin_amdgcn_readlane((int)p_, 63);                        \
+  } while (0)
+
+#pragma unroll
+  for (uint32_t j = 0; j < kSD; ++j) GDSM_SLOAD(j, j);
+#pragma unroll
+  for (uint32_t j = 0; j < kSG; ++j) GDSM_SGATHER(j, j, j);
+
+  // the span's first event continues the page before it: its first segment starts from PROBE
+  const uint32_t x0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)X[0]);
+  const bool first_cont = !batch_first && nev > 0 && (x0 >> 4) == (xprev >> 4);
+  uint32_t carry = kSProbe;                   // inclusive scan value after the previous chunk
+  uint32_t inv = 0, xfer = 0;
+  uint64_t F64 = 0;                           // per-node faults, 8 bits each
+  bool prefix_done = false;                   // the span's first CONST has been seen
+  uint32_t P8 = 0, pw_node = 0;
+  bool pw = false;
+  bool open_local = false;                    // the open segment started in this span
+  uint32_t open_page = x0 >> 4, open_f0 = 0, open_cnt = 0;
+  bool has_d = false;                         // the span's first segment ended inside it
+  uint32_t d_state = 0, d_cnt = 0, d_page = 0;
+  bool any_head = false;
+
+  for (uint32_t c0 = 0; c0 < nch; c0 += kSD) {
+#pragma unroll
+    for (uint32_t j = 0; j < kSD; ++j) {
+      const uint32_t c = c0 + j;
+      if (c >= nch) break;
+      const uint64_t x = X[j];
+      const uint64_t W = Wg[j % kSG];
+      const uint64_t Hd = Hg[j % kSG];
+      any_head |= Hd != 0;
+      // the open segment closes at the previous chunk's end when this chunk starts a page
+      if (c > 0 && (Hd & 1ull)) {
+        if (open_local) {
+          if (lane == 0 && open_page < n_pages)
+            pt[open_page] = (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32);
+        } else {
+          has_d = true;
+          d_state = carry;
+          d_cnt = open_cnt;
+          d_page = open_page;
+        }
+      }
+      const bool valid = kFull || lo + 64ull * c + lane < n;
+      const uint32_t xl = (uint32_t)x;
+      const bool head = (Hd >> lane) & 1ull;
+      const uint32_t nd = (xl >> 1) & 7u, wr = xl & 1u, bit = 1u << nd;
+      const uint32_t wl = (uint32_t)W & 0x7FFFFu;
+      uint32_t v = wr ? (kSF | 0x60000u | (nd << 8) | bit)
+                      : ((head ? (kSF | wl) : 0u) | (bit << 20));
+      if (!valid) v = 0;
+      if (lane == 0 && !(v & kSF)) v |= carry;
+      const uint32_t incl = sor_scan(v);
+      const uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)incl, 0x138, 0xF,
+                                                                0xF, false);
+      const uint32_t sin = head ? (kSF | wl) : ex;   // the state this event meets
+      const bool exact = (sin & kSF) != 0;
+      const uint32_t st = s_state(sin);
+      const uint32_t cs = st & 0xFFu, own = (st >> 8) & 0xFFu;
+      const bool excl = ((st >> 16) & 3u) == 2u;
+      const bool fault_w = !(excl && own == nd);
+      const bool m = wr ? fault_w : !((cs >> nd) & 1u);
+      const bool mm = valid && (exact || !wr) && m;
+      const bool wx = valid && exact && wr;
+      inv += (wx && fault_w) ? (uint32_t)__popc(cs & ~bit) : 0u;
+      xfer += (wx && own != nd) ? 1u : 0u;
+      F64 += (uint64_t)(mm ? 1u : 0u) << (8u * nd);
+      const uint64_t M = __ballot(mm);
+      // the span's prefix: readers before its first CONST, and that CONST if it is a write
+      if (!prefix_done) {
+        const uint64_t cm = __ballot(valid && (head || wr));
+        if (cm) {
+          const uint32_t l = (uint32_t)__builtin_ctzll(cm);
+          P8 = ((uint32_t)__builtin_amdgcn_readlane((int)ex, (int)l) >> 20) & 0xFFu;
+          pw = !((Hd >> l) & 1ull);
+          pw_node = ((uint32_t)__builtin_amdgcn_readlane((int)xl, (int)l) >> 1) & 7u;
+          prefix_done = true;
+        }
+      }
+      // segments ending inside the chunk: lane i ends when lane i + 1 is a head
+      const uint64_t Ein = Hd >> 1;
+      if (Ein) {
+        const bool end = (Ein >> lane) & 1ull;
+        const uint64_t hb = Hd & lem;
+        const bool inchunk = hb != 0;
+        const uint32_t h = inchunk ? 63u - (uint32_t)__builtin_clzll(hb) : 0u;
+        const uint32_t cnt = popc64(M & lem & ~((1ull << h) - 1ull));
+        const uint32_t f0 = (uint32_t)__shfl((int)(uint32_t)(W >> 32), (int)h, 64);
+        const uint32_t pg = xl >> 4;
+        if (end && pg < n_pages && (inchunk || open_local))
+          pt[pg] = (uint64_t)s_state(incl) |
+                   ((uint64_t)(inchunk ? f0 + cnt : open_f0 + open_cnt + cnt) << 32);
+        if (!open_local) {
+          const uint64_t dm = __ballot(end && !inchunk);
+          if (dm) {  // the span's first segment ends here (lowest end lane)
+            const uint32_t l = (uint32_t)__builtin_ctzll(dm);
+            has_d = true;
+            d_state = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)l);
+            d_cnt = open_cnt + (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)l);
+            d_page = (uint32_t)__builtin_amdgcn_readlane((int)pg, (int)l);
+          }
+        }
+      }
+      // the open segment after this chunk
+      if (Hd) {
+        const uint32_t hl = 63u - (uint32_t)__builtin_clzll(Hd);
+        open_local = true;
+        open_page = (uint32_t)__builtin_amdgcn_readlane((int)(xl >> 4), (int)hl);
+        open_f0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(W >> 32), (int)hl);
+        open_cnt = popc64(M & ~((1ull << hl) - 1ull));
+      } else {
+        open_cnt += popc64(M);
+      }
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      // refill the rings: events kSD chunks ahead, head words kSG chunks ahead
+      GDSM_SLOAD(c + kSD, j);
+      GDSM_SGATHER(c + kSG, (j + kSG) % kSD, j % kSG);
+    }
+  }
+#undef GDSM_SLOAD
+#undef GDSM_SGATHER
+  if (!prefix_done) P8 = (carry >> 20) & 0xFFu;
+  // the open segment at the span's end: closed when the next event starts a page
+  const uint32_t last_page = open_page;
+  const bool next_head = !has_next || ((xnext >> 4) != last_page);
+  bool cont_first = false;   // the span's first segment runs past it
+  if (next_head) {
+    if (open_local) {
+      if (lane == 0 && last_page < n_pages)
+        pt[last_page] = (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32);
+    } else {
+      has_d = true;
+      d_state = carry;
+      d_cnt = open_cnt;
+      d_page = last_page;
+    }
+  } else if (open_local) {
+    if (lane == 0 && open_cnt && last_page < n_pages)
+      atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, open_cnt);
+  } else {
+    cont_first = true;
+  }
+
+  // ---- publish the span's aggregate once its loads landed, then look back
+  const uint32_t agg = (carry & kSF) ? (kConst | s_state(carry)) : ((carry >> 20) & 0xFFu);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0)
+    __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (any_head ? kFHead : 0ull) | agg,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool ordered = has_d;
+  uint32_t cur = 0;
+  if (b > 0) {
+    int64_t pos = (int64_t)b - 1;
+    for (;;) {
+      const int64_t q = pos - (int64_t)lane;
+      uint64_t stv = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : kFIncl;
+      uint32_t sidx, spins = 0;
+      for (;;) {
+        const uint64_t pub = __ballot((stv >> 62) != 0);
+        const uint64_t stop =
+            __ballot(ordered ? (stv & kFHead) != 0
+                             : ((stv >> 62) == 2 || (stv & kFHead) || (stv & kConst)));
+        const uint32_t u = ~pub ? (uint32_t)__builtin_ctzll(~pub) : 64u;
+        sidx = (stop & pub) ? (uint32_t)__builtin_ctzll(stop & pub) : 64u;
+        if (sidx < u || u == 64) break;
+        if (++spins > (1u << 24)) {  // never expected: fail the batch rather than hang the GPU
+          bad = 1;
+          sidx = u;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if ((stv >> 62) == 0 && q >= 0)
+          stv = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t part;
+      if (sidx == 0)
+        part = (uint32_t)lane_bcast64(stv, 0);
+      else
+        part = wave_rev_compose_dpp(lane <= sidx ? (uint32_t)stv : 0u);
+      cur = tcompose(part, cur);
+      if (sidx < 64) break;
+      pos -= 64;
+    }
+    if (lane == 0)
+      __hip_atomic_store(status + b, kFIncl | (any_head ? kFHead : 0ull) | tcompose(cur, agg),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  // ---- the span's first segment, now that its incoming state `cur` is known
+  uint32_t dfc = 0;                 // correction of the first segment's fault count
+  uint32_t Fcorr_node_minus = 0;    // nodes whose probe read fault did not happen
+  uint32_t pw_fault = 0;
+  if (first_cont) {
+    if (!(cur & kConst)) bad = 1;   // a continuing segment always has a CONST before it
+    const uint32_t cs_in = cur & 0xFFu;
+    Fcorr_node_minus = P8 & cs_in;
+    dfc = 0u - (uint32_t)__popc(Fcorr_node_minus);
+    const uint32_t s1 = tcompose(cur, P8) & 0x7FFFFu;
+    if (pw) {
+      const uint32_t cs1 = s1 & 0xFFu, own1 = (s1 >> 8) & 0xFFu;
+      const bool f = !(((s1 >> 16) & 3u) == 2u && own1 == pw_node);
+      if (f) {
+        pw_fault = 1;
+        dfc += 1;
+        inv += lane == 0 ? (uint32_t)__popc(cs1 & ~(1u << pw_node)) : 0u;
+      }
+      xfer += (lane == 0 && own1 != pw_node) ? 1u : 0u;
+    }
+    if (has_d) {
+      const uint32_t word = (d_state & kSF) ? s_state(d_state) : (tcompose(cur, (d_state >> 20) & 0xFFu) & 0x7FFFFu);
+      if (lane == 0 && d_page < n_pages) {
+        uint32_t* pst = reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)d_page;
+        pst[0] = word;
+        const uint32_t c = d_cnt + dfc;
+        if (c) atomicAdd(pst + 1, c);
+      }
+    } else if (cont_first) {
+      const uint32_t c = open_cnt + dfc;
+      if (lane == 0 && c && last_page < n_pages)
+        atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, c);
+    }
+  } else if (has_d || cont_first) {
+    // no prefix (the span starts a page): the first segment was counted exactly
+    if (has_d && lane == 0 && d_page < n_pages) {
+      uint32_t* pst = reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)d_page;
+      pst[0] = s_state(d_state);
+      if (d_cnt) atomicAdd(pst + 1, d_cnt);
+    }
+  }
+
+  // ---- totals: one partial row per span
+  uint32_t tot[10];
+  tot[0] = wave_sum(inv);
+  tot[1] = wave_sum(xfer);
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) tot[2 + q] = wave_sum((uint32_t)(F64 >> (8 * q)) & 0xFFu);
+  if (first_cont) {
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) tot[2 + q] -= (Fcorr_node_minus >> q) & 1u;
+    if (pw_fault) tot[2 + pw_node] += 1;
+  }
+  uint32_t mine = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 10; ++q) mine = lane == q ? tot[q] : mine;
+  if (lane < 10) partial[b * 10 + lane] = mine;
+  if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
+}
+
+template <bool kFull>
+__global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ pt,
+                                                         uint64_t n_pages,
+                                                         const uint64_t* __restrict__ ev,
+                                                         uint64_t n, uint64_t nb,
+                                                         uint64_t* __restrict__ ws,
+                                                         uint32_t* __restrict__ partial,
+                                                         uint32_t* __restrict__ err,
+                                                         uint32_t n_nodes) {
+  __shared__ uint32_t tk;
+  uint64_t b;
+  if (kFull) {  // tickets as coh_fold_kernel
+    const uint32_t cls = blockIdx.x % kFoldCtrs;
+    if (threadIdx.x == 0) tk = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
+    __syncthreads();
+    const uint32_t ticket = __builtin_amdgcn_readfirstlane(tk);
+    const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
+    b = w * 4 + (threadIdx.x >> 6);
+    if (b >= nb) return;
+  } else {
+    if (threadIdx.x >= 64) return;
+    b = nb - 1;
+  }
+  coh_stream_wave<kFull>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes);
+}
+
 // ---------------------------------------------------------------- D: totals
 __global__ __launch_bounds__(256) void coh_reduce_kernel(const uint32_t* __restrict__ partial,
                                                          uint64_t nb,
@@ -729,9 +1108,9 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 // removed in round 4; its last version is in git history, commit 585a356.)
 #ifdef GDSM_MEASURE
 constexpr int kCohVariants = 7;
-static bool coh_variant_ok(int v) { return v == 0 || (v >= 4 && v < kCohVariants); }
+static bool coh_variant_ok(int v) { return v == 0 || v == 1 || (v >= 4 && v < kCohVariants); }
 #else
-static bool coh_variant_ok(int v) { return v == 0; }
+static bool coh_variant_ok(int v) { return v == 0 || v == 1; }
 #endif
 static int coh_variant_from_env() {
   const char* e = getenv("GDSM_COH_VARIANT");
@@ -772,6 +1151,29 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   hipError_t r = hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
   if (r != hipSuccess || n_events == 0) return r;
   if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
+  if (cv == 1) {
+    const uint64_t ns = (n_events + kSpan - 1) / kSpan;
+    uint64_t* fws = reinterpret_cast<uint64_t*>(ws);
+    uint32_t* fpart = reinterpret_cast<uint32_t*>(fws + kFoldStatus + ns);
+    r = hipMemsetAsync(fws, 0, 8 * (kFoldStatus + ns), s);
+    if (r != hipSuccess) return r;
+    {
+      ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
+      const uint64_t full = n_events / kSpan;
+      if (full)
+        hipLaunchKernelGGL(coh_stream_kernel<true>, dim3((unsigned)((full + 3) / 4)), dim3(256), 0,
+                           s, pt, n_pages, events, n_events, full, fws, fpart, err, n_nodes);
+      if (ns > full)
+        hipLaunchKernelGGL(coh_stream_kernel<false>, dim3(1), dim3(64), 0, s, pt, n_pages, events,
+                           n_events, ns, fws, fpart, err, n_nodes);
+    }
+    uint64_t g = (ns + 255) / 256;
+    if (g > 1024) g = 1024;
+    ProfScope ps(prof, GDSM_PROF_COH_REDUCE, s);
+    hipLaunchKernelGGL(coh_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, fpart, ns,
+                       reinterpret_cast<unsigned long long*>(totals));
+    return hipGetLastError();
+  }
   if (cv == 0 || cv >= 4) {
     const uint64_t nf = fold_blocks(n_events);
     uint64_t* fws = reinterpret_cast<uint64_t*>(ws);

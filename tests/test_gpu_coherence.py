@@ -268,7 +268,7 @@ def test_config4_full_size_parity(dist):
     assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
 
 
-@pytest.mark.parametrize("variant", [0])
+@pytest.mark.parametrize("variant", [0, 1])
 def test_every_selectable_coherence_variant(variant):
     """Every coherence path the product library can select (gdsm_tune "coh_variant": 0 = the
     single-pass fold; the round-2 four-pass path is in measurement builds only) is bit-exact on

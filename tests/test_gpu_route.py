@@ -291,7 +291,9 @@ def test_route_notify_local_failure_is_collective():
         init = [s.ctx.coh_download() for s in shards]
         fails = 0
         for _ in range(8):
-            assert lib.gdsm_debug_fail_alloc(shards[2].ctx.handle, 1) == 0
+            # the first call fails the first growth; each later one lets the growth that failed
+            # last time happen and fails the next one
+            assert lib.gdsm_debug_fail_alloc(shards[2].ctx.handle, 2 if fails else 1) == 0
             rcs = notify_all()
             if rcs == [0, 0, 0]:
                 break
