@@ -697,8 +697,9 @@ __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt
 // Status granules, tickets and ordering are the fold's (F above): a wave publishes after its
 // loads landed; a wave that stores the state of a segment opened before it looks back to a span
 // that holds a head.
-constexpr uint32_t kSC = 64;              // chunks per span
-constexpr uint32_t kSpan = 64 * kSC;      // events per span
+// Chunks per span: 64 (4096 events) for whole-GPU batches (coh_variant 1), 4 (256 events) for
+// small batches, where the number of waves in flight, not their efficiency, sets the time.
+constexpr uint32_t kSCBig = 64, kSCSmall = 4;
 constexpr uint32_t kSD = 6;               // event loads in flight (chunks ahead)
 constexpr uint32_t kSG = 3;               // head-word gathers in flight (chunks ahead)
 static_assert(kSD % kSG == 0 && kSG < kSD, "ring geometry");
@@ -734,12 +735,13 @@ __device__ __forceinline__ uint64_t le_mask(uint32_t lane) {  // lanes 0..lane
 }
 __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
 
-template <bool kFull>
+template <uint32_t kSC, bool kFull>
 __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                 const uint64_t* __restrict__ ev, uint64_t n,
                                                 uint64_t b, uint64_t* __restrict__ status,
                                                 uint32_t* __restrict__ partial,
                                                 uint32_t* __restrict__ err, uint32_t n_nodes) {
+  constexpr uint32_t kSpan = 64 * kSC;
   const uint32_t lane = lane_id();
   const uint64_t lo = b * kSpan;
   const uint64_t hi = lo + kSpan;
@@ -1028,7 +1030,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
-template <bool kFull>
+template <uint32_t kSC, bool kFull>
 __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ pt,
                                                          uint64_t n_pages,
                                                          const uint64_t* __restrict__ ev,
@@ -1051,7 +1053,7 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
     if (threadIdx.x >= 64) return;
     b = nb - 1;
   }
-  coh_stream_wave<kFull>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes);
+  coh_stream_wave<kSC, kFull>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes);
 }
 
 // ---------------------------------------------------------------- D: totals
@@ -1101,16 +1103,19 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------- launchers
-// Coherence variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 = the single-pass fold
-// (coh_fold_kernel), the only one in the product library. Measurement builds (-DGDSM_MEASURE,
+// Coherence variant (gdsm_tune "coh_variant" or GDSM_COH_VARIANT): 0 (default) = automatic: the
+// streaming fold with 256-event spans up to kCohSmall events, the single-pass fold
+// (coh_fold_kernel) beyond; 1 = the streaming fold with 4096-event spans at every size; 2 = the
+// single-pass fold at every size. All write the same page table and totals
+// (tests/test_gpu_coherence.py runs each). Measurement builds (-DGDSM_MEASURE,
 // scripts/dev/build_measure.sh; output invalid) add 4 / 5 / 6 = the fold without its walk /
 // without its look-back / without the ordered look-back. (1-3, the round-2 four-pass path, were
 // removed in round 4; its last version is in git history, commit 585a356.)
 #ifdef GDSM_MEASURE
 constexpr int kCohVariants = 7;
-static bool coh_variant_ok(int v) { return v == 0 || v == 1 || (v >= 4 && v < kCohVariants); }
+static bool coh_variant_ok(int v) { return v <= 2 || (v >= 4 && v < kCohVariants); }
 #else
-static bool coh_variant_ok(int v) { return v == 0 || v == 1; }
+static bool coh_variant_ok(int v) { return v >= 0 && v <= 2; }
 #endif
 static int coh_variant_from_env() {
   const char* e = getenv("GDSM_COH_VARIANT");
@@ -1128,9 +1133,16 @@ int coh_tune(const char* key, int64_t value) {
 
 static inline uint64_t fold_blocks(uint64_t n) { return (n + kFBlock - 1) / kFBlock; }
 
+// Batches up to kCohSmall events take the streaming fold with 256-event spans (S above): the
+// fold's 2048-event blocks would leave most of the GPU idle, and a block's serial load -> walk
+// -> look-back chain is the whole batch's time (config 5: ~8000 events per round).
+constexpr uint64_t kCohSmall = 1u << 20;
+
 uint64_t coh_workspace_bytes(uint64_t n_events) {
-  // ticket counters + one status granule per block, one partial row of totals per block
-  const uint64_t nf = fold_blocks(n_events);
+  // ticket counters + one status granule per block (or span), one partial row of totals each;
+  // non-decreasing in n (a workspace reserved for n serves every smaller batch)
+  const uint64_t ns = (min(n_events, kCohSmall) + 64 * kSCSmall - 1) / (64 * kSCSmall);
+  const uint64_t nf = max(ns, fold_blocks(n_events));
   return 8 * (kFoldStatus + nf) + 40 * nf + 512;
 }
 
@@ -1151,21 +1163,25 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   hipError_t r = hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
   if (r != hipSuccess || n_events == 0) return r;
   if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
-  if (cv == 1) {
-    const uint64_t ns = (n_events + kSpan - 1) / kSpan;
+  const bool small = cv == 0 && n_events <= kCohSmall;
+  if (cv == 1 || small) {
+    const uint64_t span = 64ull * (small ? kSCSmall : kSCBig);
+    const uint64_t ns = (n_events + span - 1) / span;
     uint64_t* fws = reinterpret_cast<uint64_t*>(ws);
     uint32_t* fpart = reinterpret_cast<uint32_t*>(fws + kFoldStatus + ns);
     r = hipMemsetAsync(fws, 0, 8 * (kFoldStatus + ns), s);
     if (r != hipSuccess) return r;
     {
       ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
-      const uint64_t full = n_events / kSpan;
+      const uint64_t full = n_events / span;
+      auto kfull = small ? coh_stream_kernel<kSCSmall, true> : coh_stream_kernel<kSCBig, true>;
+      auto ktail = small ? coh_stream_kernel<kSCSmall, false> : coh_stream_kernel<kSCBig, false>;
       if (full)
-        hipLaunchKernelGGL(coh_stream_kernel<true>, dim3((unsigned)((full + 3) / 4)), dim3(256), 0,
-                           s, pt, n_pages, events, n_events, full, fws, fpart, err, n_nodes);
+        hipLaunchKernelGGL(kfull, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
+                           events, n_events, full, fws, fpart, err, n_nodes);
       if (ns > full)
-        hipLaunchKernelGGL(coh_stream_kernel<false>, dim3(1), dim3(64), 0, s, pt, n_pages, events,
-                           n_events, ns, fws, fpart, err, n_nodes);
+        hipLaunchKernelGGL(ktail, dim3(1), dim3(64), 0, s, pt, n_pages, events, n_events, ns, fws,
+                           fpart, err, n_nodes);
     }
     uint64_t g = (ns + 255) / 256;
     if (g > 1024) g = 1024;
@@ -1174,7 +1190,7 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                        reinterpret_cast<unsigned long long*>(totals));
     return hipGetLastError();
   }
-  if (cv == 0 || cv >= 4) {
+  if (cv == 0 || cv == 2 || cv >= 4) {
     const uint64_t nf = fold_blocks(n_events);
     uint64_t* fws = reinterpret_cast<uint64_t*>(ws);
     uint32_t* fpart = reinterpret_cast<uint32_t*>(fws + kFoldStatus + nf);

@@ -732,54 +732,72 @@ __device__ __forceinline__ void store_run_chunk(uint8_t* __restrict__ page, uint
   store_chunk<kNT>(page + cs, mask, pay, pp + (lo - off));
 }
 
-// Applies up to four records at once, one per 16-lane DPP row (a lane per run). Pass 1 validates
-// every header of the row's record (length, bounds, sorted and non-overlapping, total size), so
-// a malformed record writes nothing. Pass 2 spreads the record's (run, 16-B chunk) pairs over
-// the row's lanes — a run is found by a 4-step binary search over the row's pair offsets — so
-// short and long runs cost the same per byte. `has` is false for rows without a record.
-// Returns false in the lanes of a row whose record is malformed.
+// Applies up to four records at once, one per 16-lane DPP row (a lane per run), or, with kW = 64,
+// one record over the whole wave. Pass 1 validates every header of the row's record (length,
+// bounds, sorted and non-overlapping, total size), so a malformed record writes nothing. Pass 2
+// spreads the record's (run, 16-B chunk) pairs over the row's lanes — a run is found by a binary
+// search over the row's pair offsets — so short and long runs cost the same per byte. `has` is
+// false for rows without a record. Returns false in the lanes of a row whose record is malformed.
 // kMode: 0 = plain stores, 1 = MEASUREMENT ONLY (no replica stores), 2 = nontemporal stores.
-template <int kMode, typename P32, typename P8>
+template <uint32_t kW>
+__device__ __forceinline__ uint32_t grp_incl_sum(uint32_t x) {
+  return kW == 16 ? row_incl_sum(x) : wave_incl_sum(x);
+}
+template <uint32_t kW>
+__device__ __forceinline__ uint32_t grp_incl_max(uint32_t x) {
+  return kW == 16 ? row_incl_max(x) : wave_incl_max(x);
+}
+template <uint32_t kW>
+__device__ __forceinline__ uint32_t grp_last(uint32_t x) {
+  return kW == 16 ? row_last(x) : lane_bcast(x, 63);
+}
+template <uint32_t kW>
+__device__ __forceinline__ uint32_t grp_prev(uint32_t x) {
+  return kW == 16 ? row_prev(x) : from_prev_lane(x);
+}
+
+template <int kMode, typename P32, typename P8, uint32_t kW = 16>
 __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32, P8 rec8,
                                            uint32_t size, bool has, uint32_t& sink) {
-  const uint32_t lane = lane_id(), lr = lane & 15, rb = lane & ~15u;
+  static_assert(kW == 16 || kW == 64, "a DPP row or the wave");
+  const uint32_t lane = lane_id(), lr = lane & (kW - 1), rb = lane & ~(kW - 1);
   uint32_t nr = has ? rec32[0] : 0u;
   bool bad = has && (nr == 0 || nr > kMaxRuns || size < 4u + 4u * nr);
   if (bad) nr = 0;
-  const uint32_t nit = lane_bcast(wave_incl_max((nr + 15u) >> 4), 63);
+  const uint32_t nit = lane_bcast(wave_incl_max((nr + kW - 1) / kW), 63);
   uint32_t pay = 0, prev_end = 0, lbad = 0;
   for (uint32_t it = 0; it < nit; ++it) {
-    const uint32_t r = it * 16u + lr;
+    const uint32_t r = it * kW + lr;
     const bool v = r < nr;
     const uint32_t h = v ? rec32[1 + r] : 0u;
     const uint32_t off = h & 0xFFFFu, len = h >> 16, end = v ? off + len : 0u;
-    uint32_t pe = row_prev(end);
+    uint32_t pe = grp_prev<kW>(end);
     if (lr == 0) pe = prev_end;
     if (v && (len == 0 || end > kPage || off < pe)) lbad = 1;
-    pay += row_last(row_incl_sum(v ? len : 0u));
-    prev_end = row_last(end);
+    pay += grp_last<kW>(grp_incl_sum<kW>(v ? len : 0u));
+    prev_end = grp_last<kW>(end);
   }
-  if (row_last(row_incl_max(lbad))) bad = true;
+  if (grp_last<kW>(grp_incl_max<kW>(lbad))) bad = true;
   if (has && !bad && size != 4u + 4u * nr + ((pay + 3u) & ~3u)) bad = true;
   const uint32_t nrw = bad ? 0u : nr;  // runs this row writes
-  const uint32_t nit2 = lane_bcast(wave_incl_max((nrw + 15u) >> 4), 63);
+  const uint32_t nit2 = lane_bcast(wave_incl_max((nrw + kW - 1) / kW), 63);
   uint32_t pcarry = 0;
   for (uint32_t it = 0; it < nit2; ++it) {
-    const uint32_t r = it * 16u + lr;
+    const uint32_t r = it * kW + lr;
     const bool v = r < nrw;
     const uint32_t h = v ? rec32[1 + r] : 0u;
     const uint32_t off = h & 0xFFFFu, len = v ? h >> 16 : 0u, end = off + len;
-    const uint32_t pinc = row_incl_sum(len);
+    const uint32_t pinc = grp_incl_sum<kW>(len);
     const uint32_t pp = 4u + 4u * nr + pcarry + pinc - len;  // payload of this run
-    pcarry += row_last(pinc);
+    pcarry += grp_last<kW>(pinc);
     const uint32_t nch = len ? ((end - 1u) >> 4) - (off >> 4) + 1u : 0u;
-    const uint32_t cinc = row_incl_sum(nch);
+    const uint32_t cinc = grp_incl_sum<kW>(nch);
     const uint32_t cex = cinc - nch;
-    const uint32_t T = row_last(cinc);
+    const uint32_t T = grp_last<kW>(cinc);
     if (__ballot(nch > 2u) == 0) {
       // short runs (<= 2 chunks each, e.g. word-sized edits): every lane stores its own run, no
       // cross-lane lookup (a 4-step bpermute search per 16 pairs dominated many-run records);
-      // longer runs keep the spread below, whose 16 lanes store consecutive chunks
+      // longer runs keep the spread below, whose lanes store consecutive chunks
       for (uint32_t c = 0; c < nch; ++c) {
         if (kMode != 1)
           store_run_chunk<kMode == 2>(page, ((off >> 4) + c) << 4, off, end, rec8, pp);
@@ -789,10 +807,10 @@ __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32
       continue;
     }
     const uint32_t tmax = lane_bcast(wave_incl_max(T), 63);
-    for (uint32_t g = lr; g < ((tmax + 15u) & ~15u); g += 16) {
+    for (uint32_t g = lr; g < ((tmax + kW - 1) & ~(kW - 1)); g += kW) {
       uint32_t i = 0;
 #pragma unroll
-      for (uint32_t step = 8; step; step >>= 1) {
+      for (uint32_t step = kW / 2; step; step >>= 1) {
         const uint32_t c = (uint32_t)__shfl(cex, (int)(rb + i + step), 64);
         if (c <= g) i += step;
       }
@@ -809,6 +827,31 @@ __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32
     }
   }
   return !bad;
+}
+
+// Tiny lists (<= kApplyTiny records): one wave per record, its runs 64 at a time over the whole
+// wave, read straight from global memory. Such a list costs latency, not bandwidth: a page of
+// rewritten doubles is ~500 runs of ~7 bytes (config 5), which one 16-lane row of apply_kernel
+// walked in 33 steps with 4 records per wave.
+constexpr uint64_t kApplyTiny = 4096;
+template <int kMode>
+__global__ __launch_bounds__(256) void apply_tiny_kernel(uint8_t* __restrict__ target,
+                                                         const uint32_t* __restrict__ ids,
+                                                         uint64_t n,
+                                                         const uint64_t* __restrict__ rec_off,
+                                                         const uint8_t* __restrict__ data,
+                                                         uint32_t* __restrict__ err) {
+  const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const uint64_t o0 = rec_off[r], o1 = rec_off[r + 1];
+  const uint64_t p = ids ? ids[r] : r;
+  const uint8_t* rec = data + o0;
+  uint32_t sink = 0;
+  const bool ok = apply_rows<kMode, const uint32_t*, const uint8_t*, 64>(
+      target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec,
+      o1 > o0 ? (uint32_t)min(o1 - o0, (uint64_t)0xFFFFFFFFu) : 0u, o1 > o0, sink);
+  if (__ballot(!ok) && lane_id() == 0) atomicOr(err, 1u);
+  if (kMode == 1 && sink == 0x9E3779B9u) atomicOr(err, 2u);
 }
 
 template <int kMode, uint32_t kApplyWin>
@@ -1421,6 +1464,11 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
   const bool short_list = n <= 16384;
   const uint32_t per_task = short_list ? 4u : 64u;
   const int av = g_apply_variant.load(std::memory_order_relaxed);
+  if (n <= kApplyTiny && av == 0) {
+    hipLaunchKernelGGL(apply_tiny_kernel<0>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s,
+                       target, ids, n, rec_off, data, err);
+    return hipGetLastError();
+  }
   if (!short_list && (av == 0 || av >= 3)) {
     auto kf = av == 0 ? apply_flat_kernel<4096, true, 1>
               : av == 3 ? apply_flat_kernel<8192, true, 1>

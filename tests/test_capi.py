@@ -139,12 +139,12 @@ def test_tune_rejects_measurement_only_variants():
     variants are."""
     from gallocy_amd import _lib
     L = _lib.load()
-    for key, bad in ((b"coh_variant", 2), (b"coh_variant", 3), (b"coh_variant", 4),
+    for key, bad in ((b"coh_variant", 3), (b"coh_variant", 4), (b"coh_variant", -1),
                      (b"diff_variant", 8),
                      (b"apply_variant", 9), (b"no_such_knob", 0)):
         assert L.gdsm_tune(key, bad) == -22, (key, bad)
     for key, ok in ((b"diff_variant", 1), (b"diff_variant", 2), (b"diff_variant", 3),
                     (b"diff_variant", 4), (b"diff_variant", 5), (b"diff_variant", 6), (b"diff_variant", 7),
-                    (b"coh_variant", 0), (b"coh_variant", 1)):
+                    (b"coh_variant", 0), (b"coh_variant", 1), (b"coh_variant", 2)):
         assert L.gdsm_tune(key, ok) == 0
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0

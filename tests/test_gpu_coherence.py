@@ -268,12 +268,12 @@ def test_config4_full_size_parity(dist):
     assert np.array_equal(gfl, fl), np.flatnonzero(gfl != fl)[:10]
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_every_selectable_coherence_variant(variant):
-    """Every coherence path the product library can select (gdsm_tune "coh_variant": 0 = the
-    single-pass fold; the round-2 four-pass path is in measurement builds only) is bit-exact on
-    Zipf batches with hot pages, uploaded arbitrary states, fewer nodes and a partial last
-    block."""
+    """Every coherence path the product library can select (gdsm_tune "coh_variant": 0 =
+    automatic, the streaming fold with 256-event spans for this small batch; 1 = the streaming
+    fold with 4096-event spans; 2 = the single-pass fold at every size) is bit-exact on Zipf batches with hot
+    pages, uploaded arbitrary states, fewer nodes and a partial last block."""
     L = ga.gdsm.lib()
     assert L.gdsm_tune(b"coh_variant", variant) == 0
     try:
