@@ -713,20 +713,22 @@ __device__ __forceinline__ uint32_t s_state(uint32_t v) {
   return (base | R) ^ (flip ? 0x30000u : 0u);
 }
 
-// Segmented OR scan (inclusive) over the 64 lanes: a lane with kSF keeps its value.
+// Segmented OR scan (inclusive) over the 64 lanes: a lane with kSF keeps its value. Per step one
+// v_or_b32_dpp (the source lane's value OR this one; out-of-range sources read 0), then a v_bfi
+// keyed by the lane's own kSF (arithmetic shift): 3 VALU, 4 for the row-masked broadcasts, which
+// leave the rows they skip alone and so need the destination preset.
+template <int kCtrl, int kRowMask, bool kBC>
+__device__ __forceinline__ uint32_t sor_step(uint32_t v) {
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xF, kBC);
+  return bfi((uint32_t)((int32_t)v >> 31), v, t | v);
+}
 __device__ __forceinline__ uint32_t sor_scan(uint32_t v) {
-#define GDSM_SOR(ctrl, rm)                                                  \
-  do {                                                                      \
-    const uint32_t t_ = dpp0<ctrl, rm>(v);                                  \
-    v = v | (t_ & ~(uint32_t)((int32_t)v >> 31));                           \
-  } while (0)
-  GDSM_SOR(0x111, 0xF);
-  GDSM_SOR(0x112, 0xF);
-  GDSM_SOR(0x114, 0xF);
-  GDSM_SOR(0x118, 0xF);
-  GDSM_SOR(0x142, 0xA);
-  GDSM_SOR(0x143, 0xC);
-#undef GDSM_SOR
+  v = sor_step<0x111, 0xF, true>(v);
+  v = sor_step<0x112, 0xF, true>(v);
+  v = sor_step<0x114, 0xF, true>(v);
+  v = sor_step<0x118, 0xF, true>(v);
+  v = sor_step<0x142, 0xA, false>(v);
+  v = sor_step<0x143, 0xC, false>(v);
   return v;
 }
 
@@ -827,15 +829,17 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       const uint32_t xl = (uint32_t)x;
       const bool head = (Hd >> lane) & 1ull;
       const uint32_t nd = (xl >> 1) & 7u, wr = xl & 1u, bit = 1u << nd;
-      const uint32_t wl = (uint32_t)W & 0x7FFFFu;
-      uint32_t v = wr ? (kSF | 0x60000u | (nd << 8) | bit)
-                      : ((head ? (kSF | wl) : 0u) | (bit << 20));
+      const uint32_t wl = kSF | ((uint32_t)W & 0x7FFFFu);  // a head's CONST: its word
+      const uint32_t hmask = 0u - (head ? 1u : 0u);
+      // write: CONST(EXCLUSIVE, owner nd, copyset {nd}, dirty); read: its reader bit (after the
+      // head's word when it is a head). Selected branch-free (a divergent ?: became a branch)
+      uint32_t v = bfi(0u - wr, kSF | 0x60000u | (nd << 8) | bit, (hmask & wl) | (bit << 20));
       if (!valid) v = 0;
-      if (lane == 0 && !(v & kSF)) v |= carry;
+      if (lane == 0) v = bfi((uint32_t)((int32_t)v >> 31), v, v | carry);
       const uint32_t incl = sor_scan(v);
       const uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)incl, 0x138, 0xF,
                                                                 0xF, false);
-      const uint32_t sin = head ? (kSF | wl) : ex;   // the state this event meets
+      const uint32_t sin = bfi(hmask, wl, ex);   // the state this event meets
       const bool exact = (sin & kSF) != 0;
       const uint32_t st = s_state(sin);
       const uint32_t cs = st & 0xFFu, own = (st >> 8) & 0xFFu;

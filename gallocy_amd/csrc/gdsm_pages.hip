@@ -1236,11 +1236,14 @@ __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ t
 //   5  64 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
 //   6  32 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
 //   7  16 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
+//   8  1 page per wave (automatic for lists of <= kDiffTiny pages: a wave per page, and a dense
+//      page's record, ~4.6 KiB for a page of rewritten doubles, fits the LDS buffer instead of
+//      being re-read as the second page of a 2-page unit)
 // Measurement-only kernels (invalid output) are not part of the library.
 static int diff_variant_from_env() {
   const char* e = getenv("GDSM_DIFF_VARIANT");
   const int v = e ? atoi(e) : 0;
-  return (v >= 0 && v <= 7) ? v : 0;
+  return (v >= 0 && v <= 8) ? v : 0;
 }
 static std::atomic<int> g_diff_variant{diff_variant_from_env()};
 static int diff_variant() { return g_diff_variant.load(std::memory_order_relaxed); }
@@ -1269,7 +1272,7 @@ static int apply_variant_from_env() {
 static std::atomic<int> g_apply_variant{apply_variant_from_env()};
 
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 7) {
+  if (!strcmp(key, "diff_variant") && value >= 0 && value <= 8) {
     g_diff_variant.store((int)value, std::memory_order_relaxed);
     return 0;
   }
@@ -1285,7 +1288,7 @@ int tune(const char* key, int64_t value) {
 // the 64-page geometry (a generation word per workgroup slot, then kSpillWGs or
 // fewer workgroup slots of 4 x kDiffSpill bytes). Non-decreasing in n, so a workspace reserved
 // for n fits every shorter list.
-constexpr uint64_t kDiffShort = 32768;
+constexpr uint64_t kDiffShort = 32768, kDiffTiny = 2048;
 constexpr uint32_t kDiffSpill = 24576;
 // Densities (stream bytes per page) the automatic geometry switches at: up to kDense64, 64 pages
 // per wave (their records fill the 8 KiB buffer at 128 B); up to kDense16, 16 pages (8 KiB / 16
@@ -1304,7 +1307,8 @@ static uint64_t spill_pool_bytes(uint64_t n) {
 }
 uint64_t diff_workspace_bytes(uint64_t n) {
   const uint64_t u16 = (n + 15) / 16, u2 = (min(n, kDiffShort) + 1) / 2;
-  const uint64_t base = 8 * (1 + max(u16, u2)) + 64;
+  const uint64_t u1 = diff_variant() == 8 ? n : min(n, kDiffTiny);  // 1-page units
+  const uint64_t base = 8 * (1 + max(max(u16, u2), u1)) + 64;
   return up256(base) + up256(4 * (uint64_t)kSpillWGs) + spill_pool_bytes(n);
 }
 
@@ -1403,11 +1407,15 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
   const uint64_t n = sp.first[sp.G] - sp.first[0];
   int v = diff_variant();
   // the spill pool's place in the workspace (after the largest status area n may need)
-  const uint64_t status_end = up256(8 * (1 + max((n + 15) / 16, (min(n, kDiffShort) + 1) / 2)) + 64);
+  const uint64_t u1 = v == 8 ? n : min(n, kDiffTiny);
+  const uint64_t status_end =
+      up256(8 * (1 + max(max((n + 15) / 16, (min(n, kDiffShort) + 1) / 2), u1)) + 64);
   const uint64_t pool_at = status_end + up256(4 * (uint64_t)kSpillWGs);
   const bool pool_ok = ws_bytes >= pool_at + spill_pool_bytes(n);
   if (v == 0) {
-    if (n <= kDiffShort)
+    if (n <= kDiffTiny)
+      v = 8;
+    else if (n <= kDiffShort)
       v = 3;
     else if (bpp_hint)  // the density this context saw last: sparse -> 64 pages, denser -> 16
       v = bpp_hint <= kDense64 ? (pool_ok ? 5 : 4) : bpp_hint <= kDense16 || !pool_ok ? 1 : 7;
@@ -1416,7 +1424,7 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
   }
   const bool spill = v >= 5;
   if (spill && !pool_ok) return hipErrorInvalidValue;
-  const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : (v == 2 || v == 6) ? 32 : 16;
+  const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : v == 8 ? 1 : (v == 2 || v == 6) ? 32 : 16;
   sp.ustart[0] = 0;
   for (uint32_t d = 0; d < sp.G; ++d)
     sp.ustart[d + 1] = sp.ustart[d] + (sp.first[d + 1] - sp.first[d] + U - 1) / U;
@@ -1439,6 +1447,7 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
                        : v == 7 ? diff_single_kernel<16, 8192, 4, true, kDiffSpill>
                        : v == 4 ? diff_single_kernel<64, 8192, 4, true>
                        : v == 3 ? diff_single_kernel<2, 8192, 4, true>
+                       : v == 8 ? diff_single_kernel<1, 8192, 4, true>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, true>
                                 : diff_single_kernel<16, 8192, 4, true>)
                      : (v == 5   ? diff_single_kernel<64, 8192, 4, false, kDiffSpill>
@@ -1446,6 +1455,7 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
                        : v == 7 ? diff_single_kernel<16, 8192, 4, false, kDiffSpill>
                        : v == 4 ? diff_single_kernel<64, 8192, 4, false>
                        : v == 3 ? diff_single_kernel<2, 8192, 4, false>
+                       : v == 8 ? diff_single_kernel<1, 8192, 4, false>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,

@@ -98,7 +98,8 @@ def test_workspace_sizing():
     (16 pages per wave, plus two workgroups for the partial units of split streams: a
     generation word per workgroup slot, up to 1280 workgroup slots of 4 x 24 KiB); non-decreasing
     in n. Short lists (<= 32768 pages, the 2-page geometry) get no spill pool unless a spill
-    geometry is forced (gdsm_tune "diff_variant" 5-7)."""
+    geometry is forced (gdsm_tune "diff_variant" 5-7); lists of <= 2048 pages take one page per
+    wave (a granule per page)."""
     from gallocy_amd import _lib
     lib = _lib.load()
     up = lambda v: (v + 255) // 256 * 256  # noqa: E731
@@ -108,8 +109,8 @@ def test_workspace_sizing():
         try:
             for n in (1, 1000, 32768, 32769, 1 << 20, 1 << 24):
                 pool = slots(n) * 4 * 24576 if (n > 32768 or forced) else 0
-                want = up(8 * (1 + max((n + 15) // 16, (min(n, 32768) + 1) // 2)) + 64) \
-                    + up(4 * 1280) + pool
+                want = up(8 * (1 + max((n + 15) // 16, (min(n, 32768) + 1) // 2,
+                                       min(n, 2048))) + 64) + up(4 * 1280) + pool
                 assert lib.gdsm_diff_workspace_bytes(n) == want, (n, forced)
             sizes = [lib.gdsm_diff_workspace_bytes(n) for n in range(1, 200000, 997)]
             assert sizes == sorted(sizes)
@@ -140,11 +141,12 @@ def test_tune_rejects_measurement_only_variants():
     from gallocy_amd import _lib
     L = _lib.load()
     for key, bad in ((b"coh_variant", 3), (b"coh_variant", 4), (b"coh_variant", -1),
-                     (b"diff_variant", 8),
+                     (b"diff_variant", 9),
                      (b"apply_variant", 9), (b"no_such_knob", 0)):
         assert L.gdsm_tune(key, bad) == -22, (key, bad)
     for key, ok in ((b"diff_variant", 1), (b"diff_variant", 2), (b"diff_variant", 3),
                     (b"diff_variant", 4), (b"diff_variant", 5), (b"diff_variant", 6), (b"diff_variant", 7),
+                    (b"diff_variant", 8),
                     (b"coh_variant", 0), (b"coh_variant", 1), (b"coh_variant", 2)):
         assert L.gdsm_tune(key, ok) == 0
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0

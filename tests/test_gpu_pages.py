@@ -533,7 +533,7 @@ def _lds_overflow_pages(rng, n):
     return tw, cu
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_diff_variants_bit_exact(variant, golden):
     """Every diff geometry (gdsm_tune "diff_variant": automatic, 16, 32, 2 or 64 pages per wave,
     64 pages per wave with the global spill slot) is bit-exact on edge pages, random byte
@@ -592,7 +592,7 @@ def test_c1_windows_pinned_by_reference_diff(golden):
         assert zlib.crc32(rep[w].tobytes()) == int(g["crc"][w][1]), w
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_diff_apply_fused_equals_diff_then_apply(variant, golden):
     """gdsm_diff_apply (the diff kernel also applying the runs to a home copy on this GPU) writes
     the same stream as gdsm_diff, and leaves the target exactly as gdsm_apply of that stream
@@ -761,7 +761,7 @@ def test_apply_variants_long_lists(variant):
         L.gdsm_tune(b"apply_variant", 0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5, 6, 7, 8])
 def test_diff_split_equals_per_range_diffs(variant):
     """gdsm_diff_split (one launch, G <= 8 streams, each with its own look-back chain) writes
     exactly the stream gdsm_diff writes for each range, in every diff geometry: ranges that are
