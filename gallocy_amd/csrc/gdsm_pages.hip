@@ -1301,7 +1301,7 @@ static inline uint64_t up256(uint64_t v) { return (v + 255) & ~255ull; }
 // streams (launch_diff_split: each stream's last unit may be partial): two more workgroups. None
 // for short lists, which take the 2-page geometry, unless a spill geometry is forced (gdsm_tune).
 static uint64_t spill_pool_bytes(uint64_t n) {
-  if (n <= kDiffShort && diff_variant() < 5) return 0;
+  if (n <= kDiffShort && (diff_variant() < 5 || diff_variant() > 7)) return 0;
   const uint64_t wgs = ((n + 15) / 16 + 3) / 4 + 2;
   return (uint64_t)(wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill;
 }
@@ -1422,7 +1422,7 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
     else  // unknown density: 64 pages with the spill slot, valid at any density
       v = pool_ok ? 5 : (cap <= 128 * n) ? 4 : (cap <= 384 * n) ? 2 : 1;
   }
-  const bool spill = v >= 5;
+  const bool spill = v >= 5 && v <= 7;  // 8: one page per wave, no spill slot
   if (spill && !pool_ok) return hipErrorInvalidValue;
   const uint32_t U = (v == 4 || v == 5) ? 64 : v == 3 ? 2 : v == 8 ? 1 : (v == 2 || v == 6) ? 32 : 16;
   sp.ustart[0] = 0;
