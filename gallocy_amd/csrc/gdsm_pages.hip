@@ -830,9 +830,10 @@ __device__ __forceinline__ bool apply_rows(uint8_t* __restrict__ page, P32 rec32
 }
 
 // Tiny lists (<= kApplyTiny records): one wave per record, its runs 64 at a time over the whole
-// wave, read straight from global memory. Such a list costs latency, not bandwidth: a page of
-// rewritten doubles is ~500 runs of ~7 bytes (config 5), which one 16-lane row of apply_kernel
-// walked in 33 steps with 4 records per wave.
+// wave. Such a list costs latency, not bandwidth: a page of rewritten doubles is ~500 runs of ~7
+// bytes (config 5), which one 16-lane row of apply_kernel walked in 33 steps with 4 records per
+// wave. The record is staged in LDS first (16 B per lane by LDS-DMA, every load in flight at
+// once): read from global memory, each of the run loops' steps waited one round trip.
 constexpr uint64_t kApplyTiny = 4096;
 template <int kMode>
 __global__ __launch_bounds__(256) void apply_tiny_kernel(uint8_t* __restrict__ target,
@@ -841,16 +842,38 @@ __global__ __launch_bounds__(256) void apply_tiny_kernel(uint8_t* __restrict__ t
                                                          const uint64_t* __restrict__ rec_off,
                                                          const uint8_t* __restrict__ data,
                                                          uint32_t* __restrict__ err) {
+  // +4 dwords: pay_dw's second dword at the record's end stays inside the buffer
+  __shared__ __attribute__((aligned(16))) uint32_t win_all[4][kApplyWinShort / 4 + 4];
   const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n) return;
+  const uint32_t lane = lane_id();
+  uint32_t* win = win_all[threadIdx.x >> 6];
   const uint64_t o0 = rec_off[r], o1 = rec_off[r + 1];
   const uint64_t p = ids ? ids[r] : r;
   const uint8_t* rec = data + o0;
+  const uint32_t size = o1 > o0 ? (uint32_t)min(o1 - o0, (uint64_t)0xFFFFFFFFu) : 0u;
   uint32_t sink = 0;
-  const bool ok = apply_rows<kMode, const uint32_t*, const uint8_t*, 64>(
-      target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec,
-      o1 > o0 ? (uint32_t)min(o1 - o0, (uint64_t)0xFFFFFFFFu) : 0u, o1 > o0, sink);
-  if (__ballot(!ok) && lane_id() == 0) atomicOr(err, 1u);
+  bool ok;
+  if (size <= kApplyWinShort) {
+    typedef __attribute__((address_space(1))) void* gptr;
+    typedef __attribute__((address_space(3))) void* lptr;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(rec);
+    const uint32_t words = size >> 2, n16 = words >> 2;
+    for (uint32_t q0 = 0; q0 < 4 * n16; q0 += 256) {
+      const uint32_t q = q0 / 4 + lane;
+      if (q < n16) __builtin_amdgcn_global_load_lds((gptr)(src + 4 * q), (lptr)(win + q0), 16, 0, 0);
+    }
+    const uint32_t qt = 4 * n16 + lane;
+    if (qt < words) __builtin_amdgcn_global_load_lds((gptr)(src + qt), (lptr)(win + 4 * n16), 4, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the record has landed
+    wave_lds_sync();
+    ok = apply_rows<kMode, const uint32_t*, const uint8_t*, 64>(
+        target + p * kPage, win, reinterpret_cast<const uint8_t*>(win), size, size > 0, sink);
+  } else {  // larger than any well-formed record: validated (and refused) from global memory
+    ok = apply_rows<kMode, const uint32_t*, const uint8_t*, 64>(
+        target + p * kPage, reinterpret_cast<const uint32_t*>(rec), rec, size, true, sink);
+  }
+  if (__ballot(!ok) && lane == 0) atomicOr(err, 1u);
   if (kMode == 1 && sink == 0x9E3779B9u) atomicOr(err, 2u);
 }
 
