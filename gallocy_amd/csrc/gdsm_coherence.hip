@@ -737,12 +737,15 @@ __device__ __forceinline__ uint64_t le_mask(uint32_t lane) {  // lanes 0..lane
 }
 __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
 
+// totals != nullptr (small batches): the span's totals are added to the batch totals directly
+// (10 atomics per span) instead of a partial row for coh_reduce_kernel: one launch fewer.
 template <uint32_t kSC, bool kFull>
 __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                 const uint64_t* __restrict__ ev, uint64_t n,
                                                 uint64_t b, uint64_t* __restrict__ status,
                                                 uint32_t* __restrict__ partial,
-                                                uint32_t* __restrict__ err, uint32_t n_nodes) {
+                                                uint32_t* __restrict__ err, uint32_t n_nodes,
+                                                unsigned long long* __restrict__ totals) {
   constexpr uint32_t kSpan = 64 * kSC;
   const uint32_t lane = lane_id();
   const uint64_t lo = b * kSpan;
@@ -1030,7 +1033,11 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   uint32_t mine = 0;
 #pragma unroll
   for (uint32_t q = 0; q < 10; ++q) mine = lane == q ? tot[q] : mine;
-  if (lane < 10) partial[b * 10 + lane] = mine;
+  if (totals) {
+    if (lane < 10 && mine) atomicAdd(totals + lane, (unsigned long long)mine);
+  } else if (lane < 10) {
+    partial[b * 10 + lane] = mine;
+  }
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
@@ -1042,7 +1049,8 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
                                                          uint64_t* __restrict__ ws,
                                                          uint32_t* __restrict__ partial,
                                                          uint32_t* __restrict__ err,
-                                                         uint32_t n_nodes) {
+                                                         uint32_t n_nodes,
+                                                         unsigned long long* __restrict__ totals) {
   __shared__ uint32_t tk;
   uint64_t b;
   if (kFull) {  // tickets as coh_fold_kernel
@@ -1057,7 +1065,8 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
     if (threadIdx.x >= 64) return;
     b = nb - 1;
   }
-  coh_stream_wave<kSC, kFull>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes);
+  coh_stream_wave<kSC, kFull>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes,
+                              totals);
 }
 
 // ---------------------------------------------------------------- D: totals
@@ -1180,13 +1189,15 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
       const uint64_t full = n_events / span;
       auto kfull = small ? coh_stream_kernel<kSCSmall, true> : coh_stream_kernel<kSCBig, true>;
       auto ktail = small ? coh_stream_kernel<kSCSmall, false> : coh_stream_kernel<kSCBig, false>;
+      unsigned long long* direct = small ? reinterpret_cast<unsigned long long*>(totals) : nullptr;
       if (full)
         hipLaunchKernelGGL(kfull, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
-                           events, n_events, full, fws, fpart, err, n_nodes);
+                           events, n_events, full, fws, fpart, err, n_nodes, direct);
       if (ns > full)
         hipLaunchKernelGGL(ktail, dim3(1), dim3(64), 0, s, pt, n_pages, events, n_events, ns, fws,
-                           fpart, err, n_nodes);
+                           fpart, err, n_nodes, direct);
     }
+    if (small) return hipGetLastError();
     uint64_t g = (ns + 255) / 256;
     if (g > 1024) g = 1024;
     ProfScope ps(prof, GDSM_PROF_COH_REDUCE, s);
