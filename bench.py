@@ -602,10 +602,11 @@ def run_mmult(args):
                "kernel_ms_per_round": round(kern_ms / rounds, 5),
                "wall_ms_per_round_profiled": round(dt2 / rounds * 1e3, 5),
                "stages": stages,
-               "note": "a round is ~12 dense pages: the kernels' own time is a fraction of the "
-                       "round, the rest is the device-side issue cost of ~10 dependent tiny "
-                       "operations on two streams; one HIP graph of every round (--graph) "
-                       "measured no faster (replay.py). No HBM or MFMA roofline applies."}
+               "note": "a round is ~10 dense pages (~500 runs each) and ~8000 fault events: "
+                       "every operation is a few microseconds of dependent latency, so the round "
+                       "is its operation count on the longer of two streams (page data: twin, "
+                       "row writes, diff+apply; page table: the coherence batch). No HBM or "
+                       "MFMA roofline applies."}
     res = {"metric": "mmult trace replay rounds/sec", "value": round(R.T.rounds / dt, 1),
            "unit": "rounds/s", "n_gpus": 1, "steps": R.T.rounds, "warmup": 0,
            "ms_per_step": round(dt / R.T.rounds * 1e3, 4), "higher_is_better": True,
@@ -617,6 +618,8 @@ def run_mmult(args):
            "seconds_total": round(dt, 4),
            "launch": f"one HIP graph of every round (recorded in {R.graph_build_s:.2f} s, untimed)"
                      if args.graph else "eager, two streams",
+           "round": "coherence batch | twin, the round's row writes (one batched copy), diff "
+                    "applying its runs to the home copies (gdsm_diff_apply_ids)",
            "events_per_s": round(R.events_total / dt, 1),
            "rows_per_s": round(args.ndim / dt, 1),
            "home_copy_equals_product": ok,

@@ -53,6 +53,7 @@ SIGNATURES = {
     "gdsm_memcpy_h2d": (C.c_int, [vp, vp, vp, C.c_uint64]),
     "gdsm_memcpy_d2h": (C.c_int, [vp, vp, vp, C.c_uint64]),
     "gdsm_memcpy_d2d": (C.c_int, [vp, vp, vp, C.c_uint64]),
+    "gdsm_memcpy_batch": (C.c_int, [vp, vp, C.c_uint64]),
     "gdsm_capture_begin": (C.c_int, [vp]),
     "gdsm_capture_join": (C.c_int, [vp, vp]),
     "gdsm_capture_end": (C.c_int, [vp, C.POINTER(vp)]),
@@ -69,6 +70,7 @@ SIGNATURES = {
     "gdsm_runs_free": (C.c_int, [vp, C.POINTER(GdsmRuns)]),
     "gdsm_diff": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns)]),
     "gdsm_diff_apply": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns), C.c_int]),
+    "gdsm_diff_apply_ids": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns), C.c_int, vp]),
     "gdsm_diff_split": (C.c_int, [vp, vp, C.c_uint32, C.POINTER(GdsmRuns)]),
     "gdsm_runs_total": (C.c_int, [vp, C.POINTER(GdsmRuns), C.POINTER(C.c_uint64)]),
     "gdsm_apply": (C.c_int, [vp, C.c_int, vp, C.POINTER(GdsmRuns)]),

@@ -80,7 +80,7 @@ int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const ui
   ctx->ids_safe[which] = reinterpret_cast<uint32_t*>(buf);
   if (rc) return rc;
   GDSM_TRY(gdsm::launch_check_ids(ids, n, ctx->n_pages, ctx->ids_safe[which], ctx->err,
-                                  which ? ctx->aux : ctx->stream));
+                                  which == 1 ? ctx->aux : ctx->stream));
   *out = ctx->ids_safe[which];
   return 0;
 }
@@ -396,9 +396,11 @@ int gdsm_reserve(gdsm_ctx* ctx, uint64_t diff_pages, uint64_t coh_events) {
     rc = ensure(ctx, &ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(diff_pages));
     // checked copies of the id lists of diff / twin / apply on the main stream
     if (!rc) {
-      uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[0]);
-      rc = ensure(ctx, &buf, &ctx->ids_safe_bytes[0], 4 * diff_pages);
-      ctx->ids_safe[0] = reinterpret_cast<uint32_t*>(buf);
+      for (int w : {0, 2}) {  // the diff's page list and gdsm_diff_apply_ids' target list
+        uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[w]);
+        if (!rc) rc = ensure(ctx, &buf, &ctx->ids_safe_bytes[w], 4 * diff_pages);
+        ctx->ids_safe[w] = reinterpret_cast<uint32_t*>(buf);
+      }
     }
   }
   if (!rc && coh_events)
@@ -475,6 +477,15 @@ int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches) {
     launches[i] = ctx->prof.launches[i];
   }
   ctx->prof.clear();
+  return 0;
+}
+
+int gdsm_memcpy_batch(gdsm_ctx* ctx, const uint64_t* desc, uint64_t n) {
+  if (!ctx || (n && !desc)) return -EINVAL;
+  if (!n) return 0;
+  CtxGuard g(ctx);
+  if (g.rc) return g.rc;
+  GDSM_TRY(gdsm::launch_copy_batch(desc, n, ctx->stream));
   return 0;
 }
 
@@ -570,7 +581,7 @@ int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs) {
 }
 
 static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,
-                     int target) {
+                     int target, const uint32_t* tids = nullptr) {
   if (!ctx || !out || !out->rec_off || (!out->data && out->cap)) return -EINVAL;
   if (!ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
   if (target >= 0 && (target > 2 || target == GDSM_TWIN || target == GDSM_CURRENT ||
@@ -589,13 +600,20 @@ static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* 
   if (busy != ctx->runs_busy.end()) GDSM_TRY(hipStreamWaitEvent(ctx->stream, busy->second, 0));
   int rc = ensure(ctx, &ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
   if (!rc) rc = safe_ids(ctx, ids, n, 0, &ids);
+  if (!rc && tids) rc = safe_ids(ctx, tids, n, 2, &tids);
   if (rc) return rc;
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
                              ctx->stream, ctx->P(), target >= 0 ? ctx->arena[target] : nullptr,
-                             ctx->diff_bpp));
+                             ctx->diff_bpp, tids));
   return 0;
+}
+
+int gdsm_diff_apply_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,
+                        int target, const uint32_t* target_ids) {
+  if (target < 0 || (n && !target_ids)) return -EINVAL;
+  return diff_impl(ctx, ids, n, out, target, target_ids);
 }
 
 int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out) {

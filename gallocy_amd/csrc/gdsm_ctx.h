@@ -52,8 +52,9 @@ struct gdsm_ctx {
   uint64_t wire_hdr[4] = {};  // host staging of the frame header
   // checked copies of caller page-id lists (launch_check_ids): one per stream, so an async
   // apply's list is never overwritten by a call on the main stream
-  uint32_t* ids_safe[2] = {nullptr, nullptr};
-  uint64_t ids_safe_bytes[2] = {0, 0};
+  // [2]: the target-page list of gdsm_diff_apply_ids (main stream, beside [0])
+  uint32_t* ids_safe[3] = {nullptr, nullptr, nullptr};
+  uint64_t ids_safe_bytes[3] = {0, 0, 0};
   // graph capture (gdsm_capture_*): open on this context's stream (or joined into another's)
   bool capturing = false;
   bool capture_origin = false;  // this context began the capture (only it may end it)
@@ -83,7 +84,8 @@ int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need);
 int join_aux(gdsm_ctx* ctx);
 // Creates ctx->aux and its events on first use.
 int ensure_aux(gdsm_ctx* ctx);
-// A caller's device id list checked against the arenas on stream `which` (0 main, 1 aux).
+// A caller's device id list checked against the arenas into buffer `which` (0 and 2 on the main
+// stream, 1 on aux).
 int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const uint32_t** out);
 int check_and_clear_err(gdsm_ctx* ctx);
 // Records the stream density (bytes / pages) the host learned, for the diff's geometry choice

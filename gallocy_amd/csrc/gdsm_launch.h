@@ -19,12 +19,14 @@ hipError_t launch_gen_pages(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint6
 hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        hipStream_t s, Prof* prof = nullptr);
 // Full diff of n pages in one pass: rec_off[n+1], data[cap]. With `target`, the runs are also
-// applied to target (same page ids) by the same kernel. bpp_hint: stream bytes per page the
-// caller saw last time (0 = unknown); it only picks the geometry.
+// applied to target by the same kernel, page tids[i] for list entry i (tids NULL: the same page
+// ids). bpp_hint: stream bytes per page the caller saw last time (0 = unknown); it only picks
+// the geometry.
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr,
-                       uint8_t* target = nullptr, uint32_t bpp_hint = 0);
+                       uint8_t* target = nullptr, uint32_t bpp_hint = 0,
+                       const uint32_t* tids = nullptr);
 // The diff kernel's output streams: list entries [first[d], first[d+1]) go to stream d (record
 // i of stream d = entry first[d] + i); ustart: the first work unit of each stream (set by the
 // launcher). One launch serves them all, each stream with its own look-back chain.
@@ -38,6 +40,7 @@ struct DiffSplit {
   uint32_t G;
 };
 // One diff launch over arena pages [first[0], first[G]) (ids = identity) into sp's G streams.
+hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s);
 hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
                              uint64_t ws_bytes, hipStream_t s, Prof* prof, uint32_t bpp_hint);
 hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,

@@ -420,7 +420,8 @@ template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill =
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
-    uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool) {
+    uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool,
+    const uint32_t* __restrict__ tids) {
   static_assert(kU <= 64 && (kU & (kU - 1)) == 0, "unit size");
   __shared__ uint32_t sel_tab[16];
   __shared__ uint32_t ent_all[4][64];
@@ -478,6 +479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   uint64_t pj = ids ? ids[i0] : i0;
   load_page(twin, cur, pj, lane, t, c);
   for (uint32_t j = 0; j < cnt; ++j) {
+    const uint64_t pt_ = kApply ? (tids ? (uint64_t)tids[i0 + j] : pj) : 0;  // page at target
     uint32_t m[4], D = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -490,7 +492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
         dat[rank] = c[k];
       }
       D += (uint32_t)__popcll(B);
-      if (kApply && m[k]) store_masked16(target + pj * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
+      if (kApply && m[k]) store_masked16(target + pt_ * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
     }
     if (j + 1 < cnt) {
       pj = ids ? ids[i0 + j + 1] : i0 + j + 1;
@@ -1387,14 +1389,39 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
   return hipGetLastError();
 }
 
+// n device-to-device copies in one launch (gdsm_memcpy_batch): copy i = desc[3i .. 3i+2] =
+// (dst, src, bytes), one workgroup per copy; 16 B per lane where dst, src and bytes are 16-aligned,
+// else bytes.
+__global__ __launch_bounds__(256) void copy_batch_kernel(const uint64_t* __restrict__ desc,
+                                                         uint64_t n) {
+  for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    uint8_t* dst = reinterpret_cast<uint8_t*>(desc[3 * i]);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(desc[3 * i + 1]);
+    const uint64_t bytes = desc[3 * i + 2];
+    if (((uintptr_t)dst | (uintptr_t)src | bytes) & 15u) {
+      for (uint64_t b = threadIdx.x; b < bytes; b += blockDim.x) dst[b] = src[b];
+    } else {
+      for (uint64_t q = threadIdx.x; q < bytes / 16; q += blockDim.x)
+        reinterpret_cast<uint4*>(dst)[q] = reinterpret_cast<const uint4*>(src)[q];
+    }
+  }
+}
+
+hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(copy_batch_kernel, dim3(grid_for(n, 1, 65536)), dim3(256), 0, s, desc, n);
+  return hipGetLastError();
+}
+
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
-                                   Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap);
+                                   Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
+                                   const uint32_t* tids);
 
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target,
-                       uint32_t bpp_hint) {
+                       uint32_t bpp_hint, const uint32_t* tids) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   DiffSplit sp{};
   sp.G = 1;
@@ -1403,7 +1430,7 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   sp.cap[0] = cap;
   sp.first[0] = 0;
   sp.first[1] = n;
-  return launch_diff_impl(twin, cur, ids, sp, ws, ws_bytes, s, prof, target, bpp_hint, cap);
+  return launch_diff_impl(twin, cur, ids, sp, ws, ws_bytes, s, prof, target, bpp_hint, cap, tids);
 }
 
 hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
@@ -1420,13 +1447,14 @@ hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit 
   }
   if (sp.first[sp.G] == sp.first[0]) return hipSuccess;
   return launch_diff_impl(twin, cur, nullptr, sp, ws, ws_bytes, s, prof, nullptr, bpp_hint,
-                          mincap);
+                          mincap, nullptr);
 }
 
 // `cap` (the smallest stream capacity) only matters to workspaces that predate the spill pool.
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
-                                   Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap) {
+                                   Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
+                                   const uint32_t* tids) {
   const uint64_t n = sp.first[sp.G] - sp.first[0];
   int v = diff_variant();
   // the spill pool's place in the workspace (after the largest status area n may need)
@@ -1482,7 +1510,7 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,
-                     reinterpret_cast<uint64_t*>(ws), target, gen, pool);
+                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids);
   return hipGetLastError();
 }
 

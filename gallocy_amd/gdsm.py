@@ -283,13 +283,18 @@ class Context:
             o.s.n = arr[d].n
 
     def diff(self, ids=None, n: Optional[int] = None, out: Optional[Runs] = None, cap: int = 0,
-             apply_to: Optional[str] = None) -> Runs:
+             apply_to: Optional[str] = None, target_ids=None) -> Runs:
         """TWIN vs CURRENT -> Runs; with apply_to (normally "replica"), the same kernel also
-        applies the runs to that arena (gdsm_diff_apply: a home copy on this GPU)."""
+        applies the runs to that arena (gdsm_diff_apply: a home copy on this GPU), at the pages
+        target_ids (device list, gdsm_diff_apply_ids) when they are not the same ids."""
         n = self._count(ids, n)
         out = out or Runs(self, n, cap)
         if apply_to is None:
             check(lib().gdsm_diff(self.handle, self._ptr(ids), n, C.byref(out.s)), "gdsm_diff")
+        elif target_ids is not None:
+            check(lib().gdsm_diff_apply_ids(self.handle, self._ptr(ids), n, C.byref(out.s),
+                                            _ARENA[apply_to], self._ptr(target_ids)),
+                  "gdsm_diff_apply_ids")
         else:
             check(lib().gdsm_diff_apply(self.handle, self._ptr(ids), n, C.byref(out.s),
                                         _ARENA[apply_to]), "gdsm_diff_apply")

@@ -10,11 +10,13 @@ rank; here the per-node views live side by side in one arena):
 Per round (one row per node, gallocy_amd/trace.py):
   1. coherence batch of the round's R/W fault events (SPEC §5);
   2. twin of every c[i] page the round writes (SPEC §2), taken in each writer's view;
-  3. each writer stores its row c[i][*] into its own view (the application's writes);
-  4. one diff of all those pages (SPEC §3) — release;
-  5. apply of the stream to the home copies (SPEC §4). Rows sharing a page are written by
-     different nodes at disjoint bytes: their records hit the same home page with disjoint
-     runs, which the store-only apply handles without a read-modify-write race.
+  3. each writer stores its row c[i][*] into its own view (the application's writes; all of the
+     round's rows as one batched copy, gdsm_memcpy_batch);
+  4. one diff of all those pages (SPEC §3) — release — whose kernel also applies the runs to
+     the home copies (gdsm_diff_apply_ids: view page t·Z + p -> home page p; fused=False: a
+     separate apply of the stream, SPEC §4). Rows sharing a page are written by different nodes
+     at disjoint bytes: their records hit the same home page with disjoint runs, which the
+     store-only apply handles without a read-modify-write race.
 The trace, the rows' values and the page lists are prepared on the host before the timed
 replay; a round is then only asynchronous launches on two streams (page table, page data),
 or, with run(graph=True), one HIP graph of all rounds recorded beforehand.
@@ -32,7 +34,9 @@ from .trace import PAGE_SZ, MmultTrace, c_row_values, mmult_layout, zone_image
 
 
 class MmultReplay:
-    def __init__(self, ndim: int = 1000, nodes: int = 4, seed: int = 0, device: int = 0):
+    def __init__(self, ndim: int = 1000, nodes: int = 4, seed: int = 0, device: int = 0,
+                 fused: bool = True):
+        self.fused = fused
         self.L = mmult_layout(ndim)
         self.T = MmultTrace(self.L, nodes, seed)
         self.P = nodes
@@ -76,6 +80,16 @@ class MmultReplay:
         self.d_home = self.data.buffer(max(4, home.nbytes)).upload(home)
         self.d_rows = self.data.buffer(rowvals.nbytes).upload(rowvals)
         self.row_bytes = 8 * L.ndim
+        # the rounds' row writes as (dst, src, bytes) copy descriptors, back to back
+        base = self.data.arena_ptr("current")
+        desc, self.desc_off = [], [0]
+        for rows in self.rows:
+            for t, i in rows:
+                desc += [base + t * self.Z * PAGE_SZ + int(L.c_rows[i]),
+                         self.d_rows.ptr + i * self.row_bytes, self.row_bytes]
+            self.desc_off.append(len(desc) // 3)
+        desc = np.array(desc or [0, 0, 0], np.uint64)
+        self.d_desc = self.data.buffer(desc.nbytes).upload(desc)
         max_ids = int(np.max(np.diff(self.id_off))) if len(self.id_off) > 1 else 1
         self._runs = gdsm.Runs(self.data, max_ids, cap=max_ids * 10244)
         max_ev = int(np.max(np.diff(self.ev_off))) if len(self.ev_off) > 1 else 1
@@ -93,13 +107,14 @@ class MmultReplay:
         a, b = int(self.id_off[r]), int(self.id_off[r + 1])
         ids, home, n = self.d_ids.ptr + 4 * a, self.d_home.ptr + 4 * a, b - a
         self.data.twin(ids, n=n)                                                           # 2
-        base = self.data.arena_ptr("current")
-        for t, i in self.rows[r]:                                                          # 3
-            dst = base + t * self.Z * PAGE_SZ + int(self.L.c_rows[i])
-            gdsm.check(lib.gdsm_memcpy_d2d(self.data.handle, dst, self.d_rows.ptr + i * self.row_bytes,
-                                           self.row_bytes), "row write")
-        self.data.diff(ids, n=n, out=self._runs)                                           # 4
-        self.data.apply(self._runs, "replica", home)                                       # 5
+        d0, d1 = self.desc_off[r], self.desc_off[r + 1]                                    # 3
+        gdsm.check(lib.gdsm_memcpy_batch(self.data.handle, self.d_desc.ptr + 24 * d0, d1 - d0),
+                   "row writes")
+        if self.fused:                                                                     # 4
+            self.data.diff(ids, n=n, out=self._runs, apply_to="replica", target_ids=home)
+        else:
+            self.data.diff(ids, n=n, out=self._runs)
+            self.data.apply(self._runs, "replica", home)
 
     def run(self, graph: bool = False) -> float:
         """Replays every round once; returns the seconds from the first launch to the end.

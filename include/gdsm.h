@@ -110,10 +110,14 @@ int gdsm_memcpy_h2d(gdsm_ctx* ctx, void* dev, const void* host, uint64_t bytes);
 int gdsm_memcpy_d2h(gdsm_ctx* ctx, void* host, const void* dev, uint64_t bytes);
 /* Asynchronous device-to-device copy on the context stream. */
 int gdsm_memcpy_d2d(gdsm_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+/* n device-to-device copies in one launch on the context stream: desc (device, 3n u64) holds
+ * (dst, src, bytes) per copy; the copies must not overlap each other. E.g. the application
+ * writes of one DSM round replayed at once (gallocy_amd/replay.py). */
+int gdsm_memcpy_batch(gdsm_ctx* ctx, const uint64_t* desc, uint64_t n);
 
 /* HIP graphs: record a launch-bound sequence once and replay it with one launch.
  * - Between gdsm_capture_begin(ctx) and gdsm_capture_end(ctx, &g), the asynchronous calls on ctx
- *   are recorded, not run: gdsm_twin, gdsm_diff, gdsm_apply, gdsm_memcpy_d2d,
+ *   are recorded, not run: gdsm_twin, gdsm_diff, gdsm_apply, gdsm_memcpy_d2d / _batch,
  *   gdsm_coherence_batch_async and the generators.
  * - gdsm_capture_join(ctx, other) adds a second context on the same device. Its asynchronous
  *   calls are recorded into the same graph, ordered after what ctx had recorded when it joined.
@@ -164,6 +168,13 @@ int gdsm_diff(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out);
  * gdsm_runs_total). Replaces the local-home half of gallocy's described release
  * (resources/NUTSHELL.md:59-69): the home applies what the writer diffed. */
 int gdsm_diff_apply(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out, int target);
+/* gdsm_diff_apply with the home copy indexed differently: list entry i (page ids[i] of TWIN and
+ * CURRENT) is applied to page target_ids[i] of arena `target` (device, n entries; out-of-range
+ * ids are reported by the next gdsm_sync and write nothing). For writers whose pages sit at other
+ * indices than their home copies on the same GPU (e.g. several nodes' views of one zone, each
+ * at its own offset, and one home copy of it). */
+int gdsm_diff_apply_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,
+                        int target, const uint32_t* target_ids);
 /* One diff launch for a release with several destinations: arena pages [bounds[d],
  * bounds[d+1]) are diffed into out[d] (G <= 8 streams, each with its own buffers; record i of
  * out[d] is page bounds[d] + i; out[d].n is set). Every stream is exactly what gdsm_diff of that

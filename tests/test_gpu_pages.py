@@ -810,3 +810,67 @@ def test_diff_split_equals_per_range_diffs(variant):
             assert L.gdsm_diff_split(c.handle, b, 9, (GdsmRuns * 9)()) == -22
     finally:
         L.gdsm_tune(b"diff_variant", 0)
+
+
+def test_diff_apply_ids_applies_at_other_indices():
+    """gdsm_diff_apply_ids: list entry i (page ids[i] of TWIN / CURRENT) is applied to page
+    target_ids[i] of REPLICA by the diff kernel itself, the stream being the same as gdsm_diff's;
+    an out-of-range target id writes nothing and is reported by the next sync."""
+    n = 3000
+    rng = np.random.default_rng(77)
+    twin, cur = oracle.gen_pages(n, seed=77, mode=1, ppm=100000)
+    ids = rng.choice(n, 700, replace=False).astype(np.uint32)
+    tids = rng.permutation(n)[:700].astype(np.uint32)
+    with ga.Context(n) as c:
+        base = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+        c.upload("twin", twin)
+        c.upload("current", cur)
+        # the home copy starts as the twin's pages, moved to their target indices
+        rep = base.copy()
+        rep[tids] = twin[ids]
+        c.upload("replica", rep)
+        r = c.diff(c.ids(ids), apply_to="replica", target_ids=c.ids(tids))
+        c.sync()
+        h = r.to_host()
+        ro, data = oracle.diff_pages(twin, cur, ids)
+        assert np.array_equal(h.rec_off, ro) and np.array_equal(h.data[:int(ro[-1])], data)
+        want = rep.copy()
+        want[tids] = cur[ids]
+        assert np.array_equal(c.download("replica"), want)
+        bad = tids.copy()
+        bad[5] = n + 3
+        c.upload("replica", rep)
+        c.diff(c.ids(ids), apply_to="replica", target_ids=c.ids(bad))
+        with pytest.raises(GdsmError) as ei:
+            c.sync()
+        assert ei.value.errno == 22
+        got = c.download("replica")
+        keep = np.ones(700, bool)
+        keep[5] = False
+        want2 = rep.copy()
+        want2[tids[keep]] = cur[ids[keep]]
+        assert np.array_equal(got, want2)
+
+
+def test_memcpy_batch():
+    """gdsm_memcpy_batch: several copies in one launch, 16-B aligned (vector path) and not (byte
+    path), next to bytes that must stay untouched."""
+    import ctypes as C
+    rng = np.random.default_rng(5)
+    with ga.Context(8, arenas=()) as c:
+        src = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+        d_src = c.buffer(src.nbytes).upload(src)
+        d_dst = c.buffer(1 << 16).upload(np.zeros(1 << 16, np.uint8))
+        copies = [(0, 0, 8000), (16384, 32, 4096), (30001, 7, 999), (40000, 50000, 3)]
+        desc = np.array([[d_dst.ptr + d, d_src.ptr + s, b] for d, s, b in copies],
+                        np.uint64).reshape(-1)
+        d_desc = c.buffer(desc.nbytes).upload(desc)
+        assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, d_desc.ptr, len(copies)) == 0
+        c.sync()
+        got = d_dst.download(np.uint8, 1 << 16)
+        want = np.zeros(1 << 16, np.uint8)
+        for d, s, b in copies:
+            want[d:d + b] = src[s:s + b]
+        assert np.array_equal(got, want)
+        assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, None, 1) == -22
+        assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, None, 0) == 0

@@ -10,15 +10,18 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("ndim,nodes,graph", [(64, 1, False), (64, 2, False), (96, 4, False),
-                                              (64, 8, False), (257, 3, False), (1000, 1, False),
-                                              (1000, 2, False), (1000, 4, False), (1000, 8, False),
-                                              (96, 4, True), (1000, 4, True)])
-def test_mmult_replay_end_to_end(ndim, nodes, graph):
+@pytest.mark.parametrize("ndim,nodes,graph,fused", [
+    (64, 1, False, True), (64, 2, False, True), (96, 4, False, True), (64, 8, False, True),
+    (257, 3, False, True), (1000, 1, False, True), (1000, 2, False, True), (1000, 4, False, True),
+    (1000, 8, False, True), (96, 4, True, True), (1000, 4, True, True), (257, 3, False, False),
+    (1000, 4, False, False), (1000, 4, True, False)])
+def test_mmult_replay_end_to_end(ndim, nodes, graph, fused):
     """NDIM = 1000 is BASELINE config 5's size (test/test_mmult.cpp:103-180 uses
     NDIM up to 1021 before the reference heap aborts). graph: every round recorded into one HIP
-    graph (gdsm_capture_*) and replayed by one launch, or issued eagerly (the default)."""
-    R = MmultReplay(ndim=ndim, nodes=nodes, seed=7)
+    graph (gdsm_capture_*) and replayed by one launch, or issued eagerly (the default). fused:
+    the diff kernel applies the runs to the home copies (gdsm_diff_apply_ids), or a separate
+    apply of the stream does."""
+    R = MmultReplay(ndim=ndim, nodes=nodes, seed=7, fused=fused)
     try:
         R.run(graph=graph)
         assert np.array_equal(R.home_copy(), R.final_image())
