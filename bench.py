@@ -594,10 +594,11 @@ def run_mmult(args):
                          "launches_per_round": round(v[1] / rounds, 2)}
     kern_ms = sum(v[0] for v in pd.values()) + sum(v[0] for v in pp.values())
     launches = sum(v[1] for v in pd.values()) + sum(v[1] for v in pp.values())
-    copies = sum(len(R.rows[r]) for r in range(rounds))  # one row write (d2d copy) per row
+    copies = sum(len(R.rows[r]) for r in range(rounds))  # rows written per round
     latency = {"bound": "latency",
                "kernel_launches_per_round": round(launches / rounds, 2),
-               "row_copies_per_round": round(copies / rounds, 2),
+               "copy_launches_per_round": 1,
+               "rows_written_per_round": round(copies / rounds, 2),
                "host_syncs_per_round": 0,
                "kernel_ms_per_round": round(kern_ms / rounds, 5),
                "wall_ms_per_round_profiled": round(dt2 / rounds * 1e3, 5),

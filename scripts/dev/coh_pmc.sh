@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 PMC passes (one per counter group) over coherence pass-C variants (COH_PMC_VARIANTS).
+# rocprofv3 PMC passes (one per counter group) over coherence variants (COH_PMC_VARIANTS);
+# counts per 64 events.
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/cohpmc
@@ -20,8 +21,8 @@ import csv, glob, collections
 for f in sorted(glob.glob("gpurun_out/cohpmc/*/*counter_collection.csv")):
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "coh_apply" in r["Kernel_Name"] or "coh_fold_kernel" in r["Kernel_Name"]:
+        if "coh_stream_kernel" in r["Kernel_Name"] or "coh_fold_kernel" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    # per 512 events (2^28 events per batch)
-    print(f.split("/")[2], {k: round(sum(v) / len(v) / 524288, 1) for k, v in sorted(acc.items())})
+    # per 64 events (2^28 events per batch)
+    print(f.split("/")[2], {k: round(sum(v) / len(v) / 4194304, 2) for k, v in sorted(acc.items())})
 PY
