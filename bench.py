@@ -224,6 +224,21 @@ def read_traffic(pages: int, mode: str, ppm: int, fused: bool):
     return None, None
 
 
+def read_kernel_traffic(prefix: str, workload: dict):
+    """Per-launch HBM bytes of kernel family `prefix` from the newest committed PMC summary of
+    this workload (profiles/*traffic*.json written by scripts/pmc_summary.py with a kernel
+    prefix), else (None, None)."""
+    for p in sorted((ROOT / "profiles").glob("*traffic*.json"), reverse=True):
+        try:
+            j = json.loads(p.read_text())
+        except Exception:  # noqa: BLE001
+            continue
+        if (j.get("workload") == workload and j.get("main_kernel_bytes_per_launch")
+                and str(j.get("main_kernel", "")).startswith(prefix)):
+            return j["main_kernel_bytes_per_launch"], p.name
+    return None, None
+
+
 def read_coh_traffic(dist: str, pages: int, events: int):
     """Per-launch HBM bytes of the coherence fold kernel from the newest committed PMC summary of
     the same batch shape (profiles/*coh_traffic*.json, scripts/coh_traffic.sh), else None."""
@@ -417,6 +432,7 @@ def run_twin(args):
     ok_apply = ctx.diff(cap=1 << 20).total() == 0
     alg = 8192 * n
     achieved = alg / (twin_ms * 1e-3) / 1e9
+    traffic, traffic_src = read_kernel_traffic("gdsm::twin_kernel", {"workload": "twin", "pages": n})
     res = None
     if rank == 0:
         res = {"metric": "pages twinned/sec (4 KiB)", "value": round(world * n * args.steps / dt, 1),
@@ -429,7 +445,8 @@ def run_twin(args):
                           "pages_per_gpu": n, "seed": args.seed},
                "roofline": {"bound": "hbm", "kernel": "gdsm::twin_kernel",
                             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                            "traffic_source": traffic_src,
                             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(twin_ms, 4)},
                "twin_equals_current": bool(ok_full),
                "retwin_by_stream": {
