@@ -62,20 +62,40 @@ __global__ __launch_bounds__(256) void gen_pages_kernel(uint8_t* __restrict__ tw
 }
 
 // ------------------------------------------------------------------------- twin (SPEC §2)
+// TWIN := CURRENT for listed pages: a wave per kP pages per step, every 16-B load of them in
+// flight before the stores (kNT: bit 0 nontemporal loads, bit 1 nontemporal stores).
+template <uint32_t kP, int kNT>
 __global__ __launch_bounds__(256) void twin_kernel(uint8_t* __restrict__ twin,
                                                    const uint8_t* __restrict__ cur,
                                                    const uint32_t* __restrict__ ids, uint64_t n) {
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n;
+  const uint64_t steps = (n + kP - 1) / kP;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < steps;
        i += (uint64_t)gridDim.x * 4) {
-    const uint64_t p = ids ? ids[i] : i;
-    const uint4* src = reinterpret_cast<const uint4*>(cur + p * kPage);
-    uint4* dst = reinterpret_cast<uint4*>(twin + p * kPage);
-    const uint4 a = src[lane], b = src[lane + 64], c = src[lane + 128], d = src[lane + 192];
-    dst[lane] = a;
-    dst[lane + 64] = b;
-    dst[lane + 128] = c;
-    dst[lane + 192] = d;
+    u32x4 v[kP][4];
+    uint64_t pg[kP];
+#pragma unroll
+    for (uint32_t k = 0; k < kP; ++k) {
+      const uint64_t e = i * kP + k;
+      pg[k] = e < n ? (ids ? ids[e] : e) : ~0ull;
+      if (pg[k] == ~0ull) continue;
+      const u32x4* src = reinterpret_cast<const u32x4*>(cur + pg[k] * kPage);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q)
+        v[k][q] = (kNT & 1) ? __builtin_nontemporal_load(src + lane + 64 * q) : src[lane + 64 * q];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kP; ++k) {
+      if (pg[k] == ~0ull) continue;
+      u32x4* dst = reinterpret_cast<u32x4*>(twin + pg[k] * kPage);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        if (kNT & 2)
+          __builtin_nontemporal_store(v[k][q], dst + lane + 64 * q);
+        else
+          dst[lane + 64 * q] = v[k][q];
+      }
+    }
   }
 }
 
@@ -1295,8 +1315,16 @@ static int apply_variant_from_env() {
   return (v >= 0 && v < kApplyVariants) ? v : 0;
 }
 static std::atomic<int> g_apply_variant{apply_variant_from_env()};
+// Twin geometry, gdsm_tune("twin_variant", v): 0 one page per wave step (default), 1 two pages
+// with nontemporal loads, 2 two pages, nontemporal loads and stores, 3 one page, both
+// nontemporal, 4 four pages, nontemporal loads (measurement A/B: scripts/dev/twin_ab.py).
+static std::atomic<int> g_twin_variant{0};
 
 int tune(const char* key, int64_t value) {
+  if (!strcmp(key, "twin_variant") && value >= 0 && value <= 4) {
+    g_twin_variant.store((int)value, std::memory_order_relaxed);
+    return 0;
+  }
   if (!strcmp(key, "diff_variant") && value >= 0 && value <= 8) {
     g_diff_variant.store((int)value, std::memory_order_relaxed);
     return 0;
@@ -1384,8 +1412,10 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
                        hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
   ProfScope ps(prof, GDSM_PROF_TWIN, s);
-  hipLaunchKernelGGL(twin_kernel, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur, ids,
-                     n);
+  const int tv = g_twin_variant.load(std::memory_order_relaxed);
+  auto kern = tv == 1 ? twin_kernel<2, 1> : tv == 2 ? twin_kernel<2, 3> : tv == 3 ? twin_kernel<1, 3>
+            : tv == 4 ? twin_kernel<4, 1> : twin_kernel<1, 0>;
+  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur, ids, n);
   return hipGetLastError();
 }
 
