@@ -1315,16 +1315,9 @@ static int apply_variant_from_env() {
   return (v >= 0 && v < kApplyVariants) ? v : 0;
 }
 static std::atomic<int> g_apply_variant{apply_variant_from_env()};
-// Twin geometry, gdsm_tune("twin_variant", v): 0 one page per wave step (default), 1 two pages
-// with nontemporal loads, 2 two pages, nontemporal loads and stores, 3 one page, both
-// nontemporal, 4 four pages, nontemporal loads (measurement A/B: scripts/dev/twin_ab.py).
-static std::atomic<int> g_twin_variant{0};
+
 
 int tune(const char* key, int64_t value) {
-  if (!strcmp(key, "twin_variant") && value >= 0 && value <= 4) {
-    g_twin_variant.store((int)value, std::memory_order_relaxed);
-    return 0;
-  }
   if (!strcmp(key, "diff_variant") && value >= 0 && value <= 8) {
     g_diff_variant.store((int)value, std::memory_order_relaxed);
     return 0;
@@ -1412,10 +1405,10 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
                        hipStream_t s, Prof* prof) {
   if (n == 0) return hipSuccess;
   ProfScope ps(prof, GDSM_PROF_TWIN, s);
-  const int tv = g_twin_variant.load(std::memory_order_relaxed);
-  auto kern = tv == 1 ? twin_kernel<2, 1> : tv == 2 ? twin_kernel<2, 3> : tv == 3 ? twin_kernel<1, 3>
-            : tv == 4 ? twin_kernel<4, 1> : twin_kernel<1, 0>;
-  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur, ids, n);
+  // one page per wave step, cached loads and stores: two or four pages per step and
+  // nontemporal loads and/or stores measured 0.3-4.5 % slower in one process (round 4)
+  hipLaunchKernelGGL(twin_kernel<1, 0>, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur,
+                     ids, n);
   return hipGetLastError();
 }
 
