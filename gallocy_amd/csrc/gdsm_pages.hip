@@ -1407,8 +1407,8 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
   ProfScope ps(prof, GDSM_PROF_TWIN, s);
   // one page per wave step, cached loads and stores: two or four pages per step and
   // nontemporal loads and/or stores measured 0.3-4.5 % slower in one process (round 4)
-  hipLaunchKernelGGL(twin_kernel<1, 0>, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur,
-                     ids, n);
+  auto kern = twin_kernel<1, 0>;
+  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur, ids, n);
   return hipGetLastError();
 }
 
