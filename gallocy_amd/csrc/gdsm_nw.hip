@@ -11,16 +11,24 @@
 // Fill (nw_fill_kernel): one 16-wave workgroup per pair. Rows are cut into strips of 256; a strip
 // belongs to one wave, 4 consecutive rows per lane. Lane l computes column x = t - l + 1 at step
 // t, so the value from the row above (lane l-1's bottom row one step earlier) arrives by one DPP
-// wave_shr:1 of a packed (score << 8 | b byte) word: no LDS traffic inside a strip. Strip s+1
+// wave_shr:1, and the byte of b by one LDS byte read (b is staged in LDS). Strip s+1
 // follows strip s two 64-step phases behind (one workgroup barrier per phase); the bottom row
 // of a strip reaches the next wave through a 256-column LDS ring (or, from wave 15 to wave 0 of
-// the next group of 16 strips, through a double-buffered row in global memory). No MFMA: the
+// the next group of 16 strips, through the strip's bottom row in global memory). No MFMA: the
 // recurrence is max/add on int32, not a contraction.
 //
-// Traceback bits: per cell two bits, nd = "not diag" (dg < max(lf, up)) and u = "up beats left"
-// (up > left, only read when nd). A lane accumulates them for its 4 rows over 16 steps into
-// one 16-byte record; record (strip, block, lane) lives at ((strip * NB + block) * 64 + lane),
-// so the 64 lanes of a wave store 1 KiB contiguously.
+// Scores are kept as U = H + y + x, which makes every border 0 and a cell one compare, one
+// add-with-carry and one max3: U = max3(U[y-1][x-1] + 2 + (a==b), U[y][x-1], U[y-1][x]). The three
+// candidates are H's candidates shifted by the same y + x, so every comparison (and the traceback)
+// is the reference's.
+//
+// No traceback leaves the fill. It stores, per strip, the lanes' state every 128 steps (a
+// checkpoint: 4 left values, diag, pass; 24 B per lane) and the strip's bottom row (the next
+// strip's input, one word per column). The trace recomputes one 128-step region of a strip from
+// its checkpoint when the path enters it, with the traceback bits this time: two bits per cell,
+// nd = "not diag" (dg < max(lf, up)) and u = "up beats left" (up > left, only read when nd), a
+// 16-byte record per lane per 16 steps, into LDS. The path crosses ~3 regions of a strip, so the
+// trace recomputes ~1.5 % of the matrix where the fill used to write 2 bits for every cell.
 //
 // Trace (nw_trace_kernel): one wave per pair walks the path with wave-uniform (scalar) state,
 // reading directions out of a 64-record window held in VGPRs (v_readlane with a uniform lane),
@@ -38,77 +46,119 @@ constexpr uint32_t kPhase = 64;           // steps per phase (between barriers)
 constexpr uint32_t kLag = 2;              // phases between consecutive strips
 constexpr uint32_t kRing = 256;           // ring slots per wave (>= 193 live columns)
 constexpr uint32_t kBlk = 16;             // steps per traceback record
+constexpr uint32_t kCk = 128;             // steps per checkpoint = per recomputed region
+constexpr uint32_t kCkBlk = kCk / kBlk;   // records per lane per region
+constexpr uint32_t kCkBytes = 64 * 24;    // one checkpoint: 64 x (left[4] | diag, pass)
 
 __device__ __forceinline__ uint32_t wave_shr1_or(uint32_t old, uint32_t v) {
   // Lane l gets lane l-1's v; lane 0 keeps `old` (bound_ctrl off).
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-__device__ __forceinline__ uint32_t pack(int32_t score, uint32_t byte) {
-  return ((uint32_t)score << 8) | byte;
+__device__ __forceinline__ uint32_t wave_rol1(uint32_t v) {
+  // Lane l gets lane l+1's v, lane 63 gets lane 0's.
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x134, 0xF, 0xF, false);
 }
 
-// Scores are kept minus one (H - 1): then lf and up of the recurrence are the stored values,
-// dg = stored diag + 1 + (a == b) is one add-with-carry, mx = max3(dg, lf, up), and both
-// traceback bits are sign bits shifted in by v_alignbit (nd = dg < mx, u = lf < up).
 struct Strip {
   uint32_t a[kRows];
-  int32_t left[kRows];  // H[y][x-1] - 1
-  int32_t diag;         // H[ytop-1][x-1] - 1
-  uint32_t pass;        // (H[ybottom][x] - 1) << 8 | b byte
+  int32_t left[kRows];  // U[y][x-1]
+  int32_t diag;         // U[ytop-1][x-1]
+  int32_t pass;         // U[ybottom][x]: the row above for lane l+1 one step later
 };
 
 __device__ __forceinline__ uint32_t shift_in_sign(uint32_t acc, int32_t v) {
   return __builtin_amdgcn_alignbit(acc, (uint32_t)v, 31);  // (acc << 1) | (v < 0)
 }
 
-// One block of 16 steps [t0, t0 + 16) of a strip. fv: lanes 0..15 hold the packed words lane 0
-// consumes at steps t0..t0+15. Returns (in lanes 0..15) the packed bottom words of lane 63.
-template <bool kMasked>
-__device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t fv, uint32_t t0, uint32_t n2,
-                                               uint32_t lane, uint4* rec) {
-  uint32_t ndA = 0, ndB = 0, uA = 0, uB = 0, wv = 0;
+// Pair geometry shared by the fill and the trace (max_len fixes the workspace strides).
+__host__ __device__ inline uint32_t step_blocks(uint32_t n2) { return (n2 + 63 + kBlk - 1) / kBlk; }
+struct Geo {
+  uint32_t CK;   // checkpoints per strip slot
+  uint64_t RS;   // words per stored bottom row
+  uint64_t ck_bytes, row_bytes, mv_bytes;
+  __host__ __device__ explicit Geo(uint32_t max_len) {
+    const uint64_t S = max_len ? (max_len + kStrip - 1) / kStrip : 1;
+    CK = (step_blocks(max_len) * kBlk + kCk - 1) / kCk;
+    RS = (uint64_t)max_len + 64;
+    ck_bytes = S * CK * kCkBytes;
+    row_bytes = (S * RS * 4 + 255) & ~255ull;
+    mv_bytes = (2 * (uint64_t)max_len + 64 + 255) & ~255ull;
+  }
+  __host__ __device__ uint64_t per_pair() const { return ck_bytes + row_bytes + mv_bytes; }
+};
+
+// One block of 16 steps [t0, t0 + 16) of a strip. R: lanes 0..15 hold the words lane 0 consumes
+// at steps t0..t0+15 (the row above the strip); bx[x] is b's byte at column x (1..n2). One
+// register carries both ways: each step lane 63's new bottom word goes in at lane 63 and R
+// rotates down a lane, so lane 0 meets the next feed word and, after the block, lanes 47..62 hold
+// the bottom words of steps t0..t0+15 (columns t0-62 .. t0-47). With kRec the traceback bits of
+// the lane's 4 x 16 cells go to *rec.
+template <bool kMasked, bool kRec>
+__device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t R, const uint8_t* bx,
+                                               uint32_t t0, uint32_t n2, uint32_t lane,
+                                               uint4* rec) {
+  uint32_t ndA = 0, ndB = 0, uA = 0, uB = 0;
+  const int32_t x0 = (int32_t)(t0 + 1) - (int32_t)lane;  // this lane's column at step t0
+  const bool top = lane == 63;
 #pragma unroll
   for (uint32_t k = 0; k < kBlk; ++k) {
-    const uint32_t feed = (uint32_t)__builtin_amdgcn_readlane((int)fv, (int)k);
-    const uint32_t in = wave_shr1_or(feed, st.pass);
-    const int32_t up_in = (int32_t)in >> 8;
-    const uint32_t bb = in & 0xFFu;
+    const int32_t x = x0 + (int32_t)k;
     bool act = true;
+    uint32_t bb;
     if (kMasked) {
-      const int32_t x = (int32_t)(t0 + k) - (int32_t)lane + 1;
       act = x >= 1 && x <= (int32_t)n2;
+      bb = bx[min(max(x, 1), (int32_t)n2)];
+    } else {
+      bb = bx[x];
     }
+    const int32_t up_in = (int32_t)wave_shr1_or(R, (uint32_t)st.pass);
     int32_t up = up_in, dgv = st.diag;
     uint32_t* acc_nd[2] = {&ndA, &ndB};
     uint32_t* acc_u[2] = {&uA, &uB};
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
       const int32_t lf = st.left[r];
-      const int32_t d = dgv + 1 + (st.a[r] == bb ? 1 : 0);
+      const int32_t d = dgv + 2 + (st.a[r] == bb ? 1 : 0);
       const int32_t mx = max(max(d, lf), up);
-      *acc_nd[r >> 1] = shift_in_sign(*acc_nd[r >> 1], d - mx);
-      *acc_u[r >> 1] = shift_in_sign(*acc_u[r >> 1], lf - up);
+      if (kRec) {
+        *acc_nd[r >> 1] = shift_in_sign(*acc_nd[r >> 1], d - mx);
+        *acc_u[r >> 1] = shift_in_sign(*acc_u[r >> 1], lf - up);
+      }
       dgv = lf;
-      up = mx - 1;
-      if (kMasked) st.left[r] = act ? up : lf;
-      else st.left[r] = up;
+      up = mx;
+      if (kMasked) st.left[r] = act ? mx : lf;
+      else st.left[r] = mx;
     }
     if (kMasked) st.diag = act ? up_in : st.diag;
     else st.diag = up_in;
-    st.pass = pack(up, bb);
-    const uint32_t bot = (uint32_t)__builtin_amdgcn_readlane((int)st.pass, 63);
-    wv = (lane == k) ? bot : wv;
+    st.pass = up;
+    R = wave_rol1(top ? (uint32_t)up : R);
   }
-  *rec = make_uint4(ndA, ndB, uA, uB);
-  return wv;
+  if (kRec) *rec = make_uint4(ndA, ndB, uA, uB);
+  return R;
 }
 
+__device__ __forceinline__ void strip_start(Strip& st, const uint8_t* a, uint64_t ao, uint32_t n1,
+                                            uint32_t s, uint32_t lane) {
+  const uint32_t y0 = s * kStrip + lane * kRows + 1;
+#pragma unroll
+  for (uint32_t r = 0; r < kRows; ++r) {
+    st.a[r] = (y0 + r <= n1) ? a[ao + y0 + r - 1] : 0u;
+    st.left[r] = 0;
+  }
+  st.diag = 0;
+  st.pass = 0;
+}
+
+constexpr uint32_t kBLds = 48 * 1024 - 16;  // b staged in LDS up to this length (64 KiB in all)
+extern __shared__ uint8_t nw_dyn_lds[];
+
+template <bool kLdsB>
 __global__ __launch_bounds__(1024) void nw_fill_kernel(
     const uint8_t* __restrict__ a, const uint64_t* __restrict__ a_off,
     const uint8_t* __restrict__ b, const uint64_t* __restrict__ b_off, uint64_t first_pair,
-    uint32_t max_len, uint32_t NB, uint64_t slot_recs, uint4* __restrict__ tb,
-    uint32_t* __restrict__ rowbuf, uint32_t* __restrict__ err) {
+    uint32_t max_len, uint8_t* __restrict__ ws, uint32_t* __restrict__ err) {
   __shared__ uint32_t ring[kWaves][kRing];
   const uint64_t pair = first_pair + blockIdx.x;
   const uint64_t ao = a_off[pair], bo = b_off[pair];
@@ -120,16 +170,23 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
   const uint32_t n1 = (uint32_t)l1, n2 = (uint32_t)l2;
   if (!n1 || !n2) return;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint8_t* bx = b + bo - 1;
+  if (kLdsB) {
+    for (uint32_t i = threadIdx.x; i < n2; i += 64 * kWaves) nw_dyn_lds[i + 1] = bx[i + 1];
+    bx = nw_dyn_lds;
+    __syncthreads();
+  }
   const uint32_t S = (n1 + kStrip - 1) / kStrip;
-  const uint32_t nblk = (n2 + 63 + kBlk - 1) / kBlk;           // step blocks per strip
+  const uint32_t nblk = step_blocks(n2);                        // step blocks per strip
   const uint32_t T = (nblk * kBlk + kPhase - 1) / kPhase;      // phases per strip
   // Group g of 16 strips starts at phase g * TT; strip 16g + w at g * TT + kLag * w. TT lets wave
   // 15 finish a strip before wave 0 of the next group reads its bottom row, and a wave's ring
   // outlive its previous reader.
   const uint32_t TT = T + kLag * (kWaves - 1);
   const uint32_t Q = ((S - 1) / kWaves) * TT + kLag * ((S - 1) % kWaves) + T;
-  uint4* tbp = tb + blockIdx.x * slot_recs;
-  uint32_t* rb = rowbuf + (uint64_t)blockIdx.x * 2 * (max_len + 64);
+  const Geo geo(max_len);
+  uint8_t* ck = ws + blockIdx.x * geo.per_pair();
+  uint32_t* rows = reinterpret_cast<uint32_t*>(ck + geo.ck_bytes);
   const uint32_t* ring_in = ring[(w + kWaves - 1) % kWaves];
   uint32_t* ring_out = ring[w];
 
@@ -140,43 +197,37 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
       const uint32_t g = (uint32_t)rel / TT, lp = (uint32_t)rel - g * TT;
       const uint32_t s = g * kWaves + w;
       if (s < S && lp < T) {
-        if (lp == 0) {  // strip start: rows y0 .. y0+3 of this lane
-          const uint32_t y0 = s * kStrip + lane * kRows + 1;
-#pragma unroll
-          for (uint32_t r = 0; r < kRows; ++r) {
-            st.a[r] = (y0 + r <= n1) ? a[ao + y0 + r - 1] : 0u;
-            st.left[r] = -(int32_t)(y0 + r) - 1;
-          }
-          st.diag = -(int32_t)(y0 - 1) - 1;
-          st.pass = 0;
-        }
+        if (lp == 0) strip_start(st, a, ao, n1, s, lane);
         for (uint32_t bi = 0; bi < kPhase / kBlk; ++bi) {
           const uint32_t t0 = lp * kPhase + bi * kBlk;
           if (t0 >= nblk * kBlk) break;
+          if ((t0 & (kCk - 1)) == 0) {  // checkpoint: the state before step t0
+            uint8_t* c = ck + ((uint64_t)s * geo.CK + t0 / kCk) * kCkBytes;
+            reinterpret_cast<int4*>(c)[lane] =
+                make_int4(st.left[0], st.left[1], st.left[2], st.left[3]);
+            reinterpret_cast<int2*>(c + 64 * 16)[lane] = make_int2(st.diag, st.pass);
+          }
           // Lane 0's feed for steps t0 + i: column x = t0 + 1 + i of the row above the strip.
           const uint32_t x = t0 + 1 + (lane & 15);
           uint32_t fv = 0;
           if (s == 0) {
-            fv = (x <= n2) ? pack(-(int32_t)x - 1, b[bo + x - 1]) : 0u;
+            fv = 0;
           } else if (w == 0) {
-            const uint32_t* src = rb + ((g - 1) & 1) * (max_len + 64);
+            const uint32_t* src = rows + (uint64_t)(s - 1) * geo.RS;
             fv = (x <= n2) ? __hip_atomic_load(src + x - 1, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)
                            : 0u;
           } else {
             fv = ring_in[(t0 + (lane & 15)) & (kRing - 1)];
           }
-          uint4 rec;
           const bool masked = t0 < 64 || t0 + kBlk > n2;
-          const uint32_t wv = masked ? fill_block<true>(st, fv, t0, n2, lane, &rec)
-                                     : fill_block<false>(st, fv, t0, n2, lane, &rec);
-          tbp[((uint64_t)s * NB + t0 / kBlk) * 64 + lane] = rec;
-          // Lane 63's bottom words at steps t0..t0+15 are columns t0-62 .. t0-47.
-          if (lane < 16) {
-            ring_out[(t0 + lane - 63) & (kRing - 1)] = wv;
-            const int32_t xo = (int32_t)(t0 + lane) - 62;
-            if (w == kWaves - 1 && s + 1 < S && xo >= 1 && xo <= (int32_t)n2)
-              rb[(g & 1) * (max_len + 64) + xo - 1] = wv;
+          const uint32_t R = masked ? fill_block<true, false>(st, fv, bx, t0, n2, lane, nullptr)
+                                    : fill_block<false, false>(st, fv, bx, t0, n2, lane, nullptr);
+          // Lanes 47..62 of R: lane 63's bottom words at steps t0..t0+15, columns t0-62 ..
+          if (lane >= 47 && lane < 63) {
+            const int32_t xo = (int32_t)(t0 + lane) - 109;
+            ring_out[(uint32_t)(xo - 1) & (kRing - 1)] = R;
+            if (s + 1 < S && xo >= 1 && xo <= (int32_t)n2) rows[(uint64_t)s * geo.RS + xo - 1] = R;
           }
         }
       }
@@ -188,21 +239,26 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
 __global__ __launch_bounds__(64) void nw_trace_kernel(
     const uint8_t* __restrict__ a, const uint64_t* __restrict__ a_off,
     const uint8_t* __restrict__ b, const uint64_t* __restrict__ b_off, uint64_t first_pair,
-    uint32_t max_len, uint32_t NB, uint64_t slot_recs, const uint4* __restrict__ tb,
-    uint8_t* __restrict__ mv, uint8_t* __restrict__ out1, uint8_t* __restrict__ out2,
-    uint64_t* __restrict__ out_len) {
+    uint32_t max_len, const uint8_t* __restrict__ ws, uint8_t* __restrict__ mv_ws,
+    uint8_t* __restrict__ out1, uint8_t* __restrict__ out2, uint64_t* __restrict__ out_len) {
+  __shared__ uint4 lrec[kCkBlk][64];
   const uint64_t pair = first_pair + blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint64_t ao = a_off[pair], bo = b_off[pair];
   const uint64_t l1 = a_off[pair + 1] - ao, l2 = b_off[pair + 1] - bo;
   if (l1 > max_len || l2 > max_len) return;  // flagged by the fill kernel
   const uint32_t n1 = (uint32_t)l1, n2 = (uint32_t)l2;
-  const uint4* tbp = tb + blockIdx.x * slot_recs;
-  uint8_t* mvp = mv + (uint64_t)blockIdx.x * (2 * (uint64_t)max_len + 64);
+  const uint32_t nblk = step_blocks(n2);
+  const uint8_t* bx = b + bo - 1;
+  const Geo geo(max_len);
+  const uint8_t* ck = ws + blockIdx.x * geo.per_pair();
+  const uint32_t* rows = reinterpret_cast<const uint32_t*>(ck + geo.ck_bytes);
+  uint8_t* mvp = mv_ws + blockIdx.x * geo.per_pair() + geo.ck_bytes + geo.row_bytes;
 
   // ---- walk (n1, n2) -> (0, 0); codes 1 diag, 2 left, 3 up, in path order from the end
   uint32_t y = n1, x = n2, L = 0;
-  int32_t ws = -1, wl0 = 0, wb0 = 0;
+  int32_t rs = -1, rq = 0;             // the region in LDS: strip rs, steps [rq*kCk, +kCk)
+  int32_t ws_ = -1, wl0 = 0, wb0 = 0;  // the record window in VGPRs
   uint4 rec = make_uint4(0, 0, 0, 0);
   uint32_t mvreg = 0;
   while (y | x) {
@@ -218,13 +274,40 @@ __global__ __launch_bounds__(64) void nw_trace_kernel(
       const uint32_t t = x - 1 + (uint32_t)l;
       const int32_t blk = (int32_t)(t / kBlk);
       const uint32_t k = t & (kBlk - 1);
-      if (s != ws || l < wl0 || blk < wb0) {  // the path only moves to smaller l and blk
-        ws = s;
+      if (s != rs || blk < rq * (int32_t)kCkBlk) {  // the path only moves to smaller t, s
+        rs = s;
+        rq = blk / (int32_t)kCkBlk;
+        const uint8_t* c = ck + ((uint64_t)s * geo.CK + (uint32_t)rq) * kCkBytes;
+        const int4 lv = reinterpret_cast<const int4*>(c)[lane];
+        const int2 dp = reinterpret_cast<const int2*>(c + 64 * 16)[lane];
+        Strip st;
+        strip_start(st, a, ao, n1, (uint32_t)s, lane);
+        st.left[0] = lv.x;
+        st.left[1] = lv.y;
+        st.left[2] = lv.z;
+        st.left[3] = lv.w;
+        st.diag = dp.x;
+        st.pass = dp.y;
+        for (uint32_t bi = 0; bi < kCkBlk; ++bi) {
+          const uint32_t t0 = (uint32_t)rq * kCk + bi * kBlk;
+          if (t0 >= nblk * kBlk) break;
+          const uint32_t xf = t0 + 1 + (lane & 15);
+          uint32_t fv = 0;
+          if (s > 0 && xf <= n2) fv = rows[(uint64_t)(s - 1) * geo.RS + xf - 1];
+          uint4 rr;
+          if (t0 < 64 || t0 + kBlk > n2) fill_block<true, true>(st, fv, bx, t0, n2, lane, &rr);
+          else fill_block<false, true>(st, fv, bx, t0, n2, lane, &rr);
+          lrec[bi][lane] = rr;
+        }
+        __syncthreads();
+        ws_ = -1;
+      }
+      if (s != ws_ || l < wl0 || blk < wb0) {  // the path only moves to smaller l and blk
+        ws_ = s;
         wl0 = l - 15;
-        wb0 = blk - 3;
+        wb0 = max(blk - 3, rq * (int32_t)kCkBlk);
         const int32_t il = wl0 + (int32_t)(lane >> 2), ib = wb0 + (int32_t)(lane & 3);
-        rec = (il >= 0 && ib >= 0) ? tbp[((uint64_t)s * NB + (uint32_t)ib) * 64 + (uint32_t)il]
-                                   : make_uint4(0, 0, 0, 0);
+        rec = il >= 0 ? lrec[ib - rq * (int32_t)kCkBlk][il] : make_uint4(0, 0, 0, 0);
       }
       const int idx = (l - wl0) * 4 + (blk - wb0);
       const uint32_t ndw = (uint32_t)__builtin_amdgcn_readlane((int)(r < 2 ? rec.x : rec.y), idx);
@@ -266,16 +349,7 @@ __global__ __launch_bounds__(64) void nw_trace_kernel(
 
 }  // namespace
 
-uint64_t nw_slot_recs(uint32_t max_len) {
-  const uint64_t S = (max_len + kStrip - 1) / kStrip;
-  const uint64_t NB = (max_len + 63 + kBlk - 1) / kBlk;
-  return (S ? S : 1) * NB * 64;
-}
-
-uint64_t nw_pair_ws_bytes(uint32_t max_len) {
-  return nw_slot_recs(max_len) * 16 + 2 * ((uint64_t)max_len + 64) * 4 +
-         (2 * (uint64_t)max_len + 64);
-}
+uint64_t nw_pair_ws_bytes(uint32_t max_len) { return Geo(max_len).per_pair(); }
 
 hipError_t launch_nw(const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
                      const uint64_t* b_off, uint64_t n, uint32_t max_len, uint8_t* out1,
@@ -285,24 +359,21 @@ hipError_t launch_nw(const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
   const uint64_t per = nw_pair_ws_bytes(max_len);
   const uint64_t chunk = ws_bytes / per;
   if (!chunk) return hipErrorInvalidValue;
-  const uint64_t recs = nw_slot_recs(max_len);
-  const uint32_t NB = (uint32_t)((max_len + 63 + kBlk - 1) / kBlk);
   for (uint64_t first = 0; first < n; first += chunk) {
     const uint64_t cnt = n - first < chunk ? n - first : chunk;
-    uint4* tb = reinterpret_cast<uint4*>(ws);
-    uint32_t* rowbuf = reinterpret_cast<uint32_t*>(ws + cnt * recs * 16);
-    uint8_t* mv = reinterpret_cast<uint8_t*>(rowbuf + cnt * 2 * ((uint64_t)max_len + 64));
     {
       ProfScope ps(prof, GDSM_PROF_NW_FILL, s);
-      hipLaunchKernelGGL(nw_fill_kernel, dim3((uint32_t)cnt), dim3(64 * kWaves), 0, s, a, a_off,
-                         b, b_off, first, max_len, NB, recs, tb, rowbuf, err);
+      const bool lds_b = max_len <= kBLds;
+      auto kern = lds_b ? nw_fill_kernel<true> : nw_fill_kernel<false>;
+      hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(64 * kWaves), lds_b ? max_len + 4 : 0,
+                         s, a, a_off, b, b_off, first, max_len, ws, err);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     {
       ProfScope ps(prof, GDSM_PROF_NW_TRACE, s);
       hipLaunchKernelGGL(nw_trace_kernel, dim3((uint32_t)cnt), dim3(64), 0, s, a, a_off, b,
-                         b_off, first, max_len, NB, recs, tb, mv, out1, out2, out_len);
+                         b_off, first, max_len, ws, ws, out1, out2, out_len);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -48,9 +48,11 @@ def test_reference_produced_vectors(ctx, golden):
 
 # Shapes around every boundary of the kernel: strips (256 rows), the 16-strip group whose last
 # strip hands over through global memory (n1 > 4096), the lane pipeline (64 columns), the
-# 16-step records and the 64-step phases.
+# 16-step records, the 64-step phases and the 128-step regions the trace recomputes from
+# checkpoints (a path through many regions: long and thin both ways).
 SHAPES = [(1, 1), (1, 300), (300, 1), (63, 64), (64, 65), (255, 17), (256, 256), (257, 1000),
-          (1000, 257), (700, 700), (4096, 33), (4097, 80), (8500, 40), (50, 5000)]
+          (1000, 257), (700, 700), (4096, 33), (4097, 80), (8500, 40), (50, 5000),
+          (128, 65), (129, 66), (200, 193), (3000, 2900), (16, 3000)]
 
 
 @pytest.mark.parametrize("alphabet", [256, 4, 2])
@@ -82,6 +84,17 @@ def test_pages_with_sparse_writes_and_shifts(ctx):
         assert g == oracle.nw_diff(a, b)
     for (a, b), (o1, o2) in zip(pairs[:6], got[:6]):
         assert o1 == a and o2 == b  # equal-length substitutions align gap-free
+
+
+def test_long_strings_read_b_from_global(ctx):
+    """Beyond 48 KiB the fill reads b from global memory instead of LDS; the whole batch takes
+    that kernel (max_len decides), short pairs included."""
+    rng = np.random.default_rng(11)
+    pairs = [(_rand(rng, 60, 4), _rand(rng, 50000, 4)), (_rand(rng, 50000, 4), _rand(rng, 70, 4)),
+             (_rand(rng, 700, 4), _rand(rng, 650, 4))]
+    got = ctx.nw_diff_batch(pairs)
+    for (a, b), g in zip(pairs, got):
+        assert g == oracle.nw_diff(a, b), (len(a), len(b))
 
 
 def test_max_len_is_enforced(ctx):
