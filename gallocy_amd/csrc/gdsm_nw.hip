@@ -40,7 +40,10 @@ namespace gdsm {
 namespace {
 
 constexpr uint32_t kRows = 4;             // DP rows per lane
-constexpr uint32_t kWaves = 16;           // waves per fill workgroup
+#ifndef GDSM_NW_WAVES
+#define GDSM_NW_WAVES 16
+#endif
+constexpr uint32_t kWaves = GDSM_NW_WAVES;  // waves per fill workgroup
 constexpr uint32_t kStrip = 64 * kRows;   // rows per strip
 constexpr uint32_t kPhase = 64;           // steps per phase (between barriers)
 constexpr uint32_t kLag = 2;              // phases between consecutive strips
@@ -88,12 +91,13 @@ struct Geo {
   __host__ __device__ uint64_t per_pair() const { return ck_bytes + row_bytes + mv_bytes; }
 };
 
-// One block of 16 steps [t0, t0 + 16) of a strip. R: lanes 0..15 hold the words lane 0 consumes
-// at steps t0..t0+15 (the row above the strip); bx[x] is b's byte at column x (1..n2). One
-// register carries both ways: each step lane 63's new bottom word goes in at lane 63 and R
-// rotates down a lane, so lane 0 meets the next feed word and, after the block, lanes 47..62 hold
-// the bottom words of steps t0..t0+15 (columns t0-62 .. t0-47). With kRec the traceback bits of
-// the lane's 4 x 16 cells go to *rec.
+// One block of 16 steps [t0, t0 + 16) of a strip. R: lane i holds the word lane 0 consumes at
+// step t0 + i (the row above the strip, up to 64 steps ahead); bx[x] is b's byte at column x
+// (1..n2). One register carries both ways: each step R rotates down a lane (lane 0 meets the next
+// feed word, the consumed one wraps to lane 63) and lane 63 takes the new bottom word, so after
+// the block lanes 48..63 hold the bottom words of steps t0..t0+15 (columns t0-62 .. t0-47) and
+// lanes 0..47 the feed words of the next 48 steps. With kRec the traceback bits of the lane's
+// 4 x 16 cells go to *rec.
 template <bool kMasked, bool kRec>
 __device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t R, const uint8_t* bx,
                                                uint32_t t0, uint32_t n2, uint32_t lane,
@@ -113,17 +117,18 @@ __device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t R, const uint
       bb = bx[x];
     }
     const int32_t up_in = (int32_t)wave_shr1_or(R, (uint32_t)st.pass);
+    R = wave_rol1(R);  // lane 0: the next feed word; lane 63: free (this step's feed, consumed)
     int32_t up = up_in, dgv = st.diag;
-    uint32_t* acc_nd[2] = {&ndA, &ndB};
-    uint32_t* acc_u[2] = {&uA, &uB};
+    uint32_t* acc_nd = k < kBlk / 2 ? &ndA : &ndB;
+    uint32_t* acc_u = k < kBlk / 2 ? &uA : &uB;
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
       const int32_t lf = st.left[r];
       const int32_t d = dgv + 2 + (st.a[r] == bb ? 1 : 0);
       const int32_t mx = max(max(d, lf), up);
       if (kRec) {
-        *acc_nd[r >> 1] = shift_in_sign(*acc_nd[r >> 1], d - mx);
-        *acc_u[r >> 1] = shift_in_sign(*acc_u[r >> 1], lf - up);
+        *acc_nd = shift_in_sign(*acc_nd, d - mx);
+        *acc_u = shift_in_sign(*acc_u, lf - up);
       }
       dgv = lf;
       up = mx;
@@ -133,7 +138,7 @@ __device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t R, const uint
     if (kMasked) st.diag = act ? up_in : st.diag;
     else st.diag = up_in;
     st.pass = up;
-    R = wave_rol1(top ? (uint32_t)up : R);
+    R = top ? (uint32_t)up : R;
   }
   if (kRec) *rec = make_uint4(ndA, ndB, uA, uB);
   return R;
@@ -155,7 +160,7 @@ constexpr uint32_t kBLds = 48 * 1024 - 16;  // b staged in LDS up to this length
 extern __shared__ uint8_t nw_dyn_lds[];
 
 template <bool kLdsB>
-__global__ __launch_bounds__(1024) void nw_fill_kernel(
+__global__ __launch_bounds__(64 * kWaves) void nw_fill_kernel(
     const uint8_t* __restrict__ a, const uint64_t* __restrict__ a_off,
     const uint8_t* __restrict__ b, const uint64_t* __restrict__ b_off, uint64_t first_pair,
     uint32_t max_len, uint8_t* __restrict__ ws, uint32_t* __restrict__ err) {
@@ -198,6 +203,19 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
       const uint32_t s = g * kWaves + w;
       if (s < S && lp < T) {
         if (lp == 0) strip_start(st, a, ao, n1, s, lane);
+        // The phase's 64 feed words, one per lane: column x = 64 lp + 1 + lane of the row above.
+        const uint32_t x = lp * kPhase + 1 + lane;
+        uint32_t R = 0;
+        if (s == 0) {
+          R = 0;
+        } else if (w == 0) {
+          const uint32_t* src = rows + (uint64_t)(s - 1) * geo.RS;
+          R = (x <= n2) ? __hip_atomic_load(src + x - 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : 0u;
+        } else {
+          R = ring_in[(x - 1) & (kRing - 1)];
+        }
         for (uint32_t bi = 0; bi < kPhase / kBlk; ++bi) {
           const uint32_t t0 = lp * kPhase + bi * kBlk;
           if (t0 >= nblk * kBlk) break;
@@ -207,25 +225,12 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
                 make_int4(st.left[0], st.left[1], st.left[2], st.left[3]);
             reinterpret_cast<int2*>(c + 64 * 16)[lane] = make_int2(st.diag, st.pass);
           }
-          // Lane 0's feed for steps t0 + i: column x = t0 + 1 + i of the row above the strip.
-          const uint32_t x = t0 + 1 + (lane & 15);
-          uint32_t fv = 0;
-          if (s == 0) {
-            fv = 0;
-          } else if (w == 0) {
-            const uint32_t* src = rows + (uint64_t)(s - 1) * geo.RS;
-            fv = (x <= n2) ? __hip_atomic_load(src + x - 1, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                           : 0u;
-          } else {
-            fv = ring_in[(t0 + (lane & 15)) & (kRing - 1)];
-          }
           const bool masked = t0 < 64 || t0 + kBlk > n2;
-          const uint32_t R = masked ? fill_block<true, false>(st, fv, bx, t0, n2, lane, nullptr)
-                                    : fill_block<false, false>(st, fv, bx, t0, n2, lane, nullptr);
-          // Lanes 47..62 of R: lane 63's bottom words at steps t0..t0+15, columns t0-62 ..
-          if (lane >= 47 && lane < 63) {
-            const int32_t xo = (int32_t)(t0 + lane) - 109;
+          R = masked ? fill_block<true, false>(st, R, bx, t0, n2, lane, nullptr)
+                     : fill_block<false, false>(st, R, bx, t0, n2, lane, nullptr);
+          // Lanes 48..63 of R: lane 63's bottom words at steps t0..t0+15, columns t0-62 ..
+          if (lane >= 48) {
+            const int32_t xo = (int32_t)(t0 + lane) - 110;
             ring_out[(uint32_t)(xo - 1) & (kRing - 1)] = R;
             if (s + 1 < S && xo >= 1 && xo <= (int32_t)n2) rows[(uint64_t)s * geo.RS + xo - 1] = R;
           }
@@ -236,6 +241,7 @@ __global__ __launch_bounds__(1024) void nw_fill_kernel(
   }
 }
 
+template <bool kLdsB>
 __global__ __launch_bounds__(64) void nw_trace_kernel(
     const uint8_t* __restrict__ a, const uint64_t* __restrict__ a_off,
     const uint8_t* __restrict__ b, const uint64_t* __restrict__ b_off, uint64_t first_pair,
@@ -250,76 +256,120 @@ __global__ __launch_bounds__(64) void nw_trace_kernel(
   const uint32_t n1 = (uint32_t)l1, n2 = (uint32_t)l2;
   const uint32_t nblk = step_blocks(n2);
   const uint8_t* bx = b + bo - 1;
+  if (kLdsB) {
+#pragma unroll 16
+    for (uint32_t i = lane; i < n2; i += 64) nw_dyn_lds[i + 1] = bx[i + 1];
+    bx = nw_dyn_lds;
+    __syncthreads();
+  }
   const Geo geo(max_len);
   const uint8_t* ck = ws + blockIdx.x * geo.per_pair();
   const uint32_t* rows = reinterpret_cast<const uint32_t*>(ck + geo.ck_bytes);
   uint8_t* mvp = mv_ws + blockIdx.x * geo.per_pair() + geo.ck_bytes + geo.row_bytes;
 
-  // ---- walk (n1, n2) -> (0, 0); codes 1 diag, 2 left, 3 up, in path order from the end
+  // ---- walk (n1, n2) -> (0, 0); codes 1 diag, 2 left, 3 up, in path order from the end.
+  // A record holds a lane's 4 rows x 16 steps as two 64-bit masks (nd, u), cell (k, r) at bit
+  // 63 - (4k + r): inside a record a left move is bit + 4, up + 1, diag + 5, all scalar; the
+  // record changes when the path leaves the lane's rows or the block's steps.
   uint32_t y = n1, x = n2, L = 0;
   int32_t rs = -1, rq = 0;             // the region in LDS: strip rs, steps [rq*kCk, +kCk)
   int32_t ws_ = -1, wl0 = 0, wb0 = 0;  // the record window in VGPRs
   uint4 rec = make_uint4(0, 0, 0, 0);
   uint32_t mvreg = 0;
-  while (y | x) {
-    uint32_t code;
-    if (x == 0) {
-      code = 3;
-    } else if (y == 0) {
-      code = 2;
-    } else {
-      const uint32_t yy = y - 1;
-      const int32_t s = (int32_t)(yy / kStrip), l = (int32_t)((yy / kRows) & 63);
-      const uint32_t r = yy & (kRows - 1);
-      const uint32_t t = x - 1 + (uint32_t)l;
-      const int32_t blk = (int32_t)(t / kBlk);
-      const uint32_t k = t & (kBlk - 1);
-      if (s != rs || blk < rq * (int32_t)kCkBlk) {  // the path only moves to smaller t, s
-        rs = s;
-        rq = blk / (int32_t)kCkBlk;
-        const uint8_t* c = ck + ((uint64_t)s * geo.CK + (uint32_t)rq) * kCkBytes;
-        const int4 lv = reinterpret_cast<const int4*>(c)[lane];
-        const int2 dp = reinterpret_cast<const int2*>(c + 64 * 16)[lane];
-        Strip st;
-        strip_start(st, a, ao, n1, (uint32_t)s, lane);
-        st.left[0] = lv.x;
-        st.left[1] = lv.y;
-        st.left[2] = lv.z;
-        st.left[3] = lv.w;
-        st.diag = dp.x;
-        st.pass = dp.y;
-        for (uint32_t bi = 0; bi < kCkBlk; ++bi) {
-          const uint32_t t0 = (uint32_t)rq * kCk + bi * kBlk;
-          if (t0 >= nblk * kBlk) break;
-          const uint32_t xf = t0 + 1 + (lane & 15);
-          uint32_t fv = 0;
-          if (s > 0 && xf <= n2) fv = rows[(uint64_t)(s - 1) * geo.RS + xf - 1];
-          uint4 rr;
-          if (t0 < 64 || t0 + kBlk > n2) fill_block<true, true>(st, fv, bx, t0, n2, lane, &rr);
-          else fill_block<false, true>(st, fv, bx, t0, n2, lane, &rr);
-          lrec[bi][lane] = rr;
-        }
-        __syncthreads();
-        ws_ = -1;
-      }
-      if (s != ws_ || l < wl0 || blk < wb0) {  // the path only moves to smaller l and blk
-        ws_ = s;
-        wl0 = l - 15;
-        wb0 = max(blk - 3, rq * (int32_t)kCkBlk);
-        const int32_t il = wl0 + (int32_t)(lane >> 2), ib = wb0 + (int32_t)(lane & 3);
-        rec = il >= 0 ? lrec[ib - rq * (int32_t)kCkBlk][il] : make_uint4(0, 0, 0, 0);
-      }
-      const int idx = (l - wl0) * 4 + (blk - wb0);
-      const uint32_t ndw = (uint32_t)__builtin_amdgcn_readlane((int)(r < 2 ? rec.x : rec.y), idx);
-      const uint32_t uw = (uint32_t)__builtin_amdgcn_readlane((int)(r < 2 ? rec.z : rec.w), idx);
-      const uint32_t bit = 31 - (2 * k + (r & 1));
-      code = !((ndw >> bit) & 1u) ? 1u : !((uw >> bit) & 1u) ? 2u : 3u;
-    }
-    mvreg = (lane == (L & 63)) ? code : mvreg;
+  auto put = [&](uint32_t code) {  // move L goes to lane L % 64 of mvreg; 64 at a time out
+    // One scalar operand per VALU on gfx950: the lane select goes through M0.
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0"
+                 : "+v"(mvreg)
+                 : "s"(code), "s"(L & 63)
+                 : "m0");
     if ((L & 63) == 63) mvp[L - 63 + lane] = (uint8_t)mvreg;
     ++L;
+  };
+  auto emit = [&](uint32_t code) {
+    put(code);
     y -= (code != 2);
     x -= (code != 3);
+  };
+  while (y | x) {
+    if (x == 0) {
+      emit(3);
+      continue;
+    }
+    if (y == 0) {
+      emit(2);
+      continue;
+    }
+    const uint32_t yy = y - 1;
+    const int32_t s = (int32_t)(yy / kStrip), l = (int32_t)((yy / kRows) & 63);
+    uint32_t r = yy & (kRows - 1);
+    const uint32_t t = x - 1 + (uint32_t)l;
+    const int32_t blk = (int32_t)(t / kBlk);
+    uint32_t k = t & (kBlk - 1);
+    if (s != rs || blk < rq * (int32_t)kCkBlk) {  // the path only moves to smaller t, s
+      rs = s;
+      rq = blk / (int32_t)kCkBlk;
+      const uint8_t* c = ck + ((uint64_t)s * geo.CK + (uint32_t)rq) * kCkBytes;
+      const int4 lv = reinterpret_cast<const int4*>(c)[lane];
+      const int2 dp = reinterpret_cast<const int2*>(c + 64 * 16)[lane];
+      Strip st;
+      strip_start(st, a, ao, n1, (uint32_t)s, lane);
+      st.left[0] = lv.x;
+      st.left[1] = lv.y;
+      st.left[2] = lv.z;
+      st.left[3] = lv.w;
+      st.diag = dp.x;
+      st.pass = dp.y;
+      // The row above the strip: 64 columns per lane-register, both halves of the region loaded
+      // at once.
+      const uint32_t* above = rows + (uint64_t)(s > 0 ? s - 1 : 0) * geo.RS;
+      auto feed = [&](uint32_t t0) -> uint32_t {
+        const uint32_t xf = t0 + 1 + lane;
+        return (s > 0 && xf <= n2) ? above[xf - 1] : 0u;
+      };
+      uint32_t R = feed((uint32_t)rq * kCk);
+      const uint32_t R2 = feed((uint32_t)rq * kCk + kPhase);
+      for (uint32_t bi = 0; bi < kCkBlk; ++bi) {
+        const uint32_t t0 = (uint32_t)rq * kCk + bi * kBlk;
+        if (t0 >= nblk * kBlk) break;
+        if (bi == kPhase / kBlk) R = R2;
+        uint4 rr;
+        R = (t0 < 64 || t0 + kBlk > n2) ? fill_block<true, true>(st, R, bx, t0, n2, lane, &rr)
+                                        : fill_block<false, true>(st, R, bx, t0, n2, lane, &rr);
+        lrec[bi][lane] = rr;
+      }
+      __syncthreads();
+      ws_ = -1;
+    }
+    if (s != ws_ || l < wl0 || blk < wb0) {  // the path only moves to smaller l and blk
+      ws_ = s;
+      wl0 = l - 15;
+      wb0 = max(blk - 3, rq * (int32_t)kCkBlk);
+      const int32_t il = wl0 + (int32_t)(lane >> 2), ib = wb0 + (int32_t)(lane & 3);
+      rec = il >= 0 ? lrec[ib - rq * (int32_t)kCkBlk][il] : make_uint4(0, 0, 0, 0);
+    }
+    const int idx = (l - wl0) * 4 + (blk - wb0);
+    const uint64_t nd = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.x, idx) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)rec.y, idx);
+    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.z, idx) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)rec.w, idx);
+    // Leaving the record: the row above lane l's rows (r < 0), the step before the block (k < 0)
+    // or column 0 (k < l - 16 blk): bit > bmax.
+    const int32_t kmin = max(0, l - 16 * blk);
+    const uint32_t bmax = 63 - 4 * (uint32_t)kmin;
+    uint32_t bit = 63 - (4 * k + r);
+    for (;;) {  // inside record (l, blk); integer flags keep it all scalar
+      const uint32_t ndb = (uint32_t)(nd >> bit) & 1u, ub = (uint32_t)(u >> bit) & 1u;
+      const uint32_t upm = ndb & ub;          // 1: up
+      const uint32_t code = 1u + ndb + upm;   // 1 diag, 2 left, 3 up
+      const uint32_t dk = 1u - upm;           // x moves
+      const uint32_t dr = 1u - ndb + upm;     // y moves
+      put(code);
+      x -= dk;
+      y -= dr;
+      const uint32_t wrap = ((bit & 3u) + dr) & 4u;  // r was 0 and y moved
+      bit += 4u * dk + dr;
+      if ((int32_t)((bmax - bit) | (0u - wrap)) < 0) break;
+    }
   }
   if ((L & 63) && lane < (L & 63)) mvp[(L & ~63u) + lane] = (uint8_t)mvreg;
   __syncthreads();
@@ -372,8 +422,10 @@ hipError_t launch_nw(const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
     if (e != hipSuccess) return e;
     {
       ProfScope ps(prof, GDSM_PROF_NW_TRACE, s);
-      hipLaunchKernelGGL(nw_trace_kernel, dim3((uint32_t)cnt), dim3(64), 0, s, a, a_off, b,
-                         b_off, first, max_len, ws, ws, out1, out2, out_len);
+      const bool lds_b = max_len <= kBLds;
+      auto kern = lds_b ? nw_trace_kernel<true> : nw_trace_kernel<false>;
+      hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(64), lds_b ? max_len + 4 : 0, s, a,
+                         a_off, b, b_off, first, max_len, ws, ws, out1, out2, out_len);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;

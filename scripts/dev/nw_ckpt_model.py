@@ -22,7 +22,7 @@ def step_blocks(n2):
 
 
 def run_block(st, R, b, t0, n2, rec):
-    """One 16-step block; st = dict(a, left, diag, pass). Returns R (bottoms in lanes 47..62)."""
+    """One 16-step block; st = dict(a, left, diag, pass). Returns R (bottoms in lanes 48..63)."""
     nd = np.zeros((64, ROWS, BLK), bool)
     uu = np.zeros((64, ROWS, BLK), bool)
     for k in range(BLK):
@@ -30,6 +30,7 @@ def run_block(st, R, b, t0, n2, rec):
         act = (x >= 1) & (x <= n2)
         bb = b[np.clip(x, 1, n2) - 1]
         up_in = np.concatenate(([R[0]], st["pass"][:-1]))
+        R = np.roll(R, -1)  # lane l <- lane l+1, lane 63 <- lane 0 (consumed)
         up, dgv = up_in.copy(), st["diag"].copy()
         for r in range(ROWS):
             lf = st["left"][:, r].copy()
@@ -43,7 +44,6 @@ def run_block(st, R, b, t0, n2, rec):
         st["diag"] = np.where(act, up_in, st["diag"])
         st["pass"] = up
         R = np.where(LANE == 63, up, R)
-        R = np.roll(R, -1)  # lane l <- lane l+1
     if rec is not None:
         rec.append((nd, uu))
     return R
@@ -64,15 +64,16 @@ def fill(a, b, rng):
         for t0 in range(0, nblk * BLK, BLK):
             if t0 % CK == 0:
                 ck[(s, t0 // CK)] = {k: v.copy() for k, v in st.items()}
-            x = t0 + 1 + (LANE & 15)
-            if s == 0:
-                fv = np.zeros(64, np.int64)
-            else:
-                prev = rows[s - 1]
-                fv = np.where(x <= n2, prev[np.minimum(x, n2) - 1], rng.integers(0, 1 << 20, 64))
-            R = run_block(st, fv, b, t0, n2, None)
-            for L in range(47, 63):
-                xo = t0 + L - 109
+            if t0 % 64 == 0:  # a phase: 64 feed words, one per lane
+                x = t0 + 1 + LANE
+                if s == 0:
+                    R = np.zeros(64, np.int64)
+                else:
+                    prev = rows[s - 1]
+                    R = np.where(x <= n2, prev[np.minimum(x, n2) - 1], rng.integers(0, 1 << 20, 64))
+            R = run_block(st, R, b, t0, n2, None)
+            for L in range(48, 64):
+                xo = t0 + L - 110
                 if 1 <= xo <= n2:
                     row[xo - 1] = R[L]
         rows[s] = row
@@ -102,10 +103,11 @@ def trace(a, b, ck, rows):
                     t0 = rq * CK + bi * BLK
                     if t0 >= nblk * BLK:
                         break
-                    xf = t0 + 1 + (LANE & 15)
-                    fv = np.zeros(64, np.int64) if s == 0 else \
-                        np.where(xf <= n2, rows[s - 1][np.minimum(xf, n2) - 1], 0)
-                    run_block(st, fv, b, t0, n2, lrec)
+                    if t0 % 64 == 0:
+                        xf = t0 + 1 + LANE
+                        R = np.zeros(64, np.int64) if s == 0 else \
+                            np.where(xf <= n2, rows[s - 1][np.minimum(xf, n2) - 1], 0)
+                    R = run_block(st, R, b, t0, n2, lrec)
             nd, uu = lrec[blk - rq * (CK // BLK)]
             code = 1 if not nd[lane, r, k] else (2 if not uu[lane, r, k] else 3)
         moves.append(code)
