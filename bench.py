@@ -651,7 +651,7 @@ def run_mmult(args):
 
 
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (MICROARCH)
-NW_OPS_PER_CELL = 8  # cmp, addc, max3, 2 x (sub, alignbit), add: gdsm_nw.hip fill_block
+NW_OPS_PER_CELL = 4.5  # 18 VALU per step of 4 cells: gdsm_nw.hip fill_block (cmp, addc, max3 per cell)
 
 
 def run_nw(args):

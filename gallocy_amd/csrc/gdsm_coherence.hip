@@ -384,9 +384,6 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     }                          \
   } while (0)
   uint32_t xprevh = 0;  // the event before X[0] in this lane (half 1)
-#if defined(GDSM_PAD_SALU) || defined(GDSM_PAD_VALU)
-  uint32_t pad_s = 0, pad_v = lane;
-#endif
 #pragma unroll
   for (uint32_t h = 0; h < (kM == 1 ? 0u : kFK / kFH); ++h) {
     fold_half(tr, lane, h, X);
@@ -456,17 +453,6 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
         // accumulate now: left alone, the compiler sinks these sums past the walk and keeps
         // every event's intermediate values live
         asm volatile("" : "+v"(inv), "+v"(xfer), "+v"(F[k / 8]), "+v"(Hc), "+v"(Xc));
-#ifdef GDSM_PAD_SALU  // MEASUREMENT ONLY: extra independent scalar ALU work per walk step
-#pragma unroll
-        for (int q_ = 0; q_ < GDSM_PAD_SALU; ++q_) {
-          uint32_t t_;
-          asm volatile("s_add_u32 %0, %1, %2" : "=s"(t_) : "s"(q_ + 7), "s"(q_ + 1));
-        }
-#endif
-#ifdef GDSM_PAD_VALU  // MEASUREMENT ONLY: extra independent vector ALU work per walk step
-#pragma unroll
-        for (int q_ = 0; q_ < GDSM_PAD_VALU; ++q_) asm volatile("v_add_u32 %0, %0, %1" : "+v"(pad_v) : "v"(x));
-#endif
       }
     }
     xprevh = X[kFH - 1];
@@ -650,9 +636,6 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   }
   if (lane < 10) partial[b * 10 + lane] = mine;
   if (kM == 0 && __ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
-#if defined(GDSM_PAD_SALU) || defined(GDSM_PAD_VALU)
-  if ((pad_s ^ pad_v) == 0x9E3779B9u) atomicOr(err, 4u);  // keeps the padding alive
-#endif
   COH_FSTAMP(4, __builtin_amdgcn_s_memtime());
 }
 
