@@ -30,9 +30,9 @@
 // 16-byte record per lane per 16 steps, into LDS. The path crosses ~3 regions of a strip, so the
 // trace recomputes ~1.5 % of the matrix where the fill used to write 2 bits for every cell.
 //
-// Trace (nw_trace_kernel): one wave per pair walks the path with wave-uniform (scalar) state,
-// reading directions out of a 64-record window held in VGPRs (v_readlane with a uniform lane),
-// writes the moves, then turns them into the two alignment strings with wave prefix counts.
+// Trace (nw_trace_kernel, 8 waves per pair): the strips are walked in parallel from guessed
+// entries, then checked in order (a strip whose real entry differs is walked again until it meets
+// its first walk), and every DP row's share of the output is written at once (see below).
 #include "gdsm_common.h"
 #include "gdsm_launch.h"
 
@@ -49,7 +49,10 @@ constexpr uint32_t kPhase = 64;           // steps per phase (between barriers)
 constexpr uint32_t kLag = 2;              // phases between consecutive strips
 constexpr uint32_t kRing = 256;           // ring slots per wave (>= 193 live columns)
 constexpr uint32_t kBlk = 16;             // steps per traceback record
-constexpr uint32_t kCk = 128;             // steps per checkpoint = per recomputed region
+#ifndef GDSM_NW_CK
+#define GDSM_NW_CK 128
+#endif
+constexpr uint32_t kCk = GDSM_NW_CK;      // steps per checkpoint = per recomputed region
 constexpr uint32_t kCkBlk = kCk / kBlk;   // records per lane per region
 constexpr uint32_t kCkBytes = 64 * 24;    // one checkpoint: 64 x (left[4] | diag, pass)
 
@@ -79,16 +82,16 @@ __host__ __device__ inline uint32_t step_blocks(uint32_t n2) { return (n2 + 63 +
 struct Geo {
   uint32_t CK;   // checkpoints per strip slot
   uint64_t RS;   // words per stored bottom row
-  uint64_t ck_bytes, row_bytes, mv_bytes;
+  uint64_t ck_bytes, row_bytes, rec_bytes;
   __host__ __device__ explicit Geo(uint32_t max_len) {
     const uint64_t S = max_len ? (max_len + kStrip - 1) / kStrip : 1;
     CK = (step_blocks(max_len) * kBlk + kCk - 1) / kCk;
     RS = (uint64_t)max_len + 64;
     ck_bytes = S * CK * kCkBytes;
     row_bytes = (S * RS * 4 + 255) & ~255ull;
-    mv_bytes = (2 * (uint64_t)max_len + 64 + 255) & ~255ull;
+    rec_bytes = (((uint64_t)max_len + 1) * 8 + 255) & ~255ull;  // the trace's row records
   }
-  __host__ __device__ uint64_t per_pair() const { return ck_bytes + row_bytes + mv_bytes; }
+  __host__ __device__ uint64_t per_pair() const { return ck_bytes + row_bytes + rec_bytes; }
 };
 
 // One block of 16 steps [t0, t0 + 16) of a strip. R: lane i holds the word lane 0 consumes at
@@ -241,159 +244,275 @@ __global__ __launch_bounds__(64 * kWaves) void nw_fill_kernel(
   }
 }
 
-template <bool kLdsB>
-__global__ __launch_bounds__(64) void nw_trace_kernel(
+// ---- trace: strips in parallel from guessed entries, then checked in order -------------------
+// The path is recorded per DP row y as (lo, hi, how it leaves the row): it enters row y at column
+// hi, moves left to lo, then up (3) or diagonally (1) into row y - 1; row 0 holds the final run of
+// left moves. Phase A: the pair's 8 waves walk all strips at once, each from a guessed entry on
+// its strip's bottom row (the last strip's, (n1, n2), is exact; the others y * n2 / n1).
+// Phase B: wave 0 takes the strips in order from the end: a strip whose real entry (the exit of
+// the strip below) is not its guess is walked again from the real one until it meets its
+// recorded path (a cell inside that row's [lo, hi]: from a common cell on the two paths agree).
+// Phase C: every row's share of the output by a scan, and its characters.
+#ifndef GDSM_NW_TW
+#define GDSM_NW_TW 8
+#endif
+constexpr uint32_t kTW = GDSM_NW_TW;       // trace waves per pair
+constexpr uint64_t kX21 = (1ull << 21) - 1;  // columns <= 2^20 (gdsm_nw_diff_batch's limit)
+
+__device__ __forceinline__ uint64_t row_rec(uint32_t lo, uint32_t hi, uint32_t code) {
+  return (uint64_t)lo | ((uint64_t)hi << 21) | ((uint64_t)code << 42);
+}
+__device__ __forceinline__ uint64_t ld_row(const uint64_t* p) {  // other waves' rows (L2)
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
     const uint8_t* __restrict__ a, const uint64_t* __restrict__ a_off,
     const uint8_t* __restrict__ b, const uint64_t* __restrict__ b_off, uint64_t first_pair,
-    uint32_t max_len, const uint8_t* __restrict__ ws, uint8_t* __restrict__ mv_ws,
-    uint8_t* __restrict__ out1, uint8_t* __restrict__ out2, uint64_t* __restrict__ out_len) {
-  __shared__ uint4 lrec[kCkBlk][64];
+    uint32_t max_len, uint8_t* __restrict__ ws, uint8_t* __restrict__ out1,
+    uint8_t* __restrict__ out2, uint64_t* __restrict__ out_len) {
+  __shared__ uint4 lrec_all[kTW][kCkBlk][64];  // each wave's recomputed region (64 KiB)
+  __shared__ uint8_t bwin_all[kTW][256];         // each wave's region of b (kCk + 63 columns)
   const uint64_t pair = first_pair + blockIdx.x;
-  const uint32_t lane = threadIdx.x;
+  // the wave index as a scalar: everything a wave walks with is wave-uniform
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63;
   const uint64_t ao = a_off[pair], bo = b_off[pair];
   const uint64_t l1 = a_off[pair + 1] - ao, l2 = b_off[pair + 1] - bo;
   if (l1 > max_len || l2 > max_len) return;  // flagged by the fill kernel
   const uint32_t n1 = (uint32_t)l1, n2 = (uint32_t)l2;
   const uint32_t nblk = step_blocks(n2);
   const uint8_t* bx = b + bo - 1;
-  if (kLdsB) {
-#pragma unroll 16
-    for (uint32_t i = lane; i < n2; i += 64) nw_dyn_lds[i + 1] = bx[i + 1];
-    bx = nw_dyn_lds;
-    __syncthreads();
-  }
   const Geo geo(max_len);
   const uint8_t* ck = ws + blockIdx.x * geo.per_pair();
   const uint32_t* rows = reinterpret_cast<const uint32_t*>(ck + geo.ck_bytes);
-  uint8_t* mvp = mv_ws + blockIdx.x * geo.per_pair() + geo.ck_bytes + geo.row_bytes;
+  uint64_t* rr = reinterpret_cast<uint64_t*>(ws + blockIdx.x * geo.per_pair() + geo.ck_bytes +
+                                             geo.row_bytes);
+  uint4(*lrec)[64] = lrec_all[w];
+  const uint32_t S = (n1 + kStrip - 1) / kStrip;
+  auto guess = [&](uint32_t s) -> uint32_t {
+    if (s + 1 == S) return n2;
+    return (uint32_t)(((uint64_t)kStrip * (s + 1) * n2 + n1 / 2) / n1);
+  };
 
-  // ---- walk (n1, n2) -> (0, 0); codes 1 diag, 2 left, 3 up, in path order from the end.
   // A record holds a lane's 4 rows x 16 steps as two 64-bit masks (nd, u), cell (k, r) at bit
   // 63 - (4k + r): inside a record a left move is bit + 4, up + 1, diag + 5, all scalar; the
   // record changes when the path leaves the lane's rows or the block's steps.
-  uint32_t y = n1, x = n2, L = 0;
   int32_t rs = -1, rq = 0;             // the region in LDS: strip rs, steps [rq*kCk, +kCk)
   int32_t ws_ = -1, wl0 = 0, wb0 = 0;  // the record window in VGPRs
   uint4 rec = make_uint4(0, 0, 0, 0);
-  uint32_t mvreg = 0;
-  auto put = [&](uint32_t code) {  // move L goes to lane L % 64 of mvreg; 64 at a time out
+  // row records leave 64 at a time: lane j of (rlo, rhi) holds row ybase - j
+  uint32_t rlo = 0, rhi = 0, nrow = 0, ybase = 0;
+  auto put_row = [&](uint32_t yr, uint64_t v) {
+    const uint32_t j = nrow & 63;
+    if (j == 0) ybase = yr;
     // One scalar operand per VALU on gfx950: the lane select goes through M0.
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0"
-                 : "+v"(mvreg)
-                 : "s"(code), "s"(L & 63)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %3, m0\n\t"
+                 "v_writelane_b32 %1, %4, m0"
+                 : "+v"(rlo), "+v"(rhi)
+                 : "s"(j), "s"((uint32_t)v), "s"((uint32_t)(v >> 32))
                  : "m0");
-    if ((L & 63) == 63) mvp[L - 63 + lane] = (uint8_t)mvreg;
-    ++L;
+    ++nrow;
+    if (j == 63) rr[ybase - lane] = ((uint64_t)rhi << 32) | rlo;
   };
-  auto emit = [&](uint32_t code) {
-    put(code);
-    y -= (code != 2);
-    x -= (code != 3);
+  auto flush_rows = [&]() {
+    const uint32_t j = nrow & 63;
+    if (j && lane < j) rr[ybase - lane] = ((uint64_t)rhi << 32) | rlo;
+    nrow = 0;
   };
-  while (y | x) {
-    if (x == 0) {
-      emit(3);
-      continue;
-    }
-    if (y == 0) {
-      emit(2);
-      continue;
-    }
-    const uint32_t yy = y - 1;
-    const int32_t s = (int32_t)(yy / kStrip), l = (int32_t)((yy / kRows) & 63);
-    uint32_t r = yy & (kRows - 1);
-    const uint32_t t = x - 1 + (uint32_t)l;
-    const int32_t blk = (int32_t)(t / kBlk);
-    uint32_t k = t & (kBlk - 1);
-    if (s != rs || blk < rq * (int32_t)kCkBlk) {  // the path only moves to smaller t, s
-      rs = s;
-      rq = blk / (int32_t)kCkBlk;
-      const uint8_t* c = ck + ((uint64_t)s * geo.CK + (uint32_t)rq) * kCkBytes;
-      const int4 lv = reinterpret_cast<const int4*>(c)[lane];
-      const int2 dp = reinterpret_cast<const int2*>(c + 64 * 16)[lane];
-      Strip st;
-      strip_start(st, a, ao, n1, (uint32_t)s, lane);
-      st.left[0] = lv.x;
-      st.left[1] = lv.y;
-      st.left[2] = lv.z;
-      st.left[3] = lv.w;
-      st.diag = dp.x;
-      st.pass = dp.y;
-      // The row above the strip: 64 columns per lane-register, both halves of the region loaded
-      // at once.
-      const uint32_t* above = rows + (uint64_t)(s > 0 ? s - 1 : 0) * geo.RS;
-      auto feed = [&](uint32_t t0) -> uint32_t {
-        const uint32_t xf = t0 + 1 + lane;
-        return (s > 0 && xf <= n2) ? above[xf - 1] : 0u;
-      };
-      uint32_t R = feed((uint32_t)rq * kCk);
-      const uint32_t R2 = feed((uint32_t)rq * kCk + kPhase);
-      for (uint32_t bi = 0; bi < kCkBlk; ++bi) {
-        const uint32_t t0 = (uint32_t)rq * kCk + bi * kBlk;
-        if (t0 >= nblk * kBlk) break;
-        if (bi == kPhase / kBlk) R = R2;
-        uint4 rr;
-        R = (t0 < 64 || t0 + kBlk > n2) ? fill_block<true, true>(st, R, bx, t0, n2, lane, &rr)
-                                        : fill_block<false, true>(st, R, bx, t0, n2, lane, &rr);
-        lrec[bi][lane] = rr;
+
+  // Walk strip s from (y, x) on until the path leaves the strip's top row. With `merge`, stop
+  // at the first cell inside the recorded row's [lo, hi] (the row keeps its lo and exit).
+  auto walk = [&](uint32_t s, uint32_t y, uint32_t x, bool merge) {
+    const uint32_t top = s * kStrip + 1;
+    uint32_t hi = x;
+    uint64_t spec = merge ? ld_row(rr + y) : 0;
+    while (y >= top) {
+      if (merge) {
+        const uint32_t lo_s = (uint32_t)(spec & kX21), hi_s = (uint32_t)((spec >> 21) & kX21);
+        if (lo_s <= x && x <= hi_s) {
+          put_row(y, (spec & ~(kX21 << 21)) | ((uint64_t)hi << 21));
+          break;
+        }
       }
-      __syncthreads();
-      ws_ = -1;
+      if (x == 0) {  // column 0: straight up
+        put_row(y, row_rec(0, hi, 3));
+        --y;
+        hi = 0;
+        if (merge && y >= top) spec = ld_row(rr + y);
+        continue;
+      }
+      const uint32_t yy = y - 1;
+      const int32_t l = (int32_t)((yy / kRows) & 63);
+      const uint32_t r = yy & (kRows - 1);
+      const uint32_t t = x - 1 + (uint32_t)l;
+      const int32_t blk = (int32_t)(t / kBlk);
+      const uint32_t k = t & (kBlk - 1);
+      if ((int32_t)s != rs || blk < rq * (int32_t)kCkBlk ||
+          blk >= (rq + 1) * (int32_t)kCkBlk) {  // recompute the region from its checkpoint
+        rs = (int32_t)s;
+        rq = blk / (int32_t)kCkBlk;
+        const uint8_t* c = ck + ((uint64_t)s * geo.CK + (uint32_t)rq) * kCkBytes;
+        const int4 lv = reinterpret_cast<const int4*>(c)[lane];
+        const int2 dp = reinterpret_cast<const int2*>(c + 64 * 16)[lane];
+        Strip st;
+        strip_start(st, a, ao, n1, s, lane);
+        st.left[0] = lv.x;
+        st.left[1] = lv.y;
+        st.left[2] = lv.z;
+        st.left[3] = lv.w;
+        st.diag = dp.x;
+        st.pass = dp.y;
+        // the row above the strip: 64 columns per register, both halves loaded at once
+        const uint32_t* above = rows + (uint64_t)(s > 0 ? s - 1 : 0) * geo.RS;
+        auto feed = [&](uint32_t t0) -> uint32_t {
+          const uint32_t xf = t0 + 1 + lane;
+          return (s > 0 && xf <= n2) ? above[xf - 1] : 0u;
+        };
+        uint32_t R = feed((uint32_t)rq * kCk);
+        const uint32_t R2 = kCkBlk > kPhase / kBlk ? feed((uint32_t)rq * kCk + kPhase) : 0u;
+        // the region's columns of b, loaded with the checkpoint: bw[x] for x in
+        // [rq kCk - 62, rq kCk + kCk] (masked blocks clamp x inside it)
+        uint8_t* bwin = bwin_all[w];
+        const int32_t xb = (int32_t)((uint32_t)rq * kCk) - 63;
+        static_assert(kCk + 64 <= 256, "b window");
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const int32_t xc = xb + (int32_t)(4 * lane + j);
+          bwin[4 * lane + j] = (xc >= 1 && xc <= (int32_t)n2) ? bx[xc] : (uint8_t)0;
+        }
+        const uint8_t* bw = bwin - xb;
+        for (uint32_t bi = 0; bi < kCkBlk; ++bi) {
+          const uint32_t t0 = (uint32_t)rq * kCk + bi * kBlk;
+          if (t0 >= nblk * kBlk) break;
+          if (bi == kPhase / kBlk) R = R2;
+          uint4 rr4;
+          R = (t0 < 64 || t0 + kBlk > n2) ? fill_block<true, true>(st, R, bw, t0, n2, lane, &rr4)
+                                          : fill_block<false, true>(st, R, bw, t0, n2, lane, &rr4);
+          lrec[bi][lane] = rr4;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are done
+        __builtin_amdgcn_wave_barrier();
+        ws_ = -1;
+      }
+      // (a walk moves to smaller l and blk; a new walk may start anywhere)
+      if ((int32_t)s != ws_ || l < wl0 || blk < wb0 || l > wl0 + 15 || blk > wb0 + 3) {
+        ws_ = (int32_t)s;
+        wl0 = l - 15;
+        wb0 = max(blk - 3, rq * (int32_t)kCkBlk);
+        const int32_t il = wl0 + (int32_t)(lane >> 2), ib = wb0 + (int32_t)(lane & 3);
+        rec = il >= 0 ? lrec[ib - rq * (int32_t)kCkBlk][il] : make_uint4(0, 0, 0, 0);
+      }
+      const int idx = (l - wl0) * 4 + (blk - wb0);
+      const uint64_t nd = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.x, idx) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)rec.y, idx);
+      const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.z, idx) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)rec.w, idx);
+      // Leaving the record: the row above lane l's rows (r < 0), the step before the block
+      // (k < 0) or column 0 (k < l - 16 blk): bit > bmax.
+      const int32_t kmin = max(0, l - 16 * blk);
+      const uint32_t bmax = 63 - 4 * (uint32_t)kmin;
+      uint32_t bit = 63 - (4 * k + r);
+      const uint32_t y0 = y;
+      for (;;) {  // inside record (l, blk); integer flags keep it all scalar
+        const uint32_t ndb = (uint32_t)(nd >> bit) & 1u, ub = (uint32_t)(u >> bit) & 1u;
+        const uint32_t upm = ndb & ub;         // 1: up
+        const uint32_t code = 1u + ndb + upm;  // 1 diag, 2 left, 3 up
+        const uint32_t dk = 1u - upm;          // x moves
+        const uint32_t dr = 1u - ndb + upm;    // y moves
+        if (dr) {  // the row ends here
+          put_row(y, row_rec(x, hi, code));
+          hi = x - dk;
+        }
+        x -= dk;
+        y -= dr;
+        const uint32_t wrap = ((bit & 3u) + dr) & 4u;  // r was 0 and y moved
+        bit += 4u * dk + dr;
+        if (merge || (int32_t)((bmax - bit) | (0u - wrap)) < 0) break;
+      }
+      if (merge && y != y0 && y >= top) spec = ld_row(rr + y);
     }
-    if (s != ws_ || l < wl0 || blk < wb0) {  // the path only moves to smaller l and blk
-      ws_ = s;
-      wl0 = l - 15;
-      wb0 = max(blk - 3, rq * (int32_t)kCkBlk);
-      const int32_t il = wl0 + (int32_t)(lane >> 2), ib = wb0 + (int32_t)(lane & 3);
-      rec = il >= 0 ? lrec[ib - rq * (int32_t)kCkBlk][il] : make_uint4(0, 0, 0, 0);
-    }
-    const int idx = (l - wl0) * 4 + (blk - wb0);
-    const uint64_t nd = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.x, idx) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane((int)rec.y, idx);
-    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.z, idx) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)rec.w, idx);
-    // Leaving the record: the row above lane l's rows (r < 0), the step before the block (k < 0)
-    // or column 0 (k < l - 16 blk): bit > bmax.
-    const int32_t kmin = max(0, l - 16 * blk);
-    const uint32_t bmax = 63 - 4 * (uint32_t)kmin;
-    uint32_t bit = 63 - (4 * k + r);
-    for (;;) {  // inside record (l, blk); integer flags keep it all scalar
-      const uint32_t ndb = (uint32_t)(nd >> bit) & 1u, ub = (uint32_t)(u >> bit) & 1u;
-      const uint32_t upm = ndb & ub;          // 1: up
-      const uint32_t code = 1u + ndb + upm;   // 1 diag, 2 left, 3 up
-      const uint32_t dk = 1u - upm;           // x moves
-      const uint32_t dr = 1u - ndb + upm;     // y moves
-      put(code);
-      x -= dk;
-      y -= dr;
-      const uint32_t wrap = ((bit & 3u) + dr) & 4u;  // r was 0 and y moved
-      bit += 4u * dk + dr;
-      if ((int32_t)((bmax - bit) | (0u - wrap)) < 0) break;
-    }
-  }
-  if ((L & 63) && lane < (L & 63)) mvp[(L & ~63u) + lane] = (uint8_t)mvreg;
+    flush_rows();
+  };
+
+  // ---- phase A: every strip from its guessed entry
+  for (int32_t s = (int32_t)S - 1 - (int32_t)w; s >= 0; s -= (int32_t)kTW)
+    walk((uint32_t)s, min(kStrip * ((uint32_t)s + 1), n1), guess((uint32_t)s), false);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's row stores have landed
   __syncthreads();
 
-  // ---- alignment strings: move i (from the end) fills position L-1-i
-  const uint64_t oo = ao + bo + pair;
-  uint32_t cy = 0, cx = 0;
-  for (uint32_t base = 0; base < L; base += 64) {
-    const uint32_t i = base + lane;
-    const uint32_t c = i < L ? mvp[i] : 0u;
-    const uint32_t isy = (c == 1 || c == 3), isx = (c == 1 || c == 2);
-    const uint32_t ey = wave_incl_sum(isy) - isy, ex = wave_incl_sum(isx) - isx;
-    if (i < L) {
-      const uint32_t yk = n1 - cy - ey, xk = n2 - cx - ex;
-      out1[oo + L - 1 - i] = isy ? a[ao + yk - 1] : (uint8_t)'-';
-      out2[oo + L - 1 - i] = isx ? b[bo + xk - 1] : (uint8_t)'-';
+  // ---- phase B: in order from the last strip, each strip's real entry. The strips' top rows
+  // are loaded 64 at a time up front; only a strip walked again reloads its own.
+  if (w == 0) {
+    uint64_t topv = 0;  // lane j: the top row of strip sb + j
+    int32_t sb = -1;
+    bool again = false;  // strip s + 1 was walked again
+    for (int32_t s = (int32_t)S - 2; s >= 0; --s) {
+      if (s + 1 < sb || sb < 0) {
+        sb = max(s + 1 - 63, 1);
+        const uint32_t sj = (uint32_t)sb + lane;
+        topv = sj < S ? ld_row(rr + kStrip * sj + 1) : 0;
+      }
+      uint64_t v = lane_bcast64(topv, s + 1 - sb);
+      if (again) v = ld_row(rr + kStrip * ((uint32_t)s + 1) + 1);
+      const uint32_t xe = (uint32_t)(v & kX21) - (((v >> 42) & 3u) == 1u ? 1u : 0u);
+      again = xe != guess((uint32_t)s);
+      if (again) {
+        walk((uint32_t)s, kStrip * ((uint32_t)s + 1), xe, true);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+      }
     }
-    cy += wave_sum(isy);
-    cx += wave_sum(isx);
+    uint32_t hi0 = n2;  // row 0: the run of left moves into (0, 0)
+    if (n1) {
+      const uint64_t v = ld_row(rr + 1);
+      hi0 = (uint32_t)(v & kX21) - (((v >> 42) & 3u) == 1u ? 1u : 0u);
+    }
+    if (lane == 0) rr[0] = row_rec(0, hi0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
   }
-  if (lane == 0) {
-    out1[oo + L] = 0;
-    out2[oo + L] = 0;
-    out_len[pair] = L;
+  __syncthreads();
+
+  // ---- phase C: thread i owns rows [i m, i m + m); row y's characters start at the number of
+  // characters of rows 0 .. y-1 (one block scan)
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(&lrec_all[0][0][0]);
+  const uint64_t oo = ao + bo + pair;
+  const uint32_t m = (n1 + 64 * kTW) / (64 * kTW);  // ceil((n1 + 1) / threads)
+  const uint32_t y0 = threadIdx.x * m, y1 = min(y0 + m, n1 + 1);
+  auto row_chars = [](uint32_t y, uint64_t v) -> uint32_t {
+    const uint32_t lo = (uint32_t)(v & kX21), hi = (uint32_t)((v >> 21) & kX21);
+    return y ? 1u + hi - lo : hi;
+  };
+  uint32_t cnt = 0;
+#pragma unroll 4
+  for (uint32_t y = y0; y < y1; ++y) cnt += row_chars(y, ld_row(rr + y));
+  const uint32_t incl = wave_incl_sum(cnt);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t off = 0, carry = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kTW; ++i) {
+    const uint32_t q = wsum[i];
+    off += i < w ? q : 0u;
+    carry += q;
+  }
+  uint64_t p = oo + off + incl - cnt;
+  for (uint32_t y = y0; y < y1; ++y) {
+    const uint64_t v = ld_row(rr + y);
+    const uint32_t lo = (uint32_t)(v & kX21), hi = (uint32_t)((v >> 21) & kX21);
+    if (y) {
+      out1[p] = a[ao + y - 1];
+      out2[p] = ((v >> 42) & 3u) == 1u ? b[bo + lo - 1] : (uint8_t)'-';
+      ++p;
+    }
+    for (uint32_t xx = y ? lo + 1 : 1u; xx <= hi; ++xx, ++p) {
+      out1[p] = (uint8_t)'-';
+      out2[p] = b[bo + xx - 1];
+    }
+  }
+  if (threadIdx.x == 0) {
+    out1[oo + carry] = 0;
+    out2[oo + carry] = 0;
+    out_len[pair] = carry;
   }
 }
 
@@ -422,10 +541,8 @@ hipError_t launch_nw(const uint8_t* a, const uint64_t* a_off, const uint8_t* b,
     if (e != hipSuccess) return e;
     {
       ProfScope ps(prof, GDSM_PROF_NW_TRACE, s);
-      const bool lds_b = max_len <= kBLds;
-      auto kern = lds_b ? nw_trace_kernel<true> : nw_trace_kernel<false>;
-      hipLaunchKernelGGL(kern, dim3((uint32_t)cnt), dim3(64), lds_b ? max_len + 4 : 0, s, a,
-                         a_off, b, b_off, first, max_len, ws, ws, out1, out2, out_len);
+      hipLaunchKernelGGL(nw_trace_kernel, dim3((uint32_t)cnt), dim3(64 * kTW), 0, s, a, a_off, b,
+                         b_off, first, max_len, ws, out1, out2, out_len);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -142,5 +142,124 @@ def main():
             sys.exit(1)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and (len(sys.argv) < 3 or sys.argv[2] != "spec"):
     main()
+
+
+# ---- speculative strip-parallel trace (nw_trace_kernel v2) --------------------------------------
+class Regions:
+    """The trace's region cache for one walker: strip s, steps [rq*CK, rq*CK + CK)."""
+
+    def __init__(self, a, b, ck, rows):
+        self.a, self.b, self.ck, self.rows = a, b, ck, rows
+        self.rs, self.rq, self.lrec = -1, 0, None
+
+    def bits(self, y, x):
+        n2 = len(self.b)
+        nblk = step_blocks(n2)
+        yy = y - 1
+        s, lane, r = yy // STRIP, (yy // ROWS) & 63, yy & 3
+        t = x - 1 + lane
+        blk, k = t // BLK, t & (BLK - 1)
+        if s != self.rs or blk < self.rq * (CK // BLK) or blk >= (self.rq + 1) * (CK // BLK):
+            self.rs, self.rq = s, blk // (CK // BLK)
+            st = {kk: v.copy() for kk, v in self.ck[(s, self.rq)].items()}
+            self.lrec = []
+            for bi in range(CK // BLK):
+                t0 = self.rq * CK + bi * BLK
+                if t0 >= nblk * BLK:
+                    break
+                if t0 % 64 == 0:
+                    xf = t0 + 1 + LANE
+                    R = np.zeros(64, np.int64) if s == 0 else \
+                        np.where(xf <= n2, self.rows[s - 1][np.minimum(xf, n2) - 1], 0)
+                R = run_block(st, R, self.b, t0, n2, self.lrec)
+        nd, uu = self.lrec[blk - self.rq * (CK // BLK)]
+        return 1 if not nd[lane, r, k] else (2 if not uu[lane, r, k] else 3)
+
+
+def walk_strip(reg, s, y, x, rec, spec=None):
+    """Walk from (y, x) (y in strip s) until the path leaves the strip's top row; rec[y] =
+    (lo, hi, type) per row. With `spec` (the strip's recorded rows), stop at the first cell on
+    that path (merge): the row's hi becomes the re-walk's entry. Returns the exit (y, x)."""
+    top = STRIP * s + 1
+    hi = x
+    while y >= top:
+        if spec is not None:
+            lo_s, hi_s, _ = spec[y]
+            if lo_s <= x <= hi_s:
+                rec[y] = (spec[y][0], hi, spec[y][2])
+                return None  # merged: rows above are the spec path's
+        code = 3 if x == 0 else reg.bits(y, x)
+        if code == 2:
+            x -= 1
+            continue
+        rec[y] = (x, hi, code)
+        y -= 1
+        x -= code == 1
+        hi = x
+    return y, x
+
+
+def trace_spec(a, b, ck, rows):
+    n1, n2 = len(a), len(b)
+    rec = {}
+    if n1 == 0:
+        rec[0] = (0, n2, 0)
+    else:
+        S = (n1 + STRIP - 1) // STRIP
+        guess = {}
+        # phase A: every strip from a guessed entry (exact for the last)
+        for s in range(S - 1, -1, -1):
+            ye = min(STRIP * (s + 1), n1)
+            xg = n2 if s == S - 1 else (ye * n2 + n1 // 2) // n1
+            guess[s] = xg
+            walk_strip(Regions(a, b, ck, rows), s, ye, xg, rec)
+        spec = dict(rec)
+        # phase B: in order from the last strip, the real entry of each; re-walk on a mismatch
+        reg = Regions(a, b, ck, rows)
+        for s in range(S - 2, -1, -1):
+            lo, _, typ = rec[STRIP * (s + 1) + 1]
+            xe = lo - (typ == 1)
+            if xe != guess[s]:
+                walk_strip(reg, s, STRIP * (s + 1), xe, rec, spec)
+        lo, _, typ = rec[1]
+        rec[0] = (0, lo - (typ == 1), 0)
+    # phase C: output per row
+    o1, o2 = bytearray(), bytearray()
+    lo0, hi0, _ = rec[0]
+    for x in range(1, hi0 + 1):
+        o1.append(ord("-"))
+        o2.append(b[x - 1])
+    for y in range(1, n1 + 1):
+        lo, hi, typ = rec[y]
+        o1.append(a[y - 1])
+        o2.append(b[lo - 1] if typ == 1 else ord("-"))
+        for x in range(lo + 1, hi + 1):
+            o1.append(ord("-"))
+            o2.append(b[x - 1])
+    return bytes(o1), bytes(o2)
+
+
+def main_spec(cases=12):
+    rng = np.random.default_rng(9)
+    shapes = [(1, 1), (63, 64), (300, 257), (600, 130), (40, 700), (513, 513), (200, 193),
+              (1000, 20), (20, 1000), (780, 800), (0, 5), (5, 0)]
+    for i in range(cases):
+        n1, n2 = shapes[i % len(shapes)]
+        alpha = [2, 4, 256][i % 3]
+        a = rng.integers(0, alpha, n1).astype(np.int64)
+        b = rng.integers(0, alpha, n2).astype(np.int64)
+        if i % 4 == 3 and n1 == n2:  # near-identical: the guesses hold
+            b = a.copy()
+            b[rng.integers(0, n2, 3)] ^= 1
+        ck, rows = fill(a, b, rng) if n1 and n2 else ({}, {})
+        got = trace_spec(a, b, ck, rows)
+        want = oracle.nw_diff(bytes(a.astype(np.uint8)), bytes(b.astype(np.uint8)))
+        print("spec", i, n1, n2, alpha, "ok" if got == want else "MISMATCH")
+        if got != want:
+            sys.exit(1)
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "spec":
+    main_spec(int(sys.argv[1]))
