@@ -857,7 +857,7 @@ int gdsm_nw_diff_batch(gdsm_ctx* ctx, const uint8_t* a, const uint64_t* a_off, c
   if (!n) return 0;
   CtxGuard g(ctx);
   if (g.rc) return g.rc;
-  // Up to 4 GiB of traceback workspace per chunk of pairs, at least one pair.
+  // Up to 4 GiB of checkpoint / row workspace per chunk of pairs, at least one pair.
   const uint64_t per = gdsm::nw_pair_ws_bytes(max_len);
   uint64_t pairs = (4ull << 30) / per;
   if (pairs < 1) pairs = 1;
