@@ -651,7 +651,7 @@ def run_mmult(args):
 
 
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk (MICROARCH)
-NW_OPS_PER_CELL = 4.5  # 18 VALU per step of 4 cells: gdsm_nw.hip fill_block (cmp, addc, max3 per cell)
+NW_OPS_PER_CELL = 3.5  # 28 VALU per step of 8 cells: gdsm_nw.hip fill_block (cmp, addc, max3 per cell)
 
 
 def run_nw(args):

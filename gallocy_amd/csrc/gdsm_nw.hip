@@ -8,27 +8,28 @@
 // H[0][x] = -x, H[y][0] = -y (diff.cpp:94-102); the traceback prefers diag > left > up
 // (diff.cpp:115-120) and runs from (n, m) to (0, 0) (diff.cpp:126-158).
 //
-// Fill (nw_fill_kernel): one 16-wave workgroup per pair. Rows are cut into strips of 256; a strip
-// belongs to one wave, 4 consecutive rows per lane. Lane l computes column x = t - l + 1 at step
-// t, so the value from the row above (lane l-1's bottom row one step earlier) arrives by one DPP
-// wave_shr:1, and the byte of b by one LDS byte read (b is staged in LDS). Strip s+1
-// follows strip s two 64-step phases behind (one workgroup barrier per phase); the bottom row
-// of a strip reaches the next wave through a 256-column LDS ring (or, from wave 15 to wave 0 of
-// the next group of 16 strips, through the strip's bottom row in global memory). No MFMA: the
-// recurrence is max/add on int32, not a contraction.
+// Fill (nw_fill_kernel): one 8-wave workgroup per pair. Rows are cut into strips of 512; a strip
+// belongs to one wave, 8 consecutive rows per lane (8 rows spread the per-step DPP and feed work
+// over twice the cells of 4: the fill of 512 x 4 KiB pairs 1.27 -> 1.01 ms). Lane l computes
+// column x = t - l + 1 at step t, so the value from the row above (lane l-1's bottom row one step
+// earlier) arrives by one DPP wave_shr:1, and the byte of b by one LDS byte read (b is staged in
+// LDS). Strip s+1 follows strip s two 64-step phases behind (one workgroup barrier per phase);
+// the bottom row of a strip reaches the next wave through a 256-column LDS ring (or, from the
+// last wave to wave 0 of the next group of strips, through the strip's bottom row in global
+// memory). No MFMA: the recurrence is max/add on int32, not a contraction.
 //
 // Scores are kept as U = H + y + x, which makes every border 0 and a cell one compare, one
 // add-with-carry and one max3: U = max3(U[y-1][x-1] + 2 + (a==b), U[y][x-1], U[y-1][x]). The three
 // candidates are H's candidates shifted by the same y + x, so every comparison (and the traceback)
 // is the reference's.
 //
-// No traceback leaves the fill. It stores, per strip, the lanes' state every 128 steps (a
-// checkpoint: 4 left values, diag, pass; 24 B per lane) and the strip's bottom row (the next
-// strip's input, one word per column). The trace recomputes one 128-step region of a strip from
+// No traceback leaves the fill. It stores, per strip, the lanes' state every 64 steps (a
+// checkpoint: 8 left values, diag, pass; 40 B per lane) and the strip's bottom row (the next
+// strip's input, one word per column). The trace recomputes one 64-step region of a strip from
 // its checkpoint when the path enters it, with the traceback bits this time: two bits per cell,
 // nd = "not diag" (dg < max(lf, up)) and u = "up beats left" (up > left, only read when nd), a
-// 16-byte record per lane per 16 steps, into LDS. The path crosses ~3 regions of a strip, so the
-// trace recomputes ~1.5 % of the matrix where the fill used to write 2 bits for every cell.
+// 16-byte record per lane per 8 steps, into LDS. The path crosses ~10 regions of a strip, so the
+// trace recomputes a few % of the matrix where the fill used to write 2 bits for every cell.
 //
 // Trace (nw_trace_kernel, 8 waves per pair): the strips are walked in parallel from guessed
 // entries, then checked in order (a strip whose real entry differs is walked again until it meets
@@ -39,22 +40,28 @@
 namespace gdsm {
 namespace {
 
-constexpr uint32_t kRows = 4;             // DP rows per lane
+#ifndef GDSM_NW_ROWS
+#define GDSM_NW_ROWS 8
+#endif
+constexpr uint32_t kRows = GDSM_NW_ROWS;  // DP rows per lane
 #ifndef GDSM_NW_WAVES
-#define GDSM_NW_WAVES 16
+#define GDSM_NW_WAVES 8
 #endif
 constexpr uint32_t kWaves = GDSM_NW_WAVES;  // waves per fill workgroup
 constexpr uint32_t kStrip = 64 * kRows;   // rows per strip
 constexpr uint32_t kPhase = 64;           // steps per phase (between barriers)
 constexpr uint32_t kLag = 2;              // phases between consecutive strips
 constexpr uint32_t kRing = 256;           // ring slots per wave (>= 193 live columns)
-constexpr uint32_t kBlk = 16;             // steps per traceback record
+constexpr uint32_t kBlk = 16;             // steps per block (one feed word per lane, ...)
+constexpr uint32_t kRecK = 64 / kRows;    // steps per traceback record (a lane's rows x kRecK
+constexpr uint32_t kRecPerBlk = kBlk / kRecK;  // cells = one 64-bit mask per bit)
+static_assert(kRows == 4 || kRows == 8, "rows per lane");
 #ifndef GDSM_NW_CK
-#define GDSM_NW_CK 128
+#define GDSM_NW_CK 64
 #endif
 constexpr uint32_t kCk = GDSM_NW_CK;      // steps per checkpoint = per recomputed region
 constexpr uint32_t kCkBlk = kCk / kBlk;   // records per lane per region
-constexpr uint32_t kCkBytes = 64 * 24;    // one checkpoint: 64 x (left[4] | diag, pass)
+constexpr uint32_t kCkBytes = 64 * (4 * kRows + 8);  // one checkpoint: 64 x (left[] | diag, pass)
 
 __device__ __forceinline__ uint32_t wave_shr1_or(uint32_t old, uint32_t v) {
   // Lane l gets lane l-1's v; lane 0 keeps `old` (bound_ctrl off).
@@ -100,12 +107,15 @@ struct Geo {
 // feed word, the consumed one wraps to lane 63) and lane 63 takes the new bottom word, so after
 // the block lanes 48..63 hold the bottom words of steps t0..t0+15 (columns t0-62 .. t0-47) and
 // lanes 0..47 the feed words of the next 48 steps. With kRec the traceback bits of the lane's
-// 4 x 16 cells go to *rec.
+// kRows x 16 cells go to rec[0 .. kRecPerBlk), one 64-bit mask pair per kRecK steps.
 template <bool kMasked, bool kRec>
 __device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t R, const uint8_t* bx,
                                                uint32_t t0, uint32_t n2, uint32_t lane,
                                                uint4* rec) {
-  uint32_t ndA = 0, ndB = 0, uA = 0, uB = 0;
+  constexpr uint32_t kW = kBlk * kRows / 32;  // 32-bit words per mask per block
+  uint32_t ndw[kW], uw[kW];
+#pragma unroll
+  for (uint32_t i = 0; i < kW; ++i) ndw[i] = uw[i] = 0;
   const int32_t x0 = (int32_t)(t0 + 1) - (int32_t)lane;  // this lane's column at step t0
   const bool top = lane == 63;
 #pragma unroll
@@ -122,8 +132,8 @@ __device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t R, const uint
     const int32_t up_in = (int32_t)wave_shr1_or(R, (uint32_t)st.pass);
     R = wave_rol1(R);  // lane 0: the next feed word; lane 63: free (this step's feed, consumed)
     int32_t up = up_in, dgv = st.diag;
-    uint32_t* acc_nd = k < kBlk / 2 ? &ndA : &ndB;
-    uint32_t* acc_u = k < kBlk / 2 ? &uA : &uB;
+    uint32_t* acc_nd = &ndw[k / (32 / kRows)];
+    uint32_t* acc_u = &uw[k / (32 / kRows)];
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
       const int32_t lf = st.left[r];
@@ -143,7 +153,11 @@ __device__ __forceinline__ uint32_t fill_block(Strip& st, uint32_t R, const uint
     st.pass = up;
     R = top ? (uint32_t)up : R;
   }
-  if (kRec) *rec = make_uint4(ndA, ndB, uA, uB);
+  if (kRec) {
+#pragma unroll
+    for (uint32_t h = 0; h < kRecPerBlk; ++h)
+      rec[h] = make_uint4(ndw[2 * h], ndw[2 * h + 1], uw[2 * h], uw[2 * h + 1]);
+  }
   return R;
 }
 
@@ -224,9 +238,11 @@ __global__ __launch_bounds__(64 * kWaves) void nw_fill_kernel(
           if (t0 >= nblk * kBlk) break;
           if ((t0 & (kCk - 1)) == 0) {  // checkpoint: the state before step t0
             uint8_t* c = ck + ((uint64_t)s * geo.CK + t0 / kCk) * kCkBytes;
-            reinterpret_cast<int4*>(c)[lane] =
-                make_int4(st.left[0], st.left[1], st.left[2], st.left[3]);
-            reinterpret_cast<int2*>(c + 64 * 16)[lane] = make_int2(st.diag, st.pass);
+#pragma unroll
+            for (uint32_t q = 0; q < kRows / 4; ++q)
+              reinterpret_cast<int4*>(c + 64 * 16 * q)[lane] =
+                  make_int4(st.left[4 * q], st.left[4 * q + 1], st.left[4 * q + 2], st.left[4 * q + 3]);
+            reinterpret_cast<int2*>(c + 64 * 4 * kRows)[lane] = make_int2(st.diag, st.pass);
           }
           const bool masked = t0 < 64 || t0 + kBlk > n2;
           R = masked ? fill_block<true, false>(st, R, bx, t0, n2, lane, nullptr)
@@ -271,7 +287,7 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
     const uint8_t* __restrict__ b, const uint64_t* __restrict__ b_off, uint64_t first_pair,
     uint32_t max_len, uint8_t* __restrict__ ws, uint8_t* __restrict__ out1,
     uint8_t* __restrict__ out2, uint64_t* __restrict__ out_len) {
-  __shared__ uint4 lrec_all[kTW][kCkBlk][64];  // each wave's recomputed region (64 KiB)
+  __shared__ uint4 lrec_all[kTW][kCkBlk * kRecPerBlk][64];  // each wave's region (64 KiB)
   __shared__ uint8_t bwin_all[kTW][256];         // each wave's region of b (kCk + 63 columns)
   const uint64_t pair = first_pair + blockIdx.x;
   // the wave index as a scalar: everything a wave walks with is wave-uniform
@@ -289,15 +305,16 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
   uint64_t* rr = reinterpret_cast<uint64_t*>(ws + blockIdx.x * geo.per_pair() + geo.ck_bytes +
                                              geo.row_bytes);
   uint4(*lrec)[64] = lrec_all[w];
+  constexpr int32_t kRecs = (int32_t)(kCkBlk * kRecPerBlk);  // records per lane per region
   const uint32_t S = (n1 + kStrip - 1) / kStrip;
   auto guess = [&](uint32_t s) -> uint32_t {
     if (s + 1 == S) return n2;
     return (uint32_t)(((uint64_t)kStrip * (s + 1) * n2 + n1 / 2) / n1);
   };
 
-  // A record holds a lane's 4 rows x 16 steps as two 64-bit masks (nd, u), cell (k, r) at bit
-  // 63 - (4k + r): inside a record a left move is bit + 4, up + 1, diag + 5, all scalar; the
-  // record changes when the path leaves the lane's rows or the block's steps.
+  // A record holds a lane's kRows rows x kRecK steps as two 64-bit masks (nd, u), cell (k, r) at
+  // bit 63 - (kRows k + r): inside a record a left move is bit + kRows, up + 1, diag + kRows + 1,
+  // all scalar; the record changes when the path leaves the lane's rows or the record's steps.
   int32_t rs = -1, rq = 0;             // the region in LDS: strip rs, steps [rq*kCk, +kCk)
   int32_t ws_ = -1, wl0 = 0, wb0 = 0;  // the record window in VGPRs
   uint4 rec = make_uint4(0, 0, 0, 0);
@@ -346,21 +363,24 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
       const int32_t l = (int32_t)((yy / kRows) & 63);
       const uint32_t r = yy & (kRows - 1);
       const uint32_t t = x - 1 + (uint32_t)l;
-      const int32_t blk = (int32_t)(t / kBlk);
-      const uint32_t k = t & (kBlk - 1);
-      if ((int32_t)s != rs || blk < rq * (int32_t)kCkBlk ||
-          blk >= (rq + 1) * (int32_t)kCkBlk) {  // recompute the region from its checkpoint
+      const int32_t blk = (int32_t)(t / kRecK);  // the record (kRecK steps) holding the cell
+      const uint32_t k = t & (kRecK - 1);
+      if ((int32_t)s != rs || blk < rq * kRecs ||
+          blk >= (rq + 1) * kRecs) {  // recompute the region from its checkpoint
         rs = (int32_t)s;
-        rq = blk / (int32_t)kCkBlk;
+        rq = blk / kRecs;
         const uint8_t* c = ck + ((uint64_t)s * geo.CK + (uint32_t)rq) * kCkBytes;
-        const int4 lv = reinterpret_cast<const int4*>(c)[lane];
-        const int2 dp = reinterpret_cast<const int2*>(c + 64 * 16)[lane];
+        const int2 dp = reinterpret_cast<const int2*>(c + 64 * 4 * kRows)[lane];
         Strip st;
         strip_start(st, a, ao, n1, s, lane);
-        st.left[0] = lv.x;
-        st.left[1] = lv.y;
-        st.left[2] = lv.z;
-        st.left[3] = lv.w;
+#pragma unroll
+        for (uint32_t q = 0; q < kRows / 4; ++q) {
+          const int4 lv = reinterpret_cast<const int4*>(c + 64 * 16 * q)[lane];
+          st.left[4 * q] = lv.x;
+          st.left[4 * q + 1] = lv.y;
+          st.left[4 * q + 2] = lv.z;
+          st.left[4 * q + 3] = lv.w;
+        }
         st.diag = dp.x;
         st.pass = dp.y;
         // the row above the strip: 64 columns per register, both halves loaded at once
@@ -386,10 +406,11 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
           const uint32_t t0 = (uint32_t)rq * kCk + bi * kBlk;
           if (t0 >= nblk * kBlk) break;
           if (bi == kPhase / kBlk) R = R2;
-          uint4 rr4;
-          R = (t0 < 64 || t0 + kBlk > n2) ? fill_block<true, true>(st, R, bw, t0, n2, lane, &rr4)
-                                          : fill_block<false, true>(st, R, bw, t0, n2, lane, &rr4);
-          lrec[bi][lane] = rr4;
+          uint4 rr4[kRecPerBlk];
+          R = (t0 < 64 || t0 + kBlk > n2) ? fill_block<true, true>(st, R, bw, t0, n2, lane, rr4)
+                                          : fill_block<false, true>(st, R, bw, t0, n2, lane, rr4);
+#pragma unroll
+          for (uint32_t h = 0; h < kRecPerBlk; ++h) lrec[bi * kRecPerBlk + h][lane] = rr4[h];
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are done
         __builtin_amdgcn_wave_barrier();
@@ -399,20 +420,20 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
       if ((int32_t)s != ws_ || l < wl0 || blk < wb0 || l > wl0 + 15 || blk > wb0 + 3) {
         ws_ = (int32_t)s;
         wl0 = l - 15;
-        wb0 = max(blk - 3, rq * (int32_t)kCkBlk);
+        wb0 = max(blk - 3, rq * kRecs);
         const int32_t il = wl0 + (int32_t)(lane >> 2), ib = wb0 + (int32_t)(lane & 3);
-        rec = il >= 0 ? lrec[ib - rq * (int32_t)kCkBlk][il] : make_uint4(0, 0, 0, 0);
+        rec = il >= 0 ? lrec[ib - rq * kRecs][il] : make_uint4(0, 0, 0, 0);
       }
       const int idx = (l - wl0) * 4 + (blk - wb0);
       const uint64_t nd = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.x, idx) << 32) |
                           (uint32_t)__builtin_amdgcn_readlane((int)rec.y, idx);
       const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.z, idx) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)rec.w, idx);
-      // Leaving the record: the row above lane l's rows (r < 0), the step before the block
-      // (k < 0) or column 0 (k < l - 16 blk): bit > bmax.
-      const int32_t kmin = max(0, l - 16 * blk);
-      const uint32_t bmax = 63 - 4 * (uint32_t)kmin;
-      uint32_t bit = 63 - (4 * k + r);
+      // Leaving the record: the row above lane l's rows (r < 0), the step before the record
+      // (k < 0) or column 0 (k < l - kRecK blk): bit > bmax.
+      const int32_t kmin = max(0, l - (int32_t)kRecK * blk);
+      const uint32_t bmax = 63 - kRows * (uint32_t)kmin;
+      uint32_t bit = 63 - (kRows * k + r);
       const uint32_t y0 = y;
       for (;;) {  // inside record (l, blk); integer flags keep it all scalar
         const uint32_t ndb = (uint32_t)(nd >> bit) & 1u, ub = (uint32_t)(u >> bit) & 1u;
@@ -426,8 +447,8 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
         }
         x -= dk;
         y -= dr;
-        const uint32_t wrap = ((bit & 3u) + dr) & 4u;  // r was 0 and y moved
-        bit += 4u * dk + dr;
+        const uint32_t wrap = ((bit & (kRows - 1)) + dr) & kRows;  // r was 0 and y moved
+        bit += kRows * dk + dr;
         if (merge || (int32_t)((bmax - bit) | (0u - wrap)) < 0) break;
       }
       if (merge && y != y0 && y >= top) spec = ld_row(rr + y);

@@ -13,7 +13,7 @@ import numpy as np
 sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from oracle import oracle  # noqa: E402
 
-ROWS, STRIP, BLK, CK = 4, 256, 16, 128
+ROWS, STRIP, BLK, CK = 8, 512, 16, 64
 LANE = np.arange(64)
 
 
@@ -92,7 +92,7 @@ def trace(a, b, ck, rows):
             code = 2
         else:
             yy = y - 1
-            s, lane, r = yy // STRIP, (yy // ROWS) & 63, yy & 3
+            s, lane, r = yy // STRIP, (yy // ROWS) & 63, yy % ROWS
             t = x - 1 + lane
             blk, k = t // BLK, t & (BLK - 1)
             if s != rs or blk < rq * (CK // BLK):
@@ -158,7 +158,7 @@ class Regions:
         n2 = len(self.b)
         nblk = step_blocks(n2)
         yy = y - 1
-        s, lane, r = yy // STRIP, (yy // ROWS) & 63, yy & 3
+        s, lane, r = yy // STRIP, (yy // ROWS) & 63, yy % ROWS
         t = x - 1 + lane
         blk, k = t // BLK, t & (BLK - 1)
         if s != self.rs or blk < self.rq * (CK // BLK) or blk >= (self.rq + 1) * (CK // BLK):
