@@ -46,12 +46,14 @@ def test_reference_produced_vectors(ctx, golden):
     assert got == [(o1, o2) for _, _, o1, o2 in cases]
 
 
-# Shapes around every boundary of the kernel: strips (256 rows), the 16-strip group whose last
-# strip hands over through global memory (n1 > 4096), the lane pipeline (64 columns), the
-# 16-step blocks, the 64-step phases and regions the trace recomputes from checkpoints (a path through many regions: long and thin both ways).
+# Shapes around every boundary of the kernel: strips (512 rows; 256 in the 4-row build), the
+# 8-strip group whose last strip hands over through global memory (n1 > 4096), the lane pipeline
+# (64 columns), the 16-step blocks, the 64-step phases and the regions the trace recomputes from
+# checkpoints (a path through many regions: long and thin both ways).
 SHAPES = [(1, 1), (1, 300), (300, 1), (63, 64), (64, 65), (255, 17), (256, 256), (257, 1000),
           (1000, 257), (700, 700), (4096, 33), (4097, 80), (8500, 40), (50, 5000),
-          (128, 65), (129, 66), (200, 193), (3000, 2900), (16, 3000)]
+          (128, 65), (129, 66), (200, 193), (3000, 2900), (16, 3000), (511, 100), (512, 512),
+          (513, 70)]
 
 
 @pytest.mark.parametrize("alphabet", [256, 4, 2])
