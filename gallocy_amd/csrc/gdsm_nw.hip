@@ -40,6 +40,9 @@
 namespace gdsm {
 namespace {
 
+// Geometry (compile-time; the defaults are the measured best for 4 KiB pairs): rows
+// per lane, waves per fill workgroup, steps per phase and phases between strips, steps per
+// checkpoint, waves per trace workgroup.
 #ifndef GDSM_NW_ROWS
 #define GDSM_NW_ROWS 8
 #endif
@@ -49,8 +52,14 @@ constexpr uint32_t kRows = GDSM_NW_ROWS;  // DP rows per lane
 #endif
 constexpr uint32_t kWaves = GDSM_NW_WAVES;  // waves per fill workgroup
 constexpr uint32_t kStrip = 64 * kRows;   // rows per strip
-constexpr uint32_t kPhase = 64;           // steps per phase (between barriers)
-constexpr uint32_t kLag = 2;              // phases between consecutive strips
+#ifndef GDSM_NW_PHASE
+#define GDSM_NW_PHASE 64
+#endif
+#ifndef GDSM_NW_LAG
+#define GDSM_NW_LAG 2
+#endif
+constexpr uint32_t kPhase = GDSM_NW_PHASE;  // steps per phase (between barriers)
+constexpr uint32_t kLag = GDSM_NW_LAG;      // phases between consecutive strips
 constexpr uint32_t kRing = 256;           // ring slots per wave (>= 193 live columns)
 constexpr uint32_t kBlk = 16;             // steps per block (one feed word per lane, ...)
 constexpr uint32_t kRecK = 64 / kRows;    // steps per traceback record (a lane's rows x kRecK
