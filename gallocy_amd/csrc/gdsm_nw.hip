@@ -105,7 +105,7 @@ struct Geo {
     RS = (uint64_t)max_len + 64;
     ck_bytes = S * CK * kCkBytes;
     row_bytes = (S * RS * 4 + 255) & ~255ull;
-    rec_bytes = (((uint64_t)max_len + 1) * 8 + 255) & ~255ull;  // the trace's row records
+    rec_bytes = (((uint64_t)max_len + 2) * 4 + 255) & ~255ull;  // the trace's row records
   }
   __host__ __device__ uint64_t per_pair() const { return ck_bytes + row_bytes + rec_bytes; }
 };
@@ -270,10 +270,11 @@ __global__ __launch_bounds__(64 * kWaves) void nw_fill_kernel(
 }
 
 // ---- trace: strips in parallel from guessed entries, then checked in order -------------------
-// The path is recorded per DP row y as (lo, hi, how it leaves the row): it enters row y at column
-// hi, moves left to lo, then up (3) or diagonally (1) into row y - 1; row 0 holds the final run of
-// left moves. Phase A: the pair's 8 waves walk all strips at once, each from a guessed entry on
-// its strip's bottom row (the last strip's, (n1, n2), is exact; the others y * n2 / n1).
+// The path is recorded per DP row y as (lo, how it leaves the row): it enters row y at column hi,
+// moves left to lo, then up (3) or diagonally (1) into row y - 1, so hi of row y is where row
+// y + 1 left it (lo - 1 after a diagonal, lo after an up; n2 for row n1) and row 0 holds the
+// final run of left moves. Phase A: the pair's waves walk all strips at once, each from a guessed
+// entry on its strip's bottom row (the last strip's, (n1, n2), is exact; the others y * n2 / n1).
 // Phase B: wave 0 takes the strips in order from the end: a strip whose real entry (the exit of
 // the strip below) is not its guess is walked again from the real one until it meets its
 // recorded path (a cell inside that row's [lo, hi]: from a common cell on the two paths agree).
@@ -281,14 +282,18 @@ __global__ __launch_bounds__(64 * kWaves) void nw_fill_kernel(
 #ifndef GDSM_NW_TW
 #define GDSM_NW_TW 8
 #endif
-constexpr uint32_t kTW = GDSM_NW_TW;       // trace waves per pair
-constexpr uint64_t kX21 = (1ull << 21) - 1;  // columns <= 2^20 (gdsm_nw_diff_batch's limit)
+constexpr uint32_t kTW = GDSM_NW_TW;     // trace waves per pair
+constexpr uint32_t kX21 = (1u << 21) - 1;  // columns <= 2^20 (gdsm_nw_diff_batch's limit)
 
-__device__ __forceinline__ uint64_t row_rec(uint32_t lo, uint32_t hi, uint32_t code) {
-  return (uint64_t)lo | ((uint64_t)hi << 21) | ((uint64_t)code << 42);
-}
-__device__ __forceinline__ uint64_t ld_row(const uint64_t* p) {  // other waves' rows (L2)
+__device__ __forceinline__ uint32_t ld_row(const uint32_t* p) {  // other waves' rows (L2)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_row_u(const uint32_t* p) {  // the same, wave-uniform
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_row(p));
+}
+// the column a row record hands to the row above it (its entry column there)
+__device__ __forceinline__ uint32_t row_exit(uint32_t v) {
+  return (v & kX21) - ((v >> 21) == 1u ? 1u : 0u);
 }
 
 __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
@@ -311,8 +316,8 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
   const Geo geo(max_len);
   const uint8_t* ck = ws + blockIdx.x * geo.per_pair();
   const uint32_t* rows = reinterpret_cast<const uint32_t*>(ck + geo.ck_bytes);
-  uint64_t* rr = reinterpret_cast<uint64_t*>(ws + blockIdx.x * geo.per_pair() + geo.ck_bytes +
-                                             geo.row_bytes);
+  uint32_t* rr = reinterpret_cast<uint32_t*>(ws + blockIdx.x * geo.per_pair() + geo.ck_bytes +
+                                             geo.row_bytes);  // rr[y]: lo | exit << 21
   uint4(*lrec)[64] = lrec_all[w];
   constexpr int32_t kRecs = (int32_t)(kCkBlk * kRecPerBlk);  // records per lane per region
   const uint32_t S = (n1 + kStrip - 1) / kStrip;
@@ -327,23 +332,24 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
   int32_t rs = -1, rq = 0;             // the region in LDS: strip rs, steps [rq*kCk, +kCk)
   int32_t ws_ = -1, wl0 = 0, wb0 = 0;  // the record window in VGPRs
   uint4 rec = make_uint4(0, 0, 0, 0);
-  // row records leave 64 at a time: lane j of (rlo, rhi) holds row ybase - j
-  uint32_t rlo = 0, rhi = 0, nrow = 0, ybase = 0;
-  auto put_row = [&](uint32_t yr, uint64_t v) {
-    const uint32_t j = nrow & 63;
-    if (j == 0) ybase = yr;
+  // Row records leave 64 at a time: lane j of rbuf holds row ystart - (nbase + j). Every cell
+  // writes its row's candidate record into slot nrow % 64; the slot only advances when the row
+  // ends (no branch per cell).
+  uint32_t rbuf = 0, nrow = 0, ystart = 0;
+  auto put = [&](uint32_t v, uint32_t dr) {
+    uint32_t j = nrow & 63;
+    asm volatile("" : "+s"(v), "+s"(j));  // both in SGPRs (a literal is no writelane operand)
     // One scalar operand per VALU on gfx950: the lane select goes through M0.
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %3, m0\n\t"
-                 "v_writelane_b32 %1, %4, m0"
-                 : "+v"(rlo), "+v"(rhi)
-                 : "s"(j), "s"((uint32_t)v), "s"((uint32_t)(v >> 32))
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0"
+                 : "+v"(rbuf)
+                 : "s"(j), "s"(v)
                  : "m0");
-    ++nrow;
-    if (j == 63) rr[ybase - lane] = ((uint64_t)rhi << 32) | rlo;
+    nrow += dr;
+    if ((j + dr) & 64) rr[ystart - (nrow - 64) - lane] = rbuf;  // slot 63 filled: 64 rows out
   };
   auto flush_rows = [&]() {
     const uint32_t j = nrow & 63;
-    if (j && lane < j) rr[ybase - lane] = ((uint64_t)rhi << 32) | rlo;
+    if (j && lane < j) rr[ystart - (nrow - j) - lane] = rbuf;
     nrow = 0;
   };
 
@@ -351,21 +357,21 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
   // at the first cell inside the recorded row's [lo, hi] (the row keeps its lo and exit).
   auto walk = [&](uint32_t s, uint32_t y, uint32_t x, bool merge) {
     const uint32_t top = s * kStrip + 1;
-    uint32_t hi = x;
-    uint64_t spec = merge ? ld_row(rr + y) : 0;
+    ystart = y;
+    uint32_t spec = merge ? ld_row_u(rr + y) : 0;  // the recorded row y
+    uint32_t spec_hi = x == n2 && y == n1 ? n2 : guess(s);  // its entry column
     while (y >= top) {
-      if (merge) {
-        const uint32_t lo_s = (uint32_t)(spec & kX21), hi_s = (uint32_t)((spec >> 21) & kX21);
-        if (lo_s <= x && x <= hi_s) {
-          put_row(y, (spec & ~(kX21 << 21)) | ((uint64_t)hi << 21));
-          break;
-        }
+      if (merge && (spec & kX21) <= x && x <= spec_hi) {
+        put(spec, 1);  // merged: this row and the ones above are the recorded path
+        break;
       }
       if (x == 0) {  // column 0: straight up
-        put_row(y, row_rec(0, hi, 3));
+        put(3u << 21, 1);
         --y;
-        hi = 0;
-        if (merge && y >= top) spec = ld_row(rr + y);
+        if (merge && y >= top) {
+          spec_hi = row_exit(spec);
+          spec = ld_row_u(rr + y);
+        }
         continue;
       }
       const uint32_t yy = y - 1;
@@ -450,17 +456,17 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
         const uint32_t code = 1u + ndb + upm;  // 1 diag, 2 left, 3 up
         const uint32_t dk = 1u - upm;          // x moves
         const uint32_t dr = 1u - ndb + upm;    // y moves
-        if (dr) {  // the row ends here
-          put_row(y, row_rec(x, hi, code));
-          hi = x - dk;
-        }
+        put(x | (code << 21), dr);             // this row's record, if the row ends here
         x -= dk;
         y -= dr;
         const uint32_t wrap = ((bit & (kRows - 1)) + dr) & kRows;  // r was 0 and y moved
         bit += kRows * dk + dr;
         if (merge || (int32_t)((bmax - bit) | (0u - wrap)) < 0) break;
       }
-      if (merge && y != y0 && y >= top) spec = ld_row(rr + y);
+      if (merge && y != y0 && y >= top) {
+        spec_hi = row_exit(spec);
+        spec = ld_row_u(rr + y);
+      }
     }
     flush_rows();
   };
@@ -474,7 +480,7 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
   // ---- phase B: in order from the last strip, each strip's real entry. The strips' top rows
   // are loaded 64 at a time up front; only a strip walked again reloads its own.
   if (w == 0) {
-    uint64_t topv = 0;  // lane j: the top row of strip sb + j
+    uint32_t topv = 0;  // lane j: the top row of strip sb + j
     int32_t sb = -1;
     bool again = false;  // strip s + 1 was walked again
     for (int32_t s = (int32_t)S - 2; s >= 0; --s) {
@@ -483,38 +489,38 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
         const uint32_t sj = (uint32_t)sb + lane;
         topv = sj < S ? ld_row(rr + kStrip * sj + 1) : 0;
       }
-      uint64_t v = lane_bcast64(topv, s + 1 - sb);
-      if (again) v = ld_row(rr + kStrip * ((uint32_t)s + 1) + 1);
-      const uint32_t xe = (uint32_t)(v & kX21) - (((v >> 42) & 3u) == 1u ? 1u : 0u);
+      uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)topv, s + 1 - sb);
+      if (again) v = ld_row_u(rr + kStrip * ((uint32_t)s + 1) + 1);
+      const uint32_t xe = row_exit(v);
       again = xe != guess((uint32_t)s);
       if (again) {
         walk((uint32_t)s, kStrip * ((uint32_t)s + 1), xe, true);
         __builtin_amdgcn_s_waitcnt(0x0F70);
       }
     }
-    uint32_t hi0 = n2;  // row 0: the run of left moves into (0, 0)
-    if (n1) {
-      const uint64_t v = ld_row(rr + 1);
-      hi0 = (uint32_t)(v & kX21) - (((v >> 42) & 3u) == 1u ? 1u : 0u);
-    }
-    if (lane == 0) rr[0] = row_rec(0, hi0, 0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);
   }
   __syncthreads();
 
-  // ---- phase C: thread i owns rows [i m, i m + m); row y's characters start at the number of
-  // characters of rows 0 .. y-1 (one block scan)
+  // ---- phase C: thread i owns rows [i m, i m + m); row y's characters (1 + hi - lo, row 0: hi)
+  // start at the number of characters of rows 0 .. y-1 (one block scan)
   uint32_t* wsum = reinterpret_cast<uint32_t*>(&lrec_all[0][0][0]);
   const uint64_t oo = ao + bo + pair;
   const uint32_t m = (n1 + 64 * kTW) / (64 * kTW);  // ceil((n1 + 1) / threads)
   const uint32_t y0 = threadIdx.x * m, y1 = min(y0 + m, n1 + 1);
-  auto row_chars = [](uint32_t y, uint64_t v) -> uint32_t {
-    const uint32_t lo = (uint32_t)(v & kX21), hi = (uint32_t)((v >> 21) & kX21);
-    return y ? 1u + hi - lo : hi;
+  // row y: lo (0 for row 0) and hi (the exit of row y + 1; n2 for row n1)
+  auto row_at = [&](uint32_t y, uint32_t& lo, uint32_t& hi, uint32_t& code) {
+    const uint32_t v = y ? ld_row(rr + y) : 0u;
+    lo = v & kX21;
+    code = v >> 21;
+    hi = y < n1 ? row_exit(ld_row(rr + y + 1)) : n2;
   };
   uint32_t cnt = 0;
 #pragma unroll 4
-  for (uint32_t y = y0; y < y1; ++y) cnt += row_chars(y, ld_row(rr + y));
+  for (uint32_t y = y0; y < y1; ++y) {
+    uint32_t lo, hi, code;
+    row_at(y, lo, hi, code);
+    cnt += y ? 1u + hi - lo : hi;
+  }
   const uint32_t incl = wave_incl_sum(cnt);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
@@ -527,11 +533,11 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
   }
   uint64_t p = oo + off + incl - cnt;
   for (uint32_t y = y0; y < y1; ++y) {
-    const uint64_t v = ld_row(rr + y);
-    const uint32_t lo = (uint32_t)(v & kX21), hi = (uint32_t)((v >> 21) & kX21);
+    uint32_t lo, hi, code;
+    row_at(y, lo, hi, code);
     if (y) {
       out1[p] = a[ao + y - 1];
-      out2[p] = ((v >> 42) & 3u) == 1u ? b[bo + lo - 1] : (uint8_t)'-';
+      out2[p] = code == 1u ? b[bo + lo - 1] : (uint8_t)'-';
       ++p;
     }
     for (uint32_t xx = y ? lo + 1 : 1u; xx <= hi; ++xx, ++p) {

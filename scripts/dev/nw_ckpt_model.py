@@ -178,35 +178,37 @@ class Regions:
         return 1 if not nd[lane, r, k] else (2 if not uu[lane, r, k] else 3)
 
 
-def walk_strip(reg, s, y, x, rec, spec=None):
+def row_exit(v):
+    lo, typ = v
+    return lo - (typ == 1)
+
+
+def walk_strip(reg, s, y, x, rec, spec=None, spec_hi=None):
     """Walk from (y, x) (y in strip s) until the path leaves the strip's top row; rec[y] =
-    (lo, hi, type) per row. With `spec` (the strip's recorded rows), stop at the first cell on
-    that path (merge): the row's hi becomes the re-walk's entry. Returns the exit (y, x)."""
+    (lo, exit) per row (the row's entry column is the exit of row y + 1). With `spec` (the
+    strip's recorded rows, whose row y was entered at spec_hi), stop at the first cell on that
+    path (merge): the row keeps its record."""
     top = STRIP * s + 1
-    hi = x
     while y >= top:
-        if spec is not None:
-            lo_s, hi_s, _ = spec[y]
-            if lo_s <= x <= hi_s:
-                rec[y] = (spec[y][0], hi, spec[y][2])
-                return None  # merged: rows above are the spec path's
+        if spec is not None and spec[y][0] <= x <= spec_hi:
+            rec[y] = spec[y]
+            return None  # merged: rows above are the spec path's
         code = 3 if x == 0 else reg.bits(y, x)
         if code == 2:
             x -= 1
             continue
-        rec[y] = (x, hi, code)
+        rec[y] = (x, code)
+        if spec is not None:
+            spec_hi = row_exit(spec[y])
         y -= 1
         x -= code == 1
-        hi = x
     return y, x
 
 
 def trace_spec(a, b, ck, rows):
     n1, n2 = len(a), len(b)
     rec = {}
-    if n1 == 0:
-        rec[0] = (0, n2, 0)
-    else:
+    if n1:
         S = (n1 + STRIP - 1) // STRIP
         guess = {}
         # phase A: every strip from a guessed entry (exact for the last)
@@ -219,23 +221,20 @@ def trace_spec(a, b, ck, rows):
         # phase B: in order from the last strip, the real entry of each; re-walk on a mismatch
         reg = Regions(a, b, ck, rows)
         for s in range(S - 2, -1, -1):
-            lo, _, typ = rec[STRIP * (s + 1) + 1]
-            xe = lo - (typ == 1)
+            xe = row_exit(rec[STRIP * (s + 1) + 1])
             if xe != guess[s]:
-                walk_strip(reg, s, STRIP * (s + 1), xe, rec, spec)
-        lo, _, typ = rec[1]
-        rec[0] = (0, lo - (typ == 1), 0)
-    # phase C: output per row
+                walk_strip(reg, s, STRIP * (s + 1), xe, rec, spec, guess[s])
+    # phase C: output per row; row y's entry column is the exit of row y + 1 (n2 for row n1)
+    hi = {y: (row_exit(rec[y + 1]) if y < n1 else n2) for y in range(n1 + 1)}
     o1, o2 = bytearray(), bytearray()
-    lo0, hi0, _ = rec[0]
-    for x in range(1, hi0 + 1):
+    for x in range(1, hi[0] + 1):
         o1.append(ord("-"))
         o2.append(b[x - 1])
     for y in range(1, n1 + 1):
-        lo, hi, typ = rec[y]
+        lo, typ = rec[y]
         o1.append(a[y - 1])
         o2.append(b[lo - 1] if typ == 1 else ord("-"))
-        for x in range(lo + 1, hi + 1):
+        for x in range(lo + 1, hi[y] + 1):
             o1.append(ord("-"))
             o2.append(b[x - 1])
     return bytes(o1), bytes(o2)
