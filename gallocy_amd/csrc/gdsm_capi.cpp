@@ -70,18 +70,26 @@ int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need) {
   return 0;
 }
 
+// The buffer `which` of checked ids, grown to n.
+int safe_buf(gdsm_ctx* ctx, uint64_t n, int which, uint32_t** out) {
+  uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[which]);
+  int rc = ensure(ctx, &buf, &ctx->ids_safe_bytes[which], 4 * n);
+  ctx->ids_safe[which] = reinterpret_cast<uint32_t*>(buf);
+  *out = ctx->ids_safe[which];
+  return rc;
+}
+
 // A caller's device id list, checked against the arenas on stream `which` (0 main, 1 aux):
 // returns the list the kernels may use (out-of-range ids -> the guard page n_pages).
 int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const uint32_t** out) {
   *out = ids;
   if (!ids || n == 0) return 0;
-  uint8_t* buf = reinterpret_cast<uint8_t*>(ctx->ids_safe[which]);
-  int rc = ensure(ctx, &buf, &ctx->ids_safe_bytes[which], 4 * n);
-  ctx->ids_safe[which] = reinterpret_cast<uint32_t*>(buf);
+  uint32_t* buf = nullptr;
+  int rc = safe_buf(ctx, n, which, &buf);
   if (rc) return rc;
-  GDSM_TRY(gdsm::launch_check_ids(ids, n, ctx->n_pages, ctx->ids_safe[which], ctx->err,
+  GDSM_TRY(gdsm::launch_check_ids(ids, n, ctx->n_pages, buf, ctx->err,
                                   which == 1 ? ctx->aux : ctx->stream));
-  *out = ctx->ids_safe[which];
+  *out = buf;
   return 0;
 }
 
@@ -531,10 +539,9 @@ int gdsm_twin(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n) {
   if (!ids && n > ctx->n_pages) return -EINVAL;
   CtxGuard g(ctx);
   if (g.rc) return g.rc;
-  int rc = safe_ids(ctx, ids, n, 0, &ids);
-  if (rc) return rc;
+  // the kernel guards the list itself (no check launch: config 5 twins every round)
   GDSM_TRY(gdsm::launch_twin(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
-                             ctx->stream, ctx->P()));
+                             ctx->stream, ctx->P(), ctx->n_pages, ctx->err));
   return 0;
 }
 
@@ -599,14 +606,17 @@ static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* 
   auto busy = ctx->runs_busy.find(out->rec_off);
   if (busy != ctx->runs_busy.end()) GDSM_TRY(hipStreamWaitEvent(ctx->stream, busy->second, 0));
   int rc = ensure(ctx, &ctx->diff_ws, &ctx->diff_ws_bytes, gdsm::diff_workspace_bytes(n));
-  if (!rc) rc = safe_ids(ctx, ids, n, 0, &ids);
-  if (!rc && tids) rc = safe_ids(ctx, tids, n, 2, &tids);
+  // the caller's lists are checked into ids_safe[0] / [2] by the diff launch's prep kernel
+  gdsm::IdGuard guard{ids, tids, nullptr, nullptr, ctx->n_pages, ctx->err};
+  if (!rc && ids && n) rc = safe_buf(ctx, n, 0, &guard.safe_ids);
+  if (!rc && tids && n) rc = safe_buf(ctx, n, 2, &guard.safe_tids);
   if (rc) return rc;
+  if (!n) guard.ids = guard.tids = nullptr;
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
                              ctx->stream, ctx->P(), target >= 0 ? ctx->arena[target] : nullptr,
-                             ctx->diff_bpp, tids));
+                             ctx->diff_bpp, tids, &guard));
   return 0;
 }
 

@@ -1041,32 +1041,42 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
 }
 
-template <uint32_t kSC, bool kFull>
+// Spans [0, nfull) are whole; a partial last span (nb > nfull) is walked by the wave that draws
+// it, in the same launch (a separate tail launch was one more dependent launch per batch).
+template <uint32_t kSC>
 __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ pt,
                                                          uint64_t n_pages,
                                                          const uint64_t* __restrict__ ev,
-                                                         uint64_t n, uint64_t nb,
+                                                         uint64_t n, uint64_t nb, uint64_t nfull,
                                                          uint64_t* __restrict__ ws,
                                                          uint32_t* __restrict__ partial,
                                                          uint32_t* __restrict__ err,
                                                          uint32_t n_nodes,
                                                          unsigned long long* __restrict__ totals) {
   __shared__ uint32_t tk;
-  uint64_t b;
-  if (kFull) {  // tickets as coh_fold_kernel
-    const uint32_t cls = blockIdx.x % kFoldCtrs;
-    if (threadIdx.x == 0) tk = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
-    __syncthreads();
-    const uint32_t ticket = __builtin_amdgcn_readfirstlane(tk);
-    const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
-    b = w * 4 + (threadIdx.x >> 6);
-    if (b >= nb) return;
-  } else {
-    if (threadIdx.x >= 64) return;
-    b = nb - 1;
-  }
-  coh_stream_wave<kSC, kFull>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes,
-                              totals);
+  // tickets as coh_fold_kernel
+  const uint32_t cls = blockIdx.x % kFoldCtrs;
+  if (threadIdx.x == 0) tk = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
+  __syncthreads();
+  const uint32_t ticket = __builtin_amdgcn_readfirstlane(tk);
+  const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
+  const uint64_t b = w * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  if (b < nfull)
+    coh_stream_wave<kSC, true>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes,
+                               totals);
+  else
+    coh_stream_wave<kSC, false>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes,
+                                totals);
+}
+
+// The small-batch path's zeroing (batch totals and the tickets + status granules) in one launch.
+__global__ __launch_bounds__(256) void coh_zero_kernel(uint64_t* __restrict__ a, uint64_t na,
+                                                       uint64_t* __restrict__ b, uint64_t nb) {
+  const uint64_t st = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = t0; i < na; i += st) a[i] = 0;
+  for (uint64_t i = t0; i < nb; i += st) b[i] = 0;
 }
 
 // ---------------------------------------------------------------- D: totals
@@ -1173,29 +1183,26 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                             uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
                             Prof* prof) {
   const int cv = g_coh_variant.load(std::memory_order_relaxed);
-  hipError_t r = hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
-  if (r != hipSuccess || n_events == 0) return r;
-  if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
   const bool small = cv == 0 && n_events <= kCohSmall;
+  if (n_events == 0) return hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
+  if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
+  hipError_t r;
   if (cv == 1 || small) {
     const uint64_t span = 64ull * (small ? kSCSmall : kSCBig);
     const uint64_t ns = (n_events + span - 1) / span;
     uint64_t* fws = reinterpret_cast<uint64_t*>(ws);
     uint32_t* fpart = reinterpret_cast<uint32_t*>(fws + kFoldStatus + ns);
-    r = hipMemsetAsync(fws, 0, 8 * (kFoldStatus + ns), s);
-    if (r != hipSuccess) return r;
+    // the totals and the tickets + status granules zeroed by one launch
+    const uint64_t nz = kFoldStatus + ns;
+    hipLaunchKernelGGL(coh_zero_kernel, dim3((unsigned)min((nz + 255) / 256, (uint64_t)1024)),
+                       dim3(256), 0, s, totals, (uint64_t)10, fws, nz);
     {
       ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
       const uint64_t full = n_events / span;
-      auto kfull = small ? coh_stream_kernel<kSCSmall, true> : coh_stream_kernel<kSCBig, true>;
-      auto ktail = small ? coh_stream_kernel<kSCSmall, false> : coh_stream_kernel<kSCBig, false>;
+      auto kern = small ? coh_stream_kernel<kSCSmall> : coh_stream_kernel<kSCBig>;
       unsigned long long* direct = small ? reinterpret_cast<unsigned long long*>(totals) : nullptr;
-      if (full)
-        hipLaunchKernelGGL(kfull, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
-                           events, n_events, full, fws, fpart, err, n_nodes, direct);
-      if (ns > full)
-        hipLaunchKernelGGL(ktail, dim3(1), dim3(64), 0, s, pt, n_pages, events, n_events, ns, fws,
-                           fpart, err, n_nodes, direct);
+      hipLaunchKernelGGL(kern, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, s, pt, n_pages,
+                         events, n_events, ns, full, fws, fpart, err, n_nodes, direct);
     }
     if (small) return hipGetLastError();
     uint64_t g = (ns + 255) / 256;
@@ -1205,6 +1212,8 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                        reinterpret_cast<unsigned long long*>(totals));
     return hipGetLastError();
   }
+  r = hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
+  if (r != hipSuccess) return r;
   if (cv == 0 || cv == 2 || cv >= 4) {
     const uint64_t nf = fold_blocks(n_events);
     uint64_t* fws = reinterpret_cast<uint64_t*>(ws);

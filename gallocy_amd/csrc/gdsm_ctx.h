@@ -87,6 +87,8 @@ int ensure_aux(gdsm_ctx* ctx);
 // A caller's device id list checked against the arenas into buffer `which` (0 and 2 on the main
 // stream, 1 on aux).
 int safe_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, int which, const uint32_t** out);
+// Only the buffer `which` for n checked ids (for a launch that checks the list itself).
+int safe_buf(gdsm_ctx* ctx, uint64_t n, int which, uint32_t** out);
 int check_and_clear_err(gdsm_ctx* ctx);
 // Records the stream density (bytes / pages) the host learned, for the diff's geometry choice
 // (stored + 1, so 0 stays "unknown"). Lists of at most kDiffShortList pages take the short-list

@@ -16,17 +16,32 @@ int coh_tune(const char* key, int64_t value);
 hipError_t launch_gen_pages(uint8_t* twin, uint8_t* cur, uint8_t* replica, uint64_t n,
                             uint64_t first_global, uint64_t stride, uint64_t seed, int mode,
                             uint32_t ppm, hipStream_t s);
+// With a caller list, n_pages / err guard it in the kernel (ids >= n_pages -> the guard page
+// n_pages, err |= 8); the defaults leave the list unchecked (raw entry points).
 hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
-                       hipStream_t s, Prof* prof = nullptr);
+                       hipStream_t s, Prof* prof = nullptr, uint64_t n_pages = ~0ull,
+                       uint32_t* err = nullptr);
 // Full diff of n pages in one pass: rec_off[n+1], data[cap]. With `target`, the runs are also
 // applied to target by the same kernel, page tids[i] for list entry i (tids NULL: the same page
 // ids). bpp_hint: stream bytes per page the caller saw last time (0 = unknown); it only picks
 // the geometry.
+// Caller page-id lists checked by the diff launch itself (in the launch that zeroes its
+// workspace): safe_ids[i] = ids[i] if < n_pages, else n_pages (the guard page), the same for
+// tids, err |= 8 when any id was out of range. A null list is not checked.
+struct IdGuard {
+  const uint32_t* ids;
+  const uint32_t* tids;
+  uint32_t* safe_ids;
+  uint32_t* safe_tids;
+  uint64_t n_pages;
+  uint32_t* err;
+};
+// With `guard`, the kernel reads guard->safe_ids / safe_tids in place of ids / tids.
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr,
                        uint8_t* target = nullptr, uint32_t bpp_hint = 0,
-                       const uint32_t* tids = nullptr);
+                       const uint32_t* tids = nullptr, const IdGuard* guard = nullptr);
 // The diff kernel's output streams: list entries [first[d], first[d+1]) go to stream d (record
 // i of stream d = entry first[d] + i); ustart: the first work unit of each stream (set by the
 // launcher). One launch serves them all, each stream with its own look-back chain.

@@ -63,11 +63,14 @@ __global__ __launch_bounds__(256) void gen_pages_kernel(uint8_t* __restrict__ tw
 
 // ------------------------------------------------------------------------- twin (SPEC §2)
 // TWIN := CURRENT for listed pages: a wave per kP pages per step, every 16-B load of them in
-// flight before the stores (kNT: bit 0 nontemporal loads, bit 1 nontemporal stores).
+// flight before the stores (kNT: bit 0 nontemporal loads, bit 1 nontemporal stores). A caller
+// list is guarded in place (as check_ids_kernel below, without a launch of its own): an id >=
+// n_pages twins the guard page n_pages instead and sets err bit 8.
 template <uint32_t kP, int kNT>
 __global__ __launch_bounds__(256) void twin_kernel(uint8_t* __restrict__ twin,
                                                    const uint8_t* __restrict__ cur,
-                                                   const uint32_t* __restrict__ ids, uint64_t n) {
+                                                   const uint32_t* __restrict__ ids, uint64_t n,
+                                                   uint64_t n_pages, uint32_t* __restrict__ err) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t steps = (n + kP - 1) / kP;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < steps;
@@ -79,6 +82,10 @@ __global__ __launch_bounds__(256) void twin_kernel(uint8_t* __restrict__ twin,
       const uint64_t e = i * kP + k;
       pg[k] = e < n ? (ids ? ids[e] : e) : ~0ull;
       if (pg[k] == ~0ull) continue;
+      if (pg[k] >= n_pages) {  // (wave-uniform: one page per wave step)
+        pg[k] = n_pages;
+        if (err && lane == 0) atomicOr(err, 8u);
+      }
       const u32x4* src = reinterpret_cast<const u32x4*>(cur + pg[k] * kPage);
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q)
@@ -116,6 +123,33 @@ __global__ __launch_bounds__(256) void check_ids_kernel(const uint32_t* __restri
     bad |= !ok;
   }
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(err, 8u);
+}
+
+// Everything a diff launch needs zeroed or checked, as ONE launch before it (instead of a memset
+// per workspace range and a check launch per caller list: a small release is a handful of
+// microsecond operations, config 5's rounds): z64[0, n64) and z32[0, n32) := 0, and the caller
+// lists guarded as check_ids_kernel does (g.ids -> g.safe_ids, g.tids -> g.safe_tids).
+__global__ __launch_bounds__(256) void diff_prep_kernel(uint64_t* __restrict__ z64, uint64_t n64,
+                                                        uint32_t* __restrict__ z32, uint64_t n32,
+                                                        IdGuard g, uint64_t n) {
+  const uint64_t st = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = t0; i < n64; i += st) z64[i] = 0;
+  for (uint64_t i = t0; i < n32; i += st) z32[i] = 0;
+  bool bad = false;
+  for (uint64_t i = t0; i < n; i += st) {
+    if (g.ids) {
+      const uint32_t p = g.ids[i];
+      bad |= p >= g.n_pages;
+      g.safe_ids[i] = p < g.n_pages ? p : (uint32_t)g.n_pages;
+    }
+    if (g.tids) {
+      const uint32_t p = g.tids[i];
+      bad |= p >= g.n_pages;
+      g.safe_tids[i] = p < g.n_pages ? p : (uint32_t)g.n_pages;
+    }
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(g.err, 8u);
 }
 
 // ------------------------------------------------------------------------- exchanged streams
@@ -1402,31 +1436,62 @@ hipError_t launch_budget_check(const uint64_t* rec_off, uint64_t n, uint64_t bud
 }
 
 hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
-                       hipStream_t s, Prof* prof) {
+                       hipStream_t s, Prof* prof, uint64_t n_pages, uint32_t* err) {
   if (n == 0) return hipSuccess;
   ProfScope ps(prof, GDSM_PROF_TWIN, s);
   // one page per wave step, cached loads and stores: two or four pages per step and
   // nontemporal loads and/or stores measured 0.3-4.5 % slower in one process (round 4)
   auto kern = twin_kernel<1, 0>;
-  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur, ids, n);
+  hipLaunchKernelGGL(kern, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, twin, cur, ids, n,
+                     n_pages, err);
   return hipGetLastError();
 }
 
+// A workgroup copies n words of T, four per lane in flight before their stores (a load-store
+// pair per step would wait out one memory latency per step).
+template <typename T>
+__device__ __forceinline__ void copy_words(T* __restrict__ d, const T* __restrict__ s,
+                                           uint64_t n) {
+  const uint64_t st = blockDim.x;
+  uint64_t i = threadIdx.x;
+  for (; i + 3 * st < n; i += 4 * st) {
+    const T a = s[i], b = s[i + st], c = s[i + 2 * st], e = s[i + 3 * st];
+    d[i] = a;
+    d[i + st] = b;
+    d[i + 2 * st] = c;
+    d[i + 3 * st] = e;
+  }
+  for (; i < n; i += st) d[i] = s[i];
+}
+
 // n device-to-device copies in one launch (gdsm_memcpy_batch): copy i = desc[3i .. 3i+2] =
-// (dst, src, bytes), one workgroup per copy; 16 B per lane where dst, src and bytes are 16-aligned,
-// else bytes.
+// (dst, src, bytes), one workgroup per copy, in the widest words (16, 8, 4 or 1 B) that dst and
+// src are both aligned to, the remainder bytes after them. (Config 5's rows are 8-B aligned:
+// copied byte by byte they took 13-16 us of a ~45 us round.)
 __global__ __launch_bounds__(256) void copy_batch_kernel(const uint64_t* __restrict__ desc,
                                                          uint64_t n) {
   for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
     uint8_t* dst = reinterpret_cast<uint8_t*>(desc[3 * i]);
     const uint8_t* src = reinterpret_cast<const uint8_t*>(desc[3 * i + 1]);
     const uint64_t bytes = desc[3 * i + 2];
-    if (((uintptr_t)dst | (uintptr_t)src | bytes) & 15u) {
-      for (uint64_t b = threadIdx.x; b < bytes; b += blockDim.x) dst[b] = src[b];
+    const uintptr_t al = (uintptr_t)dst | (uintptr_t)src;
+    uint64_t done;
+    if (!(al & 15u)) {
+      copy_words(reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), bytes / 16);
+      done = bytes & ~15ull;
+    } else if (!(al & 7u)) {
+      copy_words(reinterpret_cast<uint64_t*>(dst), reinterpret_cast<const uint64_t*>(src),
+                 bytes / 8);
+      done = bytes & ~7ull;
+    } else if (!(al & 3u)) {
+      copy_words(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src),
+                 bytes / 4);
+      done = bytes & ~3ull;
     } else {
-      for (uint64_t q = threadIdx.x; q < bytes / 16; q += blockDim.x)
-        reinterpret_cast<uint4*>(dst)[q] = reinterpret_cast<const uint4*>(src)[q];
+      copy_words(dst, src, bytes);
+      done = bytes;
     }
+    for (uint64_t b = done + threadIdx.x; b < bytes; b += blockDim.x) dst[b] = src[b];
   }
 }
 
@@ -1439,12 +1504,12 @@ hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s) {
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
                                    Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
-                                   const uint32_t* tids);
+                                   const uint32_t* tids, const IdGuard* guard);
 
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target,
-                       uint32_t bpp_hint, const uint32_t* tids) {
+                       uint32_t bpp_hint, const uint32_t* tids, const IdGuard* guard) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   DiffSplit sp{};
   sp.G = 1;
@@ -1453,7 +1518,8 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   sp.cap[0] = cap;
   sp.first[0] = 0;
   sp.first[1] = n;
-  return launch_diff_impl(twin, cur, ids, sp, ws, ws_bytes, s, prof, target, bpp_hint, cap, tids);
+  return launch_diff_impl(twin, cur, ids, sp, ws, ws_bytes, s, prof, target, bpp_hint, cap, tids,
+                          guard);
 }
 
 hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
@@ -1470,14 +1536,14 @@ hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit 
   }
   if (sp.first[sp.G] == sp.first[0]) return hipSuccess;
   return launch_diff_impl(twin, cur, nullptr, sp, ws, ws_bytes, s, prof, nullptr, bpp_hint,
-                          mincap, nullptr);
+                          mincap, nullptr, nullptr);
 }
 
 // `cap` (the smallest stream capacity) only matters to workspaces that predate the spill pool.
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
                                    Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
-                                   const uint32_t* tids) {
+                                   const uint32_t* tids, const IdGuard* guard) {
   const uint64_t n = sp.first[sp.G] - sp.first[0];
   int v = diff_variant();
   // the spill pool's place in the workspace (after the largest status area n may need)
@@ -1509,11 +1575,23 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
   if (spill && (wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill > spill_pool_bytes(n))
     return hipErrorInvalidValue;
   // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
-  // (outside the timed kernel)
-  hipError_t e = hipMemsetAsync(ws, 0, (1 + nunits) * 8, s);
-  if (e == hipSuccess && spill) e = hipMemsetAsync(ws + status_end, 0, 4 * kSpillWGs, s);
-  if (e != hipSuccess) return e;
+  // (outside the timed kernel), and the caller's lists checked, in one prep launch
   uint32_t* gen = spill ? reinterpret_cast<uint32_t*>(ws + status_end) : nullptr;
+  {
+    IdGuard g{};
+    if (guard) {
+      g = *guard;
+      if (g.ids) ids = g.safe_ids;
+      if (g.tids) tids = g.safe_tids;
+    }
+    const uint64_t nz = 1 + nunits, nchk = (g.ids || g.tids) ? n : 0;
+    const uint64_t work = nz > nchk ? nz : nchk;
+    hipLaunchKernelGGL(diff_prep_kernel, dim3(grid_for(work, 256, 1024)), dim3(256), 0, s,
+                       reinterpret_cast<uint64_t*>(ws), nz, gen, spill ? (uint64_t)kSpillWGs : 0,
+                       g, nchk);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   uint8_t* pool = spill ? ws + pool_at : nullptr;
   ProfScope ps(prof, GDSM_PROF_DIFF, s);
   auto kern = target ? (v == 5   ? diff_single_kernel<64, 8192, 4, true, kDiffSpill>

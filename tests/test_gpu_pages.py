@@ -853,15 +853,17 @@ def test_diff_apply_ids_applies_at_other_indices():
 
 
 def test_memcpy_batch():
-    """gdsm_memcpy_batch: several copies in one launch, 16-B aligned (vector path) and not (byte
-    path), next to bytes that must stay untouched."""
-    import ctypes as C
+    """gdsm_memcpy_batch: several copies in one launch, in 16-, 8-, 4- and 1-B words by the
+    alignment of dst and src, with and without a remainder after the words, next to bytes that
+    must stay untouched."""
     rng = np.random.default_rng(5)
     with ga.Context(8, arenas=()) as c:
         src = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
         d_src = c.buffer(src.nbytes).upload(src)
         d_dst = c.buffer(1 << 16).upload(np.zeros(1 << 16, np.uint8))
-        copies = [(0, 0, 8000), (16384, 32, 4096), (30001, 7, 999), (40000, 50000, 3)]
+        copies = [(0, 0, 8000), (16384, 32, 4096), (30001, 7, 999), (40000, 50000, 3),
+                  (8200, 56008, 8000), (20488, 24000, 4103), (45004, 52012, 1030),
+                  (36000, 1, 3000), (28000, 4000, 1)]
         desc = np.array([[d_dst.ptr + d, d_src.ptr + s, b] for d, s, b in copies],
                         np.uint64).reshape(-1)
         d_desc = c.buffer(desc.nbytes).upload(desc)
