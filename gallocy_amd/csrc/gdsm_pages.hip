@@ -686,12 +686,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
       }
     }
   }
+  // (short units, kU <= 2: the registers still hold the unit's last page, so a late last page
+  // that no earlier late page displaced is emitted without reading it again — two dependent
+  // round trips less for a dense page of a small release)
+  constexpr bool kKeep = kU <= 2;
   for (uint64_t rem = late; rem;) {  // wave-uniform
     const uint32_t j = (uint32_t)__builtin_ctzll(rem);
+    const bool first_late = rem == late;
     rem &= rem - 1;
     if (excl + tab[j + 1] > cap) continue;
     const uint64_t i = i0 + j;
-    load_page(twin, cur, ids ? ids[i] : i, lane, t, c);
+    if (!(kKeep && first_late && j + 1 == cnt)) load_page(twin, cur, ids ? ids[i] : i, lane, t, c);
     PageRuns P;
     scan_page(t, c, lane, P);
     emit_bytes(P, c, lane, data + excl + tab[j]);
