@@ -470,18 +470,34 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // that workgroup drew its ticket earlier, so it is running or done and never waits for t).
 constexpr uint32_t kSpillWGs = 1280;  // > the workgroups of this kernel one MI355X holds at once
 
-template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
+// kSolo (a release of at most kSoloUnits one-page units, one stream): ONE workgroup, a wave per
+// unit, no ticket and no workspace. The exclusive offsets come from the waves' totals through LDS
+// and one barrier instead of the look-back, and the caller's id lists are guarded in the kernel
+// (g, as diff_prep_kernel does), so the release is this one launch (config 5's rounds).
+constexpr uint32_t kSoloUnits = 16;
+
+__device__ __forceinline__ uint64_t guarded_id(const uint32_t* __restrict__ ids, uint64_t i,
+                                               uint64_t n_pages, uint32_t& bad) {
+  const uint32_t p = ids[i];
+  bad |= p >= n_pages ? 1u : 0u;
+  return p < n_pages ? p : n_pages;
+}
+
+template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0,
+          bool kSolo = false>
+__global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool,
-    const uint32_t* __restrict__ tids) {
+    const uint32_t* __restrict__ tids, const IdGuard g) {
   static_assert(kU <= 64 && (kU & (kU - 1)) == 0, "unit size");
+  static_assert(!kSolo || (kU == 1 && kSpill == 0), "solo: one-page units, no spill slot");
+  constexpr uint32_t kNW = kSolo ? kSoloUnits : 4;  // waves per workgroup
   __shared__ uint32_t sel_tab[16];
-  __shared__ uint32_t ent_all[4][64];
-  __shared__ uint4 dat_all[4][64];
-  __shared__ __attribute__((aligned(16))) uint32_t buf_all[4][kBuf / 4];
-  __shared__ uint32_t tab_all[4][2 * kU + 1];  // [0, kU]: record offsets; [kU+1, 2kU]: LDS source
+  __shared__ uint32_t ent_all[kNW][64];
+  __shared__ uint4 dat_all[kNW][64];
+  __shared__ __attribute__((aligned(16))) uint32_t buf_all[kNW][kBuf / 4];
+  __shared__ uint32_t tab_all[kNW][2 * kU + 1];  // [0, kU]: record offsets; [kU+1, 2kU]: LDS source
   if (threadIdx.x < 16) sel_tab[threadIdx.x] = compact_sel(threadIdx.x);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -493,7 +509,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   // one ticket per workgroup (a single counter takes ~88 returning atomics per us, so per-wave
   // tickets would queue on it); unit = 4 * ticket + wave
   __shared__ uint32_t ticket, done_waves;
-  if (threadIdx.x == 0) {
+  if (!kSolo && threadIdx.x == 0) {
     const uint32_t t = atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u);
     ticket = t;
     done_waves = 0;
@@ -505,8 +521,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     }
   }
   __syncthreads();
-  const uint64_t u = (uint64_t)ticket * 4 + wave;
-  if (u >= nunits) return;  // wave-uniform: the grid's spare waves
+  const uint64_t u = kSolo ? (uint64_t)wave : (uint64_t)ticket * 4 + wave;
+  if (u >= nunits) return;  // wave-uniform: the grid's spare waves (none in a solo launch)
+  uint32_t bad_id = 0;      // kSolo: a caller id out of range
   // the output stream this unit belongs to (units never straddle two of them) and its place in it
   uint32_t d = 0;
 #pragma unroll
@@ -530,10 +547,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   uint32_t my_size = 0;   // lane j: record size of page j
   uint32_t my_src = 0;    // lane j: LDS byte offset of page j's record
   uint4 t[4], c[4];
-  uint64_t pj = ids ? ids[i0] : i0;
+  uint64_t pj = ids ? (kSolo && g.ids ? guarded_id(ids, i0, g.n_pages, bad_id) : ids[i0]) : i0;
   load_page(twin, cur, pj, lane, t, c);
   for (uint32_t j = 0; j < cnt; ++j) {
-    const uint64_t pt_ = kApply ? (tids ? (uint64_t)tids[i0 + j] : pj) : 0;  // page at target
+    const uint64_t pt_ =
+        kApply ? (tids ? (kSolo && g.tids ? guarded_id(tids, i0 + j, g.n_pages, bad_id)
+                                          : (uint64_t)tids[i0 + j])
+                       : pj)
+               : 0;  // page at target
     uint32_t m[4], D = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -605,11 +626,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
   // ---- publish the aggregate, look back for the exclusive offset, publish the inclusive prefix
   const uint32_t incl = wave_incl_sum(my_size);  // lanes >= cnt hold 0
   const uint32_t agg = lane_bcast(incl, 63);
-  if (lane == 0)
+  uint64_t excl = 0;
+  if (kSolo) {  // the waves' totals through LDS (every wave of the launch gets here)
+    __shared__ uint32_t solo_agg[kSoloUnits];
+    if (lane == 0) solo_agg[wave] = agg;
+    __syncthreads();
+    for (uint32_t w = 0; w < wave; ++w) excl += solo_agg[w];
+    if (g.err && __ballot(bad_id != 0) && lane == 0) atomicOr(g.err, 8u);
+  }
+  if (!kSolo && lane == 0)
     __hip_atomic_store(status + u, (u == u0 ? kStIncl : kStAgg) | agg, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t excl = 0;
-  if (u > u0) {
+  if (!kSolo && u > u0) {
     int64_t pos = (int64_t)u - 1;
     for (;;) {
       const int64_t q = pos - (int64_t)lane;
@@ -696,7 +724,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWaves))) v
     rem &= rem - 1;
     if (excl + tab[j + 1] > cap) continue;
     const uint64_t i = i0 + j;
-    if (!(kKeep && first_late && j + 1 == cnt)) load_page(twin, cur, ids ? ids[i] : i, lane, t, c);
+    if (!(kKeep && first_late && j + 1 == cnt)) {
+      uint32_t unused = 0;
+      load_page(twin, cur,
+                ids ? (kSolo && g.ids ? guarded_id(ids, i, g.n_pages, unused) : ids[i]) : i, lane,
+                t, c);
+    }
     PageRuns P;
     scan_page(t, c, lane, P);
     emit_bytes(P, c, lane, data + excl + tab[j]);
@@ -1579,11 +1612,21 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
   const uint64_t wgs = (nunits + 3) / 4;
   if (spill && (wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill > spill_pool_bytes(n))
     return hipErrorInvalidValue;
+  uint32_t* gen = spill ? reinterpret_cast<uint32_t*>(ws + status_end) : nullptr;
+  if (v == 8 && sp.G == 1 && nunits <= kSoloUnits) {
+    // one workgroup, no workspace: the caller's lists are guarded by the kernel itself
+    const IdGuard g = guard ? *guard : IdGuard{};
+    ProfScope ps(prof, GDSM_PROF_DIFF, s);
+    auto kern = target ? diff_single_kernel<1, 4096, 4, true, 0, true>
+                       : diff_single_kernel<1, 4096, 4, false, 0, true>;
+    hipLaunchKernelGGL(kern, dim3(1), dim3((unsigned)(64 * nunits)), 0, s, twin, cur, ids, sp,
+                       reinterpret_cast<uint64_t*>(ws), target, nullptr, nullptr, tids, g);
+    return hipGetLastError();
+  }
   // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
   // (outside the timed kernel), and the caller's lists checked, in one prep launch
-  uint32_t* gen = spill ? reinterpret_cast<uint32_t*>(ws + status_end) : nullptr;
+  IdGuard g{};
   {
-    IdGuard g{};
     if (guard) {
       g = *guard;
       if (g.ids) ids = g.safe_ids;
@@ -1616,7 +1659,7 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,
-                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids);
+                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{});
   return hipGetLastError();
 }
 
