@@ -1355,7 +1355,8 @@ __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ t
 //   7  16 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
 //   8  1 page per wave (automatic for lists of <= kDiffTiny pages: a wave per page, and a dense
 //      page's record, ~4.6 KiB for a page of rewritten doubles, fits the LDS buffer instead of
-//      being re-read as the second page of a 2-page unit)
+//      being re-read as the second page of a 2-page unit); up to kSoloUnits pages of one stream
+//      it is the one-workgroup kSolo launch
 // Measurement-only kernels (invalid output) are not part of the library.
 static int diff_variant_from_env() {
   const char* e = getenv("GDSM_DIFF_VARIANT");
