@@ -102,6 +102,8 @@ int check_and_clear_err(gdsm_ctx* ctx) {
   GDSM_TRY(hipMemcpyAsync(&h, ctx->err, 4, hipMemcpyDeviceToHost, ctx->stream));
   GDSM_TRY(hipMemsetAsync(ctx->err, 0, 4, ctx->stream));
   GDSM_TRY(hipStreamSynchronize(ctx->stream));
+  h |= ctx->err_held;
+  ctx->err_held = 0;
   if (h && getenv("GDSM_DEBUG_ERR")) fprintf(stderr, "gdsm err word 0x%x\n", h);
   // a fixed-budget exchange stream over its budget, and nothing else: the release can be redone
   // with exact sizes (gdsm.h GDSM_XCHG_FIXED)

@@ -17,6 +17,9 @@ struct gdsm_ctx {
   hipStream_t stream = nullptr;
   uint8_t* arena[3] = {nullptr, nullptr, nullptr};
   uint32_t* err = nullptr;       // device error word (bit 0: malformed record, bit 1: bad events)
+  // error bits taken off the device word by a call that must not see them (gdsm_coherence_notify
+  // and an earlier batch's rejection); gdsm_sync reports them with the device word's
+  uint32_t err_held = 0;
   uint8_t* diff_ws = nullptr;    // diff workspace
   uint64_t diff_ws_bytes = 0;
   uint8_t* coh_ws = nullptr;

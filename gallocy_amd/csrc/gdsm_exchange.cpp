@@ -699,10 +699,11 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
   GDSM_TRY(hipMemcpyAsync(h + 4 * G + 1, ctx->err, 4, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipStreamSynchronize(s));
   const uint64_t distinct = local ? 0 : h[4 * G];
-  // an error bit an earlier batch left (kept for gdsm_sync, restored below): only this fold's
-  // rejection may refuse the call
+  // an error bit an earlier batch left: only this fold's rejection may refuse the call, so the bit
+  // moves to the host-held word, which gdsm_sync reports whatever way this call ends
   const uint32_t stale = reinterpret_cast<uint32_t*>(h + 4 * G + 1)[0] & gdsm::detail::kErrEvents;
   if (stale) {
+    ctx->err_held |= stale;
     reinterpret_cast<uint32_t*>(h + 4 * G + 1)[0] &= ~stale;
     GDSM_TRY(hipMemcpyAsync(ctx->err, h + 4 * G + 1, 4, hipMemcpyHostToDevice, s));
   }
@@ -714,7 +715,9 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
   GDSM_TRY(hipStreamSynchronize(s));
   uint64_t bound = 0;
   for (int p = 0; p < G; ++p) bound += h[G + p];
-  // this home sends at most one notice per (distinct page of its batch, node)
+  // this home sends at most one notice per (distinct page of its batch, node): the staging is
+  // sized for that worst case (G notices of 8 B per distinct page) before the agreement, since
+  // the real count is known only after the fold; it only grows
   if (!local) local = ensure(ctx, &c->staging, &c->staging_bytes, 8 * G * (distinct ? distinct : 1));
   uint64_t verdict = (local ? kVerdictLocal : 0u) | (bound > cap ? 1u : 0u);
   rc = xp->agree_max(&verdict, s);
@@ -737,11 +740,6 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
   GDSM_TRY(hipMemcpyAsync(h + 4 * G, ctx->err, 4, hipMemcpyDeviceToHost, s));
   GDSM_TRY(hipStreamSynchronize(s));
   const uint32_t err_now = reinterpret_cast<uint32_t*>(h + 4 * G)[0];
-  if (stale) {  // the earlier batch's bit goes back for gdsm_sync to report
-    reinterpret_cast<uint32_t*>(h + 4 * G + 1)[0] = err_now | stale;
-    GDSM_TRY(hipMemcpyAsync(ctx->err, h + 4 * G + 1, 4, hipMemcpyHostToDevice, s));
-    GDSM_TRY(hipStreamSynchronize(s));
-  }
   std::vector<uint64_t> off(G + 1, 0);
   uint64_t sent = 0;
   for (int p = 0; p < G; ++p) {
@@ -750,7 +748,7 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* c, const uint64_t* batch, ui
   }
   // some home's batch was rejected by this fold (its page table is unspecified): all refuse
   verdict = (local ? kVerdictLocal : 0u) | ((err_now & gdsm::detail::kErrEvents) ? 1u : 0u) |
-            (off[G] > cap || sent > 8 * G * (distinct ? distinct : 1) ? 1u : 0u);
+            (off[G] > cap || sent > (uint64_t)G * (distinct ? distinct : 1) ? 1u : 0u);
   rc = xp->agree_max(&verdict, s);
   if (rc) return rc;
   if (verdict & kVerdictLocal) return refused(local);

@@ -8,15 +8,20 @@
 //      gallocy/allocators/internal.cpp:31-57);
 //   2. the three test/test_diff.cpp bodies (DiffTinyTest :10-20, DiffGeneral_1 :23-35,
 //      DiffGeneral_2 :38-57), linked against libgdsm's diff() (mangled _Z4diffPKcmRPcS0_mS2_);
-//   3. every output checked to lie inside the internal heap's 32 MiB zone
-//      (get_heap_location(PURPOSE_INTERNAL_HEAP), utils/constants.cpp:36-54), to have an
+//   3. every output checked to lie inside the internal heap's 32 MiB zone, to have an
 //      internal_malloc_usable_size covering the string, and released with internal_free; the
 //      freed space is handed out again by the next internal_malloc (first-fit reuse,
 //      test/test_internal_allocator.cpp:105-138).
+// The zone is taken from what the heap actually mapped: SourceMmapHeap passes
+// get_heap_location(PURPOSE_INTERNAL_HEAP) (utils/constants.cpp:36-54) to mmap only as a hint,
+// without MAP_FIXED (heaplayers/source.h:21-22), so with ASLR off (brk there) or another mapping in
+// the way the kernel places the zone elsewhere. The mapping that holds the heap's first block,
+// read from /proc/self/maps, is the zone.
 // Prints "ok <checks>" and exits 0, or names the failing check and exits 1.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cinttypes>
 
 #include "gallocy/allocators/internal.h"
 #include "gallocy/utils/constants.h"
@@ -38,10 +43,30 @@ static int g_checks = 0;
     }                                                                       \
   } while (0)
 
+static uintptr_t g_zone_lo = 0, g_zone_hi = 0;
+
+// [lo, hi) of the mapping in /proc/self/maps that holds p; false if none does
+static bool mapping_of(const void* p, uintptr_t* lo, uintptr_t* hi) {
+  FILE* f = fopen("/proc/self/maps", "r");
+  if (!f) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  char line[512];
+  bool found = false;
+  while (!found && fgets(line, sizeof line, f)) {
+    uintmax_t l = 0, h = 0;
+    if (sscanf(line, "%jx-%jx", &l, &h) == 2 && a >= l && a < h) {
+      *lo = (uintptr_t)l;
+      *hi = (uintptr_t)h;
+      found = true;
+    }
+  }
+  fclose(f);
+  return found;
+}
+
 static bool in_internal_zone(const void* p) {
-  const char* base = static_cast<const char*>(get_heap_location(PURPOSE_INTERNAL_HEAP));
-  const char* q = static_cast<const char*>(p);
-  return q >= base && q < base + ZONE_SZ;
+  const uintptr_t q = reinterpret_cast<uintptr_t>(p);
+  return q >= g_zone_lo && q < g_zone_hi;
 }
 
 static void check_owned(char* s) {
@@ -51,6 +76,16 @@ static void check_owned(char* s) {
 }
 
 int main() {
+  {  // the zone: the one shared anonymous mapping of ZONE_SZ bytes that holds a heap block
+    void* first = internal_malloc(16);
+    CHECK(first != nullptr);
+    uintptr_t lo = 0, hi = 0;
+    CHECK(mapping_of(first, &lo, &hi));
+    CHECK(hi - lo >= (uintptr_t)ZONE_SZ && hi - lo < (uintptr_t)ZONE_SZ + 4096);
+    g_zone_lo = lo;
+    g_zone_hi = hi;
+    internal_free(first);
+  }
   CHECK(gdsm_set_allocator(internal_malloc, internal_free) == 0);
 
   {  // test_diff.cpp:10-20 DiffTinyTest

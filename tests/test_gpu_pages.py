@@ -812,15 +812,18 @@ def test_diff_split_equals_per_range_diffs(variant):
         L.gdsm_tune(b"diff_variant", 0)
 
 
-def test_diff_apply_ids_applies_at_other_indices():
+@pytest.mark.parametrize("m", [700, 12, 1])
+def test_diff_apply_ids_applies_at_other_indices(m):
     """gdsm_diff_apply_ids: list entry i (page ids[i] of TWIN / CURRENT) is applied to page
     target_ids[i] of REPLICA by the diff kernel itself, the stream being the same as gdsm_diff's;
-    an out-of-range target id writes nothing and is reported by the next sync."""
+    an out-of-range target id writes nothing and is reported by the next sync. m = 700 takes the
+    grid with its separate id check; m <= 16 the one-workgroup release that guards both lists
+    inside the kernel."""
     n = 3000
     rng = np.random.default_rng(77)
     twin, cur = oracle.gen_pages(n, seed=77, mode=1, ppm=100000)
-    ids = rng.choice(n, 700, replace=False).astype(np.uint32)
-    tids = rng.permutation(n)[:700].astype(np.uint32)
+    ids = rng.choice(n, m, replace=False).astype(np.uint32)
+    tids = rng.permutation(n)[:m].astype(np.uint32)
     with ga.Context(n) as c:
         base = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
         c.upload("twin", twin)
@@ -838,15 +841,18 @@ def test_diff_apply_ids_applies_at_other_indices():
         want[tids] = cur[ids]
         assert np.array_equal(c.download("replica"), want)
         bad = tids.copy()
-        bad[5] = n + 3
+        k = min(5, m - 1)
+        bad[k] = n + 3
         c.upload("replica", rep)
-        c.diff(c.ids(ids), apply_to="replica", target_ids=c.ids(bad))
+        r2 = c.diff(c.ids(ids), apply_to="replica", target_ids=c.ids(bad))
         with pytest.raises(GdsmError) as ei:
             c.sync()
         assert ei.value.errno == 22
+        h2 = r2.to_host()  # the stream is still gdsm_diff's
+        assert np.array_equal(h2.rec_off, ro) and np.array_equal(h2.data[:int(ro[-1])], data)
         got = c.download("replica")
-        keep = np.ones(700, bool)
-        keep[5] = False
+        keep = np.ones(m, bool)
+        keep[k] = False
         want2 = rep.copy()
         want2[tids[keep]] = cur[ids[keep]]
         assert np.array_equal(got, want2)

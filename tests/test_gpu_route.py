@@ -352,3 +352,57 @@ def test_notify_ignores_a_stale_event_error_bit():
             c.close()
         for s in shards:
             s.ctx.close()
+
+
+@pytest.mark.parametrize("refusal", ["enospc", "enomem"])
+def test_refused_notify_keeps_a_stale_event_error_bit(refusal):
+    """The stale bit survives a notify that is REFUSED: every rank gets -ENOSPC (a notice buffer
+    too small) or the failing rank -ENOMEM and the others -ECANCELED (a workspace growth forced to
+    fail on rank 0), and the next gdsm_sync on rank 0 still reports the earlier batch's
+    rejection (-EINVAL) while rank 1's is clean."""
+    import ctypes as C
+    G, Z = 2, 2000
+    rng = np.random.default_rng(17)
+    shards = [Shard(r, G, Z) for r in range(G)]
+    comms = exchange.Comm.loopback([s.ctx for s in shards])
+    lib = ga.gdsm.lib()
+    try:
+        s0 = shards[0]
+        bad = np.array([(5 << 4) | 1, (3 << 4)], np.uint64)
+        evb, tb = s0.ctx.buffer(16).upload(bad), s0.ctx.buffer(80)
+        stamped = stamped_batch(rng, G, Z, 1000)
+        cap = sum(len(x) for x in stamped) + 1
+        bufs = [(s.ctx.buffer(8 * len(stamped[r])).upload(stamped[r]), s.ctx.buffer(8 * cap),
+                 s.ctx.buffer(8 * (Z + 1)), s.ctx.buffer(80)) for r, s in enumerate(shards)]
+        nbs = [0] * G
+
+        def route(r):
+            ev, bt, _, _ = bufs[r]
+            nbs[r] = exchange.route_events(shards[r].ctx, comms[r], ev.ptr, len(stamped[r]), Z,
+                                           bt.ptr, cap)
+        run_ranks(G, route)
+        assert lib.gdsm_coherence_batch_async(s0.ctx.handle, evb.ptr, 2, tb.ptr) == 0
+        if refusal == "enomem":
+            assert lib.gdsm_debug_fail_alloc(s0.ctx.handle, 1) == 0
+        ncap = 1 if refusal == "enospc" else Z + 1
+        rcs = [None] * G
+
+        def notify(r):
+            s, c = shards[r], comms[r]
+            _, bt, nt, tot = bufs[r]
+            nn = C.c_uint64(0)
+            rcs[r] = lib.gdsm_coherence_notify(s.ctx.handle, c.handle, bt.ptr, nbs[r], s.base,
+                                               tot.ptr, nt.ptr, ncap, C.byref(nn))
+        run_ranks(G, notify)
+        want = ([-errno.ENOSPC] * G if refusal == "enospc"
+                else [-errno.ENOMEM, -errno.ECANCELED])
+        assert rcs == want
+        assert lib.gdsm_debug_fail_alloc(s0.ctx.handle, 0) == 0
+        assert lib.gdsm_sync(s0.ctx.handle) == -errno.EINVAL  # the earlier batch's error
+        assert lib.gdsm_sync(shards[1].ctx.handle) == 0
+        assert lib.gdsm_sync(s0.ctx.handle) == 0  # reported once
+    finally:
+        for c in comms:
+            c.close()
+        for s in shards:
+            s.ctx.close()
