@@ -77,6 +77,14 @@ int64_t or_check_stream(const uint64_t* rec_off, const uint8_t* data, uint64_t f
 int or_bench_coherence(const uint64_t* events, const uint64_t* page_off, uint64_t n_pages,
                        uint32_t n_nodes, double seconds, int threads, uint64_t* done,
                        double* elapsed);
+/* bench.py's config-5 CPU baseline (gdsm_oracle_bench.c): the mmult trace's round loop on one
+ * thread, timed in C. */
+int or_bench_mmult(uint32_t* state, uint32_t* faults, uint64_t zone_pages, uint32_t nodes,
+                   uint8_t* twin, uint8_t* cur, uint8_t* rep, uint64_t rounds,
+                   const uint64_t* events, const uint64_t* ev_off, const uint32_t* ids,
+                   const uint32_t* home, const uint64_t* ids_off, const uint64_t* row_dst,
+                   const uint32_t* row_src, const uint64_t* row_off, const uint8_t* rowvals,
+                   uint64_t row_bytes, uint64_t* totals, double* elapsed);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@
 #include <omp.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "gdsm_oracle.h"
 
@@ -153,4 +154,58 @@ int64_t or_check_stream(const uint64_t* rec_off, const uint8_t* data, uint64_t f
     free(buf);
   }
   return failed ? -2 : bad;
+}
+
+/* Config 5 (the test_mmult trace) on one host thread, the whole round loop in C: per round the
+ * coherence batch (or_coherence), the twin of the pages the round writes, the row writes, the diff
+ * of those pages (or_diff_pages) and its apply to the home copy (or_apply). `nodes` node views
+ * of the zone sit side by side in twin / cur (page t * zone_pages + p). The plan is precomputed
+ * by the caller (bench.py): round r's events are events[ev_off[r], ev_off[r+1]), its written
+ * pages ids / home[ids_off[r], ids_off[r+1]) (node view index / home copy index), its row writes
+ * (cur byte offset row_dst[k] <- rowvals row row_src[k], row_bytes each) k in
+ * [row_off[r], row_off[r+1]). Timed with CLOCK_MONOTONIC around the loop only; totals are the
+ * sums over rounds. Returns 0, -12 (allocation) or the first failing call's code. */
+
+int or_bench_mmult(uint32_t* state, uint32_t* faults, uint64_t zone_pages, uint32_t nodes,
+                   uint8_t* twin, uint8_t* cur, uint8_t* rep, uint64_t rounds,
+                   const uint64_t* events, const uint64_t* ev_off, const uint32_t* ids,
+                   const uint32_t* home, const uint64_t* ids_off, const uint64_t* row_dst,
+                   const uint32_t* row_src, const uint64_t* row_off, const uint8_t* rowvals,
+                   uint64_t row_bytes, uint64_t* totals, double* elapsed) {
+  uint64_t max_ids = 0;
+  for (uint64_t r = 0; r < rounds; ++r)
+    if (ids_off[r + 1] - ids_off[r] > max_ids) max_ids = ids_off[r + 1] - ids_off[r];
+  /* the largest record: 4 + 2048 run headers + 4096 payload bytes */
+  const uint64_t cap = (max_ids ? max_ids : 1) * (4 + 4 * 2048 + OR_PAGE_SZ);
+  uint64_t* rec_off = malloc((max_ids + 1) * sizeof(uint64_t));
+  uint8_t* data = malloc(cap);
+  if (!rec_off || !data) {
+    free(rec_off);
+    free(data);
+    return -12;
+  }
+  memset(rec_off, 0, (max_ids + 1) * sizeof(uint64_t));  /* first touches outside the clock */
+  memset(data, 0, cap);
+  for (int k = 0; k < 10; ++k) totals[k] = 0;
+  uint64_t tot[10];
+  int rc = 0;
+  struct timespec a, b;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (uint64_t r = 0; r < rounds && !rc; ++r) {
+    rc = or_coherence(state, faults, zone_pages, nodes, events + ev_off[r],
+                      ev_off[r + 1] - ev_off[r], tot);
+    for (int k = 0; k < 10; ++k) totals[k] += tot[k];
+    const uint64_t n = ids_off[r + 1] - ids_off[r];
+    const uint32_t* id = ids + ids_off[r];
+    or_twin(twin, cur, id, n);
+    for (uint64_t k = row_off[r]; k < row_off[r + 1]; ++k)
+      memcpy(cur + row_dst[k], rowvals + (uint64_t)row_src[k] * row_bytes, row_bytes);
+    or_diff_pages(twin, cur, id, n, rec_off, data, cap);
+    if (!rc) rc = or_apply(rep, home + ids_off[r], n, rec_off, data);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  *elapsed = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+  free(rec_off);
+  free(data);
+  return rc;
 }

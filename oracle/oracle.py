@@ -39,6 +39,8 @@ def lib():
                                           C.POINTER(C.c_int)]
         L.or_bench_coherence.argtypes = [C.c_void_p, C.c_void_p, u64, C.c_uint32, C.c_double,
                                          C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
+        L.or_bench_mmult.argtypes = [vp, vp, u64, C.c_uint32, vp, vp, vp, u64, vp, vp, vp, vp,
+                                     vp, vp, vp, vp, vp, u64, vp, C.POINTER(C.c_double)]
         L.or_check_stream.restype = C.c_int64
         L.or_check_stream.argtypes = [vp, vp, u64, u64, u64, C.c_int, C.c_uint32, C.c_int]
         _lib = L
@@ -160,6 +162,25 @@ def bench_diff_apply(n, mode, ppm, seed, seconds, threads):
     if rc:
         raise OSError(-rc, "or_bench_diff_apply")
     return pages.value, dt.value, bool(ok.value)
+
+
+def bench_mmult(state, faults, nodes, twin, cur, rep, plan, rowvals):
+    """bench.py's config-5 CPU baseline: the whole round loop in C on one thread
+    (or_bench_mmult). plan = dict of flat arrays events / ev_off / ids / home / ids_off / row_dst
+    / row_src / row_off. Returns (seconds, totals[10])."""
+    a = {k: np.ascontiguousarray(v) for k, v in plan.items()}
+    rv = np.ascontiguousarray(rowvals, np.uint8)
+    tot = np.zeros(10, np.uint64)
+    dt = C.c_double()
+    rounds = len(a["ev_off"]) - 1
+    rc = lib().or_bench_mmult(_p(state), _p(faults), len(state), nodes, _p(twin), _p(cur),
+                              _p(rep), rounds, _p(a["events"]), _p(a["ev_off"]), _p(a["ids"]),
+                              _p(a["home"]), _p(a["ids_off"]), _p(a["row_dst"]),
+                              _p(a["row_src"]), _p(a["row_off"]), _p(rv), rv.shape[1], _p(tot),
+                              C.byref(dt))
+    if rc:
+        raise RuntimeError(f"or_bench_mmult: {rc}")
+    return dt.value, tot
 
 
 def bench_coherence(counts, events, seconds, threads, n_nodes=8):

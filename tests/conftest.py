@@ -15,4 +15,5 @@ def pytest_configure(config):
 def golden():
     import numpy as np
     g = ROOT / "tests" / "golden"
-    return {k: np.load(g / f"{k}.npz") for k in ("nw_ref", "pages", "coherence", "c1_windows")}
+    return {k: np.load(g / f"{k}.npz") for k in ("nw_ref", "pages", "coherence", "c1_windows",
+                                                   "ref_windows")}

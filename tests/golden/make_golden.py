@@ -17,6 +17,10 @@
                  alignment length, crc32 of both alignment strings, and the positions where
                  out1[i] != out2[i] (bit-packed). This pins the page diff / apply to the
                  reference itself wherever its alignment is gap-free.
+  ref_windows.npz the same for more page sets (tests/helpers.py:REF_WINDOW_SETS): 64 pages of
+                 BASELINE config 3's clustered workload, a dense set (40 % of the words
+                 rewritten) and the SPEC edge pages of pages.npz; keys '<set>_<field>'. Windows
+                 whose reference alignment has gaps keep only L and the crc32s.
   coherence.npz  a seeded event batch and its expected page table / totals from the C oracle
                  (SPEC §5, parity unpinned by the reference, which has no coherence logic).
 """
@@ -30,7 +34,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 from oracle import oracle  # noqa: E402
-from tests.helpers import c1_windows  # noqa: E402
+from tests.helpers import REF_WINDOW_SETS, c1_windows, window_pages  # noqa: E402
 
 OUT = Path(__file__).resolve().parent
 
@@ -131,9 +135,11 @@ def make_pages():
     print("pages.npz", twin.shape[0], "edge pages;", int(ro2[-1]), "B for config 1")
 
 
-def make_c1_windows():
+def _ref_windows(t, c):
+    """The pages cut into 1024-B windows, each pair aligned by the REFERENCE diff(): alignment
+    length, crc32 of both strings, gap-free flag and (gap-free windows) the bit-packed positions
+    where out1[i] != out2[i]."""
     import zlib
-    t, c = c1_windows()
     tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
     cases = [(tw[i].tobytes(), cw[i].tobytes()) for i in range(len(tw))]
     outs = oracle.ref_nw_batch(cases)
@@ -146,8 +152,25 @@ def make_c1_windows():
             gapfree[i] = True
             a, b = np.frombuffer(o1, np.uint8), np.frombuffer(o2, np.uint8)
             mask[i] = np.packbits(a != b)
-    np.savez_compressed(OUT / "c1_windows.npz", L=L, crc=crc, gapfree=gapfree, mask=mask)
-    print("c1_windows.npz", len(cases), "windows,", int(gapfree.sum()), "gap-free")
+    return {"L": L, "crc": crc, "gapfree": gapfree, "mask": mask}
+
+
+def make_c1_windows():
+    d = _ref_windows(*c1_windows())
+    np.savez_compressed(OUT / "c1_windows.npz", **d)
+    print("c1_windows.npz", len(d["L"]), "windows,", int(d["gapfree"].sum()), "gap-free")
+
+
+def make_ref_windows():
+    """ref_windows.npz: the page sets of tests/helpers.py:REF_WINDOW_SETS (config 3's clustered
+    pages, a dense set, the SPEC edge pages) through the reference diff(), keys '<set>_<field>'."""
+    golden = {"pages": np.load(OUT / "pages.npz")}
+    out = {}
+    for name in REF_WINDOW_SETS:
+        d = _ref_windows(*window_pages(name, golden))
+        out.update({f"{name}_{k}": v for k, v in d.items()})
+        print(name, len(d["L"]), "windows,", int(d["gapfree"].sum()), "gap-free")
+    np.savez_compressed(OUT / "ref_windows.npz", **out)
 
 
 def make_coherence():
@@ -168,7 +191,7 @@ def make_coherence():
 if __name__ == "__main__":
     if not oracle.ref_available():
         raise SystemExit("oracle/_ref/ref_nw_driver missing: run `make -C oracle ref` here first")
-    which = sys.argv[1:] or ["nw", "pages", "coherence", "c1_windows"]
+    which = sys.argv[1:] or ["nw", "pages", "coherence", "c1_windows", "ref_windows"]
     for w in which:
         {"nw": make_nw, "pages": make_pages, "coherence": make_coherence,
-         "c1_windows": make_c1_windows}[w]()
+         "c1_windows": make_c1_windows, "ref_windows": make_ref_windows}[w]()

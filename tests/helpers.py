@@ -54,6 +54,32 @@ def c1_windows():
     return c1_remap(t), c1_remap(c)
 
 
+# Further page sets aligned window by window by the REFERENCE diff() (tests/golden/
+# ref_windows.npz, tests/golden/make_golden.py): name -> how the pages are made.
+#   cl     BASELINE config 3's workload (SPEC §6 CLUSTERED, 100 000 ppm, bench seed 2026): 64
+#          pages from global page 5 000 000 of the 16M
+#   dense  SPEC §6 UNIFORM at 400 000 ppm (40 % of the words rewritten, >= 30 % of the bytes)
+#   edge   the SPEC edge pages of tests/golden/pages.npz (clean, all bytes, alternating bytes,
+#          first / last byte, chunk and lane edges, tail run, sparse bytes, partial words)
+REF_WINDOW_SETS = ("cl", "dense", "edge")
+CL_FIRST = 5_000_000
+
+
+def window_pages(name: str, golden=None):
+    """(twin', cur') of a reference-window set, remapped as c1_remap; window w = bytes
+    [1024 w, 1024 w + 1024) of the flat arrays."""
+    from oracle import oracle
+    if name == "cl":
+        t, c = oracle.gen_pages(64, seed=2026, mode=1, ppm=100000, first_page=CL_FIRST)
+    elif name == "dense":
+        t, c = oracle.gen_pages(16, seed=2026, mode=0, ppm=400000)
+    elif name == "edge":
+        t, c = golden["pages"]["edge_twin"], golden["pages"]["edge_cur"]
+    else:
+        raise KeyError(name)
+    return c1_remap(t), c1_remap(c)
+
+
 def runs_positions(rec_off, data, n_pages: int) -> np.ndarray:
     """bool[n_pages * 4096]: True at every byte covered by a run of the stream (SPEC §3),
     record i describing page i."""

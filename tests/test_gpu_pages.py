@@ -10,7 +10,7 @@ from gallocy_amd import _lib
 from gallocy_amd._lib import GdsmRuns
 from gallocy_amd.gdsm import GdsmError, HostRuns, Runs
 from oracle import oracle
-from tests.helpers import c1_windows, np_diff, runs_positions
+from tests.helpers import REF_WINDOW_SETS, c1_windows, np_diff, runs_positions, window_pages
 
 pytestmark = pytest.mark.gpu
 
@@ -590,6 +590,42 @@ def test_c1_windows_pinned_by_reference_diff(golden):
         rep = c.download("replica").reshape(-1, 1024)
     for w in range(len(rep)):
         assert zlib.crc32(rep[w].tobytes()) == int(g["crc"][w][1]), w
+
+
+@pytest.mark.parametrize("variant", [0, 7, 8])
+@pytest.mark.parametrize("name", REF_WINDOW_SETS)
+def test_ref_windows_pinned_by_reference_diff(name, variant, golden):
+    """Config 3's clustered pages, a dense set and the SPEC edge pages pinned to the REFERENCE
+    diff() (gallocy/utils/diff.cpp:73-167; fixture tests/golden/ref_windows.npz from oracle/_ref):
+    for every window whose reference alignment is gap-free, {i : out1[i] != out2[i]} equals the
+    union of gdsm_diff's runs (in the default geometry, the 16-page spill geometry and the
+    one-page-per-wave geometry), and gdsm_apply of the stream to the twin gives out2 (crc32)."""
+    import zlib
+    pre = name + "_"
+    crc, gapfree, mask = (golden["ref_windows"][pre + k] for k in ("crc", "gapfree", "mask"))
+    ref = np.unpackbits(mask, axis=1).astype(bool)
+    t, cur = window_pages(name, golden)
+    n = t.shape[0]
+    L = ga.gdsm.lib()
+    L.gdsm_tune(b"diff_variant", variant)
+    try:
+        with ga.Context(n) as c:
+            c.upload("twin", t)
+            c.upload("current", cur)
+            c.upload("replica", t)
+            runs = c.diff(cap=n * 10244)
+            h = runs.to_host()
+            pos = runs_positions(h.rec_off, h.data, n).reshape(-1, 1024)
+            bad = [i for i in np.flatnonzero(gapfree) if not np.array_equal(pos[i], ref[i])]
+            assert not bad, f"windows whose runs differ from the reference alignment: {bad[:8]}"
+            c.apply(runs)
+            c.sync()
+            rep = c.download("replica").reshape(-1, 1024)
+    finally:
+        L.gdsm_tune(b"diff_variant", 0)
+    for w in np.flatnonzero(gapfree):
+        assert zlib.crc32(rep[w].tobytes()) == int(crc[w][1]), w
+    assert np.array_equal(rep.reshape(n, 4096), cur)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])

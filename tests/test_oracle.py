@@ -10,8 +10,8 @@ import numpy as np
 import pytest
 
 from oracle import oracle
-from tests.helpers import (c1_windows, hash3, np_diff, np_runs, py_coherence, runs_positions,
-                           zipf_counts)
+from tests.helpers import (REF_WINDOW_SETS, c1_windows, hash3, np_diff, np_runs, py_coherence,
+                           runs_positions, window_pages, zipf_counts)
 
 
 # ---------------------------------------------------------------- NW (reference diff())
@@ -220,6 +220,40 @@ def test_c1_windows_pinned_by_reference_diff(golden):
     for i in range(0, 256, 32):
         o1, o2 = oracle.nw_diff(tw[i].tobytes(), cw[i].tobytes())
         assert [zlib.crc32(o1), zlib.crc32(o2)] == g["crc"][i].tolist()
+
+
+@pytest.mark.parametrize("name", REF_WINDOW_SETS)
+def test_ref_windows_pinned_by_reference_diff(name, golden):
+    """More page sets pinned to the REFERENCE diff() (gallocy/utils/diff.cpp:73-167 through
+    oracle/_ref; fixture tests/golden/ref_windows.npz): config 3's clustered pages, a dense set
+    (>= 30 % of the bytes changed) and the SPEC edge pages, remapped and cut into 1024-B windows
+    (test/test_diff.cpp:38-57 shape). Every gap-free window's {i : out1[i] != out2[i]} equals the
+    positions the oracle's runs cover, and its out1 / out2 are the window's twin / current bytes
+    (crc32); the oracle's apply gives out2. Windows whose reference alignment has gaps (it slid
+    a changed run along a shifted match) are pinned through the oracle's NW restatement: same
+    length and crc32 as the reference's."""
+    import zlib
+    pre = name + "_"
+    L, crc, gapfree, mask = (golden["ref_windows"][pre + k] for k in ("L", "crc", "gapfree", "mask"))
+    t, c = window_pages(name, golden)
+    n = t.shape[0]
+    tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+    assert len(L) == len(tw) and gapfree.sum() >= len(tw) - 8
+    if name == "dense":
+        assert (t != c).mean() >= 0.30
+    ro, data = oracle.diff_pages(t, c)
+    pos = runs_positions(ro, data, n).reshape(-1, 1024)
+    ref = np.unpackbits(mask, axis=1).astype(bool)
+    for i in np.flatnonzero(gapfree):
+        assert [zlib.crc32(tw[i].tobytes()), zlib.crc32(cw[i].tobytes())] == crc[i].tolist(), i
+        assert np.array_equal(pos[i], ref[i]), i
+    assert ref[gapfree].any(axis=1).sum() > (4 if name == "edge" else len(tw) // 2)
+    rep = t.copy()
+    assert oracle.apply(rep, ro, data) == 0
+    assert np.array_equal(rep, c)
+    for i in np.flatnonzero(~gapfree):
+        o1, o2 = oracle.nw_diff(tw[i].tobytes(), cw[i].tobytes())
+        assert len(o1) == L[i] and [zlib.crc32(o1), zlib.crc32(o2)] == crc[i].tolist(), i
 
 
 def test_coherence_rejects_node_outside_the_table():
