@@ -84,6 +84,10 @@ def parse():
     ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
     ap.add_argument("--coh-nodes", type=int, default=8,
                     help="coherence: DSM nodes of the batch (BASELINE config 4: 8)")
+    ap.add_argument("--deadline", type=float, default=300.0,
+                    help="N > 1: seconds each phase (setup + first release, the timed releases) "
+                         "may take before a rank exits non-zero (a peer died or hangs; "
+                         "exchange.Watchdog); 0 = off")
     return ap.parse_args()
 
 
@@ -254,9 +258,28 @@ def read_coh_traffic(dist: str, pages: int, events: int):
     return None, None
 
 
-def ranks_setup():
+def watchdog(args, rank: int, world: int, what: str):
+    """N > 1: (re)arms the rank's deadline for the phase `what` (exchange.Watchdog: a rank
+    blocked on a dead or hung peer exits non-zero instead of hanging the job)."""
+    global WATCHDOG
+    if world <= 1 or args.deadline <= 0:
+        return
+    if WATCHDOG is None:
+        from gallocy_amd.exchange import Watchdog
+        WATCHDOG = Watchdog(rank)
+    WATCHDOG.arm(args.deadline, what)
+    hang = os.environ.get("GDSM_BENCH_HANG_RANK")  # test hook: this rank hangs in its setup
+    if hang is not None and int(hang) == rank and what.startswith("setup"):
+        log(f"bench.py: rank {rank} hangs (GDSM_BENCH_HANG_RANK)")
+        time.sleep(1e9)
+
+
+WATCHDOG = None
+
+
+def ranks_setup(args):
     """(rank, world, local device) under a launcher (gloo carries barriers and the max-over-ranks
-    time; nothing of the data path), or (0, 1, 0)."""
+    time; nothing of the data path), or (0, 1, 0). N > 1: the whole run has --deadline."""
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -265,6 +288,7 @@ def ranks_setup():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
+        watchdog(args, rank, world, "setup and run")
     return rank, world, local
 
 
@@ -295,7 +319,7 @@ def run_coherence(args):
 
     import gallocy_amd as ga
     from gallocy_amd.workloads import event_counts
-    rank, world, local = ranks_setup()
+    rank, world, local = ranks_setup(args)
     if args.coh_pages % world or args.events % world:
         raise SystemExit("--coh-pages and --events must be multiples of the GPU count")
     n, E = args.coh_pages // world, args.events // world
@@ -394,7 +418,7 @@ def run_twin(args):
     import torch
 
     import gallocy_amd as ga
-    rank, world, local = ranks_setup()
+    rank, world, local = ranks_setup(args)
     n = args.pages or (16 << 20)
     mode = ga.GEN_UNIFORM if (args.mode or "uniform") == "uniform" else ga.GEN_CLUSTERED
     ppm = args.ppm if args.ppm is not None else (10000 if mode == ga.GEN_UNIFORM else 100000)
@@ -581,6 +605,7 @@ def run_mmult_ranks(args, rank: int, world: int):
     local = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist.init_process_group("gloo")
+    watchdog(args, rank, world, "setup and run")
     R = MmultRankReplay(rank, world, ndim=args.ndim, seed=args.seed, device=local)
     dist.barrier()
     dt = R.run()
@@ -699,7 +724,7 @@ def run_nw(args):
 
     import gallocy_amd as ga
     from gallocy_amd import _lib
-    rank, world, local = ranks_setup()
+    rank, world, local = ranks_setup(args)
     n, ln = args.nw_pairs, 4096
     rng = np.random.default_rng(args.seed + rank)
     a = rng.integers(0, 256, (n, ln), dtype=np.uint8)
@@ -846,6 +871,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("gloo")
+        watchdog(args, rank, world, "setup: communicator and the first release")
     import gallocy_amd as ga
     from gallocy_amd import exchange
 
@@ -941,6 +967,7 @@ def main():
     # optionally the other mode first, for reference, then the measured run (same K steps); by
     # default only the measured mode runs, so a rocprofv3 summary of this command averages the
     # same launches the HIP events time
+    watchdog(args, rank, world, "timed releases")
     dt_other = timed(not pipelined, False)[0] if args.compare_overlap else None
     dt, prof = timed(pipelined, True)
     # The xGMI link alone: the same releases again (untimed for `value`) with GDSM_XCHG_TIMED, a

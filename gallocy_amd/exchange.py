@@ -18,6 +18,10 @@ home (send_ids). Protocol per release (gdsm_exchange; `GlooTransport` restates i
 from __future__ import annotations
 
 import ctypes as C
+import os
+import sys
+import threading
+import time
 from errno import EIO, EOVERFLOW
 
 import numpy as np
@@ -92,17 +96,83 @@ class GlooTransport:
         return out
 
 
+# ---------------------------------------------------------------- deadlines
+class Watchdog:
+    """Ends the process when a phase of a multi-rank run overruns its deadline: a peer that died
+    or hangs leaves the others blocked inside a collective (ncclCommInitRank, an RCCL group, a
+    gloo barrier) with no error to return, so the launcher would only ever see a timeout. A
+    daemon thread prints which phase overran to stderr and calls os._exit(code): the process
+    ends non-zero, and torch.distributed.run then stops the other ranks. Nothing is re-executed
+    (a process that has touched the GPU must never exec).
+
+    arm(seconds, what) (re)starts the clock for a phase; disarm() stops it. GDSM_DEADLINE_S
+    overrides the seconds of every phase (0 = off)."""
+
+    def __init__(self, rank: int = 0, code: int = 3):
+        self.rank, self.code = rank, code
+        self._cv = threading.Condition()
+        self._due = None
+        self._what = ""
+        self._thread = None
+
+    def arm(self, seconds: float, what: str):
+        env = os.environ.get("GDSM_DEADLINE_S")
+        if env is not None:
+            seconds = float(env)
+        with self._cv:
+            self._due = time.monotonic() + seconds if seconds > 0 else None
+            self._what = what
+            if self._thread is None and self._due is not None:
+                self._thread = threading.Thread(target=self._watch, name="gdsm-watchdog",
+                                                daemon=True)
+                self._thread.start()
+            self._cv.notify_all()
+        return self
+
+    def disarm(self):
+        with self._cv:
+            self._due = None
+            self._cv.notify_all()
+
+    def _watch(self):
+        with self._cv:
+            while True:
+                if self._due is None:
+                    self._cv.wait()
+                    continue
+                left = self._due - time.monotonic()
+                if left > 0:
+                    self._cv.wait(left)
+                    continue
+                msg = (f"gdsm: rank {self.rank}: deadline passed in '{self._what}' (a peer "
+                       f"died or hangs); exiting with status {self.code}")
+                print(msg, file=sys.stderr, flush=True)
+                os._exit(self.code)
+
+
 # ---------------------------------------------------------------- the GPU shard
 class Comm:
     """A communicator owned by libgdsm (gdsm_comm_*). RCCL (the product transport): bootstrapped
     with a torch.distributed group (any backend) that carries the 128-byte unique id. Loopback
     (`Comm.loopback`, tests): several ranks as threads of one process on one GPU."""
 
-    def __init__(self, ctx: gdsm.Context, rank: int, world: int, group=None, handle=None):
+    def __init__(self, ctx: gdsm.Context, rank: int, world: int, group=None, handle=None,
+                 deadline_s: float = 0):
+        """deadline_s > 0: the unique-id broadcast and gdsm_comm_init (ncclCommInitRank, which
+        blocks until every rank joins) must finish within it, else the process exits non-zero
+        (Watchdog)."""
         self.rank, self.world = rank, world
         if handle is not None:
             self.handle = handle
             return
+        wd = Watchdog(rank).arm(deadline_s, "communicator setup") if deadline_s > 0 else None
+        try:
+            self._init(ctx, rank, world, group)
+        finally:
+            if wd is not None:
+                wd.disarm()
+
+    def _init(self, ctx, rank, world, group):
         import torch
         import torch.distributed as dist
         L = gdsm.lib()

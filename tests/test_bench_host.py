@@ -1,10 +1,15 @@
 """bench.py's host-side pieces that need no GPU: the CPU baseline leg (the C oracle, one thread
 and all-core, every sample's REPLICA checked equal to CURRENT inside the leg) and the diff-stream
 payload count used for the roofline bytes."""
+from pathlib import Path
+
 import numpy as np
+import pytest
 
 import bench
 from oracle import oracle
+
+ROOT = Path(__file__).resolve().parents[1]
 
 
 def test_cpu_baseline_single_and_all_core(monkeypatch):
@@ -92,3 +97,21 @@ def test_mmult_cpu_baseline_replays_the_trace():
     out = bench.mmult_cpu_baseline(96, 3, 7)
     assert out["home_copy_equals_product"] is True
     assert out["value"] > 0 and out["unit"] == "rounds/s" and out["kind"] == "port"
+
+
+@pytest.mark.parametrize("disarm", [False, True])
+def test_watchdog_ends_the_process_or_stays_quiet(disarm):
+    """exchange.Watchdog: a phase that overruns its deadline ends the process with status 3 and
+    names the phase on stderr; a disarmed one lets the process finish normally."""
+    import subprocess
+    import sys
+    code = ("import time\nfrom gallocy_amd.exchange import Watchdog\n"
+            "w = Watchdog(rank=5).arm(0.5, 'a test phase')\n"
+            + ("w.disarm()\n" if disarm else "") + "time.sleep(3)\nprint('finished')\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=60)
+    if disarm:
+        assert r.returncode == 0 and "finished" in r.stdout
+    else:
+        assert r.returncode == 3 and "finished" not in r.stdout
+        assert "rank 5: deadline passed in 'a test phase'" in r.stderr

@@ -147,3 +147,27 @@ def test_bench_coherence_sharded_gpus_2_without_launcher():
                             "1", "--no-cpu"])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong"
     assert d["value"] > 0 and "sharded over 2 GPUs" in d["config"]["workload"]
+
+
+def test_bench_gpus_2_hung_rank_exits_nonzero_within_the_deadline():
+    """A rank that hangs in its setup (GDSM_BENCH_HANG_RANK=1, test hook) leaves its peer blocked
+    in the first release's exchange. With --deadline 20 both ranks' watchdogs end their processes
+    non-zero, torch.distributed.run stops and returns non-zero: the job ends in about the
+    deadline instead of hanging (gloo rehearsal on one GPU)."""
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(GDSM_BENCH_BACKEND="gloo", GDSM_BENCH_HANG_RANK="1")
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--total-pages", str(4 * 8192), "--no-cpu",
+                        "--deadline", "20"], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=110)
+    took = time.monotonic() - t0
+    assert r.returncode != 0
+    assert "deadline passed" in r.stderr, r.stderr[-3000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert took < 100, took
