@@ -111,7 +111,7 @@ def build_oracle(verbose: bool = False) -> None:
     """Test oracle (oracle/liboracle.so) and, when the reference tree exists, oracle/_ref."""
     targets = ["oracle"]
     if Path("/root/reference/gallocy/utils/diff.cpp").exists():
-        targets += ["ref", "caller"]
+        targets += ["ref", "caller", "layout"]
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), *targets], check=True,
                    stdout=None if verbose else subprocess.DEVNULL)
 

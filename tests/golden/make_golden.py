@@ -21,6 +21,11 @@
                  BASELINE config 3's clustered workload, a dense set (40 % of the words
                  rewritten) and the SPEC edge pages of pages.npz; keys '<set>_<field>'. Windows
                  whose reference alignment has gaps keep only L and the crc32s.
+  ref_layout.npz zone offsets of test_mmult's objects (test/test_mmult.cpp:31-37, 152-154) as
+                 the REFERENCE application heap hands them out (heaplayers/application.h:20-29
+                 layers, compiled in place into oracle/_ref/ref_layout_driver) for NDIM 4, 64,
+                 1000 and 1021, and the abort (---ENOMEM---, source.h:23-24) at NDIM 1022 with
+                 the objects allocated before it.
   coherence.npz  a seeded event batch and its expected page table / totals from the C oracle
                  (SPEC §5, parity unpinned by the reference, which has no coherence logic).
 """
@@ -173,6 +178,43 @@ def make_ref_windows():
     np.savez_compressed(OUT / "ref_windows.npz", **out)
 
 
+LAYOUT_DRIVER = ROOT / "oracle" / "_ref" / "ref_layout_driver"
+LAYOUT_NDIMS = (4, 64, 1000, 1021)
+
+
+def _layout_run(ndim):
+    import subprocess
+    r = subprocess.run([str(LAYOUT_DRIVER), str(ndim)], capture_output=True, text=True)
+    rows = {"a": [], "b": [], "c": []}
+    one = {}
+    for ln in r.stdout.splitlines():
+        f = ln.split()
+        if len(f) == 3 and f[0].endswith("_row"):
+            rows[f[0][0]].append(int(f[2]))
+        elif len(f) == 2:
+            one[f[0]] = int(f[1])
+    return r, one, rows
+
+
+def make_layout():
+    if not LAYOUT_DRIVER.exists():
+        raise SystemExit("oracle/_ref/ref_layout_driver missing: run `make -C oracle layout` first")
+    out = {}
+    for nd in LAYOUT_NDIMS:
+        r, one, rows = _layout_run(nd)
+        assert r.returncode == 0, r.stderr
+        out[f"n{nd}_rp"] = np.array([one["a_rp"], one["b_rp"], one["c_rp"]], np.int64)
+        out[f"n{nd}_rows"] = np.array([rows["a"], rows["b"], rows["c"]], np.int64)
+        out[f"n{nd}_tail"] = np.array([one["threads"], one["args"], one["zone_used_min"]], np.int64)
+    r, one, rows = _layout_run(1022)
+    assert r.returncode != 0 and "---ENOMEM---" in r.stdout, (r.returncode, r.stdout[-200:])
+    out["abort_1022"] = np.array([r.returncode, sum(len(v) for v in rows.values()) + len(one)],
+                                 np.int64)
+    np.savez_compressed(OUT / "ref_layout.npz", ndims=np.array(LAYOUT_NDIMS), **out)
+    print("ref_layout.npz", LAYOUT_NDIMS, "abort at 1022 after", int(out["abort_1022"][1]),
+          "objects, status", int(out["abort_1022"][0]))
+
+
 def make_coherence():
     rng = np.random.default_rng(11)
     n_pages = 64
@@ -191,7 +233,8 @@ def make_coherence():
 if __name__ == "__main__":
     if not oracle.ref_available():
         raise SystemExit("oracle/_ref/ref_nw_driver missing: run `make -C oracle ref` here first")
-    which = sys.argv[1:] or ["nw", "pages", "coherence", "c1_windows", "ref_windows"]
+    which = sys.argv[1:] or ["nw", "pages", "coherence", "c1_windows", "ref_windows", "layout"]
     for w in which:
         {"nw": make_nw, "pages": make_pages, "coherence": make_coherence,
-         "c1_windows": make_c1_windows, "ref_windows": make_ref_windows}[w]()
+         "c1_windows": make_c1_windows, "ref_windows": make_ref_windows,
+         "layout": make_layout}[w]()

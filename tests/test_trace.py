@@ -1,34 +1,65 @@
-"""The config-5 trace generator: heap-layout model against SURVEY §8f's measured reference
-layouts, and properties of the mmult access trace."""
+"""The config-5 trace generator: heap-layout model against the reference application heap itself
+(tests/golden/ref_layout.npz) and SURVEY §8f's figures, and properties of the mmult access
+trace."""
 import numpy as np
 import pytest
 
-from gallocy_amd.trace import (HeapExhausted, MmultTrace, c_row_values, mmult_layout, zone_image)
+from gallocy_amd.trace import (AppHeap, HeapExhausted, MmultTrace, c_row_values, mmult_layout,
+                               zone_image)
 from oracle import oracle
 
 
-def test_layout_ndim4_matches_reference_measurement():
-    # a-rowptrs@0, a[i]@48+48i, b@240, c@480, threads@720, args@768 (+40), page 0
+@pytest.mark.parametrize("ndim", [4, 64, 1000, 1021])
+def test_layout_matches_the_reference_heap(ndim, golden):
+    """Every object of test_mmult (a, b, c: row pointers and rows; threads; args) sits at the zone
+    offset the REFERENCE application heap hands out (tests/golden/ref_layout.npz, made by
+    oracle/_ref/ref_layout_driver from heaplayers/application.h:20-29's layers compiled in
+    place)."""
+    g = golden["ref_layout"]
+    L = mmult_layout(ndim)
+    assert [L.a_rp, L.b_rp, L.c_rp] == g[f"n{ndim}_rp"].tolist()
+    rows = g[f"n{ndim}_rows"]
+    assert np.array_equal(L.a_rows, rows[0]) and np.array_equal(L.b_rows, rows[1])
+    assert np.array_equal(L.c_rows, rows[2])
+    threads, args, end = g[f"n{ndim}_tail"].tolist()
+    assert [L.threads, L.args] == [threads, args]
+    assert L.args + 4 * 40 == end and L.zone_bytes >= end
+
+
+def test_layout_survey_figures():
+    """SURVEY §8f's quoted figures agree too (NDIM=4 relative offsets; NDIM=1000 row stride,
+    matrix bases, ~6010 pages, last object at ~24.6 MB)."""
     L = mmult_layout(4)
     first = L.a_rp
-    assert first == 40
     got = [L.a_rp, *L.a_rows.tolist(), L.b_rp, L.c_rp, L.threads, L.args]
     assert [g - first for g in got] == [0, 48, 96, 144, 192, 240, 480, 720, 768]
     assert L.n_pages == 5 and (L.args + 160) // 4096 == 0
-
-
-def test_layout_ndim1000_matches_reference_measurement():
     L = mmult_layout(1000)
     f = L.a_rp
     assert L.a_rows[1] - f == 16392 and L.b_rp - f == 8204016 and L.c_rp - f == 16408392
-    assert 6000 <= L.n_pages <= 6020           # "≈6010 distinct pages"
-    assert abs(L.zone_bytes - 24.6e6) < 0.1e6  # "last object at zone offset ≈24.6 MB"
+    assert 6000 <= L.n_pages <= 6020
+    assert abs(L.zone_bytes - 24.6e6) < 0.1e6
 
 
-def test_layout_limit_1021():
-    mmult_layout(1021)                          # the largest NDIM that fits the 32 MiB zone
+def test_layout_limit_1021(golden):
+    """NDIM 1021 is the largest that fits the 32 MiB zone; at 1022 the reference prints
+    ---ENOMEM--- and aborts (source.h:23-24) after the same number of objects as the model
+    allocates before HeapExhausted (fixture: the reference's exit status and object count)."""
+    mmult_layout(1021)
     with pytest.raises(HeapExhausted):
-        mmult_layout(1022)                      # the reference aborts with ---ENOMEM---
+        mmult_layout(1022)
+    status, objects = golden["ref_layout"]["abort_1022"].tolist()
+    assert status == -6  # SIGABRT
+    h = AppHeap()
+    done = 0
+    with pytest.raises(HeapExhausted):
+        for _ in range(3):
+            h.malloc(8 * 1022)
+            done += 1
+            for _ in range(1022):
+                h.malloc(8 * 1022)
+                done += 1
+    assert done == objects
 
 
 def test_c_rows_and_image():
