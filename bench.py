@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--nw-pairs", type=int, default=512, help="nw: 4 KiB page pairs per batch")
     ap.add_argument("--ndim", type=int, default=1000, help="mmult: matrix size (<= 1021)")
     ap.add_argument("--nodes", type=int, default=4, help="mmult: simulated DSM nodes (1-8)")
+    ap.add_argument("--retwin", choices=["on", "off"], default="on",
+                    help="mmult: on = each release re-twins its pages (gdsm_release, no twin step "
+                         "per round); off = a twin launch before the round's writes (round 4)")
     ap.add_argument("--graph", action="store_true",
                     help="mmult: replay one HIP graph of every round instead of eager launches")
     ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
@@ -651,12 +654,12 @@ def run_mmult(args):
     if world > 1:
         return run_mmult_ranks(args, int(os.environ.get("RANK", "0")), world)
     torch.cuda.set_device(0)
-    R = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed)
+    R = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed, retwin=args.retwin == "on")
     dt = R.run(graph=args.graph)
     ok = bool(np.array_equal(R.home_copy(), R.final_image()))
     # latency breakdown: the same replay again on a fresh state with per-launch HIP events (a
     # separate run, so the events do not weigh on `value`)
-    R2 = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed)
+    R2 = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed, retwin=args.retwin == "on")
     R2.data.prof_enable(True)
     R2.pt.prof_enable(True)
     dt2 = R2.run(graph=False)
@@ -695,8 +698,11 @@ def run_mmult(args):
            "seconds_total": round(dt, 4),
            "launch": f"one HIP graph of every round (recorded in {R.graph_build_s:.2f} s, untimed)"
                      if args.graph else "eager, two streams",
-           "round": "coherence batch | twin, the round's row writes (one batched copy), diff "
-                    "applying its runs to the home copies (gdsm_diff_apply_ids)",
+           "round": ("coherence batch | the round's row writes (one batched copy), the release "
+                     "applying its runs to the home copies and re-twinning its pages "
+                     "(gdsm_release)") if args.retwin == "on" else
+                    ("coherence batch | twin, the round's row writes (one batched copy), diff "
+                     "applying its runs to the home copies (gdsm_diff_apply_ids)"),
            "events_per_s": round(R.events_total / dt, 1),
            "rows_per_s": round(args.ndim / dt, 1),
            "home_copy_equals_product": ok,

@@ -71,6 +71,7 @@ SIGNATURES = {
     "gdsm_diff": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns)]),
     "gdsm_diff_apply": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns), C.c_int]),
     "gdsm_diff_apply_ids": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns), C.c_int, vp]),
+    "gdsm_release": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(GdsmRuns), C.c_int, vp, C.c_uint32]),
     "gdsm_diff_split": (C.c_int, [vp, vp, C.c_uint32, C.POINTER(GdsmRuns)]),
     "gdsm_runs_total": (C.c_int, [vp, C.POINTER(GdsmRuns), C.POINTER(C.c_uint64)]),
     "gdsm_apply": (C.c_int, [vp, C.c_int, vp, C.POINTER(GdsmRuns)]),

@@ -590,7 +590,7 @@ int gdsm_runs_free(gdsm_ctx* ctx, gdsm_runs* runs) {
 }
 
 static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,
-                     int target, const uint32_t* tids = nullptr) {
+                     int target, const uint32_t* tids = nullptr, bool retwin = false) {
   if (!ctx || !out || !out->rec_off || (!out->data && out->cap)) return -EINVAL;
   if (!ctx->arena[GDSM_TWIN] || !ctx->arena[GDSM_CURRENT]) return -EINVAL;
   if (target >= 0 && (target > 2 || target == GDSM_TWIN || target == GDSM_CURRENT ||
@@ -618,8 +618,16 @@ static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* 
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
                              ctx->stream, ctx->P(), target >= 0 ? ctx->arena[target] : nullptr,
-                             ctx->diff_bpp, tids, &guard));
+                             ctx->diff_bpp, tids, &guard,
+                             retwin ? ctx->arena[GDSM_TWIN] : nullptr));
   return 0;
+}
+
+int gdsm_release(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out, int target,
+                 const uint32_t* target_ids, uint32_t flags) {
+  if (flags & ~(uint32_t)GDSM_RELEASE_RETWIN) return -EINVAL;
+  if (target < 0 && target_ids) return -EINVAL;
+  return diff_impl(ctx, ids, n, out, target, target_ids, (flags & GDSM_RELEASE_RETWIN) != 0);
 }
 
 int gdsm_diff_apply_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,

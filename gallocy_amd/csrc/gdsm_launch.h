@@ -41,7 +41,11 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr,
                        uint8_t* target = nullptr, uint32_t bpp_hint = 0,
-                       const uint32_t* tids = nullptr, const IdGuard* guard = nullptr);
+                       const uint32_t* tids = nullptr, const IdGuard* guard = nullptr,
+                       uint8_t* retwin = nullptr);
+// retwin (gdsm_release's GDSM_RELEASE_RETWIN; must be the `twin` arena): after the diff, TWIN :=
+// CURRENT for every listed page whose record fits the capacity (inside the one-workgroup kernel
+// of a short release, by a second launch otherwise).
 // The diff kernel's output streams: list entries [first[d], first[d+1]) go to stream d (record
 // i of stream d = entry first[d] + i); ustart: the first work unit of each stream (set by the
 // launcher). One launch serves them all, each stream with its own look-back chain.

@@ -106,6 +106,30 @@ __global__ __launch_bounds__(256) void twin_kernel(uint8_t* __restrict__ twin,
   }
 }
 
+// Re-twin after a release (gdsm_release, GDSM_RELEASE_RETWIN) on the multi-workgroup diff path:
+// TWIN := CURRENT for list entry i's page when its record was stored (rec_off[i + 1] <= cap), so
+// a release that overflowed its stream leaves the pages it could not ship dirty. A wave per page;
+// ids are the launch's checked list (out-of-range entries already name the guard page).
+__global__ __launch_bounds__(256) void retwin_kernel(uint8_t* __restrict__ twin,
+                                                     const uint8_t* __restrict__ cur,
+                                                     const uint32_t* __restrict__ ids, uint64_t n,
+                                                     const uint64_t* __restrict__ rec_off,
+                                                     uint64_t cap) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n;
+       i += (uint64_t)gridDim.x * 4) {
+    if (rec_off[i + 1] > cap) continue;  // wave-uniform
+    const uint64_t pg = ids ? ids[i] : i;
+    const u32x4* src = reinterpret_cast<const u32x4*>(cur + pg * kPage);
+    u32x4 v[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) v[q] = src[lane + 64 * q];
+    u32x4* dst = reinterpret_cast<u32x4*>(twin + pg * kPage);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) dst[lane + 64 * q] = v[q];
+  }
+}
+
 // ------------------------------------------------------------------------- page-id guard
 // A context-level id list is copied with every out-of-range id replaced by n_pages, the guard
 // page every arena carries past its last page, so a bad list can never address outside the
@@ -489,7 +513,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool,
-    const uint32_t* __restrict__ tids, const IdGuard g) {
+    const uint32_t* __restrict__ tids, const IdGuard g, uint8_t* __restrict__ retwin) {
   static_assert(kU <= 64 && (kU & (kU - 1)) == 0, "unit size");
   static_assert(!kSolo || (kU == 1 && kSpill == 0), "solo: one-page units, no spill slot");
   constexpr uint32_t kNW = kSolo ? kSoloUnits : 4;  // waves per workgroup
@@ -547,6 +571,11 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   uint32_t my_size = 0;   // lane j: record size of page j
   uint32_t my_src = 0;    // lane j: LDS byte offset of page j's record
   uint4 t[4], c[4];
+  // kSolo re-twin (gdsm_release): with room in the stream for every record of the launch, the
+  // twin's dirty bytes are stored with the first pass's other stores; otherwise at the end, for a
+  // page whose record was stored (kU = 1 and a late page is emitted from the registers, so the
+  // twin page is never read again by this wave)
+  const bool retwin_now = kSolo && retwin && cap >= (sp.first[1] - sp.first[0]) * GDSM_MAX_RECORD;
   uint64_t pj = ids ? (kSolo && g.ids ? guarded_id(ids, i0, g.n_pages, bad_id) : ids[i0]) : i0;
   load_page(twin, cur, pj, lane, t, c);
   for (uint32_t j = 0; j < cnt; ++j) {
@@ -568,6 +597,9 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
       }
       D += (uint32_t)__popcll(B);
       if (kApply && m[k]) store_masked16(target + pt_ * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
+      // (whole chunks: a chunk's clean bytes are equal in TWIN and CURRENT, and TWIN is this
+      // writer's own, so no byte stores)
+      if (retwin_now && m[k]) *reinterpret_cast<uint4*>(retwin + pj * kPage + (k * 64 + lane) * 16u) = c[k];
     }
     if (j + 1 < cnt) {
       pj = ids ? ids[i0 + j + 1] : i0 + j + 1;
@@ -733,6 +765,14 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
     PageRuns P;
     scan_page(t, c, lane, P);
     emit_bytes(P, c, lane, data + excl + tab[j]);
+  }
+  if (kSolo && retwin && !retwin_now && excl + tab[1] <= cap) {
+    // gdsm_release's re-twin (TWIN := CURRENT, the dirty bytes only), once the record is out: the
+    // registers still hold the unit's one page (kKeep: a late page was emitted from them)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (diffmask16(t[k], c[k])) *reinterpret_cast<uint4*>(retwin + pj * kPage + (k * 64 + lane) * 16u) = c[k];
+    }
   }
   if (kSpill) {
     // the last active wave of the workgroup hands the slot to ticket + kSpillWGs once every wave's
@@ -1543,12 +1583,13 @@ hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s) {
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
                                    Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
-                                   const uint32_t* tids, const IdGuard* guard);
+                                   const uint32_t* tids, const IdGuard* guard, uint8_t* retwin);
 
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target,
-                       uint32_t bpp_hint, const uint32_t* tids, const IdGuard* guard) {
+                       uint32_t bpp_hint, const uint32_t* tids, const IdGuard* guard,
+                       uint8_t* retwin) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   DiffSplit sp{};
   sp.G = 1;
@@ -1558,7 +1599,7 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   sp.first[0] = 0;
   sp.first[1] = n;
   return launch_diff_impl(twin, cur, ids, sp, ws, ws_bytes, s, prof, target, bpp_hint, cap, tids,
-                          guard);
+                          guard, retwin);
 }
 
 hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
@@ -1575,15 +1616,16 @@ hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit 
   }
   if (sp.first[sp.G] == sp.first[0]) return hipSuccess;
   return launch_diff_impl(twin, cur, nullptr, sp, ws, ws_bytes, s, prof, nullptr, bpp_hint,
-                          mincap, nullptr, nullptr);
+                          mincap, nullptr, nullptr, nullptr);
 }
 
 // `cap` (the smallest stream capacity) only matters to workspaces that predate the spill pool.
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
                                    Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
-                                   const uint32_t* tids, const IdGuard* guard) {
+                                   const uint32_t* tids, const IdGuard* guard, uint8_t* retwin) {
   const uint64_t n = sp.first[sp.G] - sp.first[0];
+  if (retwin && sp.G != 1) return hipErrorInvalidValue;
   int v = diff_variant();
   // the spill pool's place in the workspace (after the largest status area n may need)
   const uint64_t u1 = v == 8 ? n : min(n, kDiffTiny);
@@ -1621,7 +1663,7 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
     auto kern = target ? diff_single_kernel<1, 4096, 4, true, 0, true>
                        : diff_single_kernel<1, 4096, 4, false, 0, true>;
     hipLaunchKernelGGL(kern, dim3(1), dim3((unsigned)(64 * nunits)), 0, s, twin, cur, ids, sp,
-                       reinterpret_cast<uint64_t*>(ws), target, nullptr, nullptr, tids, g);
+                       reinterpret_cast<uint64_t*>(ws), target, nullptr, nullptr, tids, g, retwin);
     return hipGetLastError();
   }
   // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
@@ -1660,7 +1702,13 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,
-                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{});
+                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{}, nullptr);
+  if (retwin) {  // after the diff has read every twin page (late pages are re-read)
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(retwin_kernel, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, retwin, cur,
+                       ids, n, sp.rec_off[0], sp.cap[0]);
+  }
   return hipGetLastError();
 }
 

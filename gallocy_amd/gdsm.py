@@ -20,6 +20,7 @@ MAX_RUNS = 2048
 MAX_RECORD = 10244
 TWIN, CURRENT, REPLICA = 0, 1, 2
 GEN_UNIFORM, GEN_CLUSTERED = 0, 1
+RELEASE_RETWIN = 1  # gdsm.h GDSM_RELEASE_RETWIN
 _ARENA = {"twin": TWIN, "current": CURRENT, "replica": REPLICA,
           TWIN: TWIN, CURRENT: CURRENT, REPLICA: REPLICA}
 
@@ -298,6 +299,19 @@ class Context:
         else:
             check(lib().gdsm_diff_apply(self.handle, self._ptr(ids), n, C.byref(out.s),
                                         _ARENA[apply_to]), "gdsm_diff_apply")
+        return out
+
+    def release(self, ids=None, n: Optional[int] = None, out: Optional[Runs] = None,
+                cap: int = 0, apply_to: Optional[str] = None, target_ids=None,
+                retwin: bool = True) -> Runs:
+        """gdsm_release: the diff of the listed pages (applied to `apply_to` at target_ids as
+        diff() does) and, with retwin, TWIN := CURRENT for every page whose record fit."""
+        n = self._count(ids, n)
+        out = out or Runs(self, n, cap)
+        check(lib().gdsm_release(self.handle, self._ptr(ids), n, C.byref(out.s),
+                                 -1 if apply_to is None else _ARENA[apply_to],
+                                 self._ptr(target_ids), RELEASE_RETWIN if retwin else 0),
+              "gdsm_release")
         return out
 
     def apply(self, runs: Runs, target="replica", ids=None):

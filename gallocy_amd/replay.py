@@ -9,14 +9,16 @@ rank; here the per-node views live side by side in one arena):
 
 Per round (one row per node, gallocy_amd/trace.py):
   1. coherence batch of the round's R/W fault events (SPEC §5);
-  2. twin of every c[i] page the round writes (SPEC §2), taken in each writer's view;
-  3. each writer stores its row c[i][*] into its own view (the application's writes; all of the
+  2. each writer stores its row c[i][*] into its own view (the application's writes; all of the
      round's rows as one batched copy, gdsm_memcpy_batch);
-  4. one diff of all those pages (SPEC §3) — release — whose kernel also applies the runs to
-     the home copies (gdsm_diff_apply_ids: view page t·Z + p -> home page p; fused=False: a
-     separate apply of the stream, SPEC §4). Rows sharing a page are written by different nodes
-     at disjoint bytes: their records hit the same home page with disjoint runs, which the
-     store-only apply handles without a read-modify-write race.
+  3. one release of all those pages (gdsm_release, SPEC §3) whose kernel also applies the runs to
+     the home copies (view page t·Z + p -> home page p) and then sets the pages' TWIN to their
+     CURRENT (GDSM_RELEASE_RETWIN), so the next round starts from clean twins without a twin
+     step (the views are uploaded with TWIN == CURRENT). retwin=False: a twin step (SPEC §2)
+     before the writes and gdsm_diff_apply_ids (fused=False: a separate apply, SPEC §4). Rows
+     sharing a page are written by different nodes at disjoint bytes: their records hit the same
+     home page with disjoint runs, which the store-only apply handles without a
+     read-modify-write race.
 The trace, the rows' values and the page lists are prepared on the host before the timed
 replay; a round is then only asynchronous launches on two streams (page table, page data),
 or, with run(graph=True), one HIP graph of all rounds recorded beforehand.
@@ -35,8 +37,11 @@ from .trace import PAGE_SZ, MmultTrace, c_row_values, mmult_layout, zone_image
 
 class MmultReplay:
     def __init__(self, ndim: int = 1000, nodes: int = 4, seed: int = 0, device: int = 0,
-                 fused: bool = True):
+                 fused: bool = True, retwin: bool = True):
         self.fused = fused
+        # retwin: every release refreshes its pages' twins (gdsm_release, GDSM_RELEASE_RETWIN), so
+        # a round needs no twin step: TWIN == CURRENT from the upload on, as after a release
+        self.retwin = retwin and fused
         self.L = mmult_layout(ndim)
         self.T = MmultTrace(self.L, nodes, seed)
         self.P = nodes
@@ -106,11 +111,14 @@ class MmultReplay:
                                                   self.d_tot.ptr + 80 * r), "coherence")   # 1
         a, b = int(self.id_off[r]), int(self.id_off[r + 1])
         ids, home, n = self.d_ids.ptr + 4 * a, self.d_home.ptr + 4 * a, b - a
-        self.data.twin(ids, n=n)                                                           # 2
+        if not self.retwin:
+            self.data.twin(ids, n=n)                                                       # 2
         d0, d1 = self.desc_off[r], self.desc_off[r + 1]                                    # 3
         gdsm.check(lib.gdsm_memcpy_batch(self.data.handle, self.d_desc.ptr + 24 * d0, d1 - d0),
                    "row writes")
-        if self.fused:                                                                     # 4
+        if self.retwin:                                                                    # 4
+            self.data.release(ids, n=n, out=self._runs, apply_to="replica", target_ids=home)
+        elif self.fused:
             self.data.diff(ids, n=n, out=self._runs, apply_to="replica", target_ids=home)
         else:
             self.data.diff(ids, n=n, out=self._runs)
@@ -308,7 +316,8 @@ class MmultRankReplay:
             self.d_notices.ptr + 8 * self.ncap * r, self.ncap)
         o = self.offs[r]
         if len(pages):
-            self.data.twin(self.d_ids.ptr + 4 * o[0], n=len(pages))                         # 2
+            # (no twin step: every release below refreshes its pages' twins, and the views were
+            # uploaded with TWIN == CURRENT)
             base = self.data.arena_ptr("current")
             for _, i in rows:
                 gdsm.check(lib.gdsm_memcpy_d2d(self.data.handle, base + int(self.L.c_rows[i]),
@@ -317,7 +326,8 @@ class MmultRankReplay:
         counts = [len(x) for x in by_dest]
         sids = [self.d_ids.ptr + 4 * o[1 + d] for d in range(self.P)]
         for d in range(self.P):                                                          # 3
-            self.data.diff(sids[d], n=counts[d], out=self.send[d])  # n = 0: rec_off[0] = 0
+            # the release for home d, re-twinning its pages (n = 0: rec_off[0] = 0)
+            self.data.release(sids[d], n=counts[d], out=self.send[d])
         exchange.exchange_runs(self.data, self.comm, self.send, sids, self.recv,
                                [b.ptr for b in self.rids])
 

@@ -175,6 +175,17 @@ int gdsm_diff_apply(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* o
  * at its own offset, and one home copy of it). */
 int gdsm_diff_apply_ids(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out,
                         int target, const uint32_t* target_ids);
+/* A whole release of a writer's pages on this GPU: gdsm_diff of the listed pages into `out`;
+ * with target >= 0 the runs are applied to arena `target` as gdsm_diff_apply_ids does
+ * (target_ids NULL: the same page ids); with GDSM_RELEASE_RETWIN, TWIN := CURRENT afterwards for
+ * every listed page whose record fit out->cap (a page whose record did not fit stays dirty, so
+ * redoing the release with a larger stream ships it), i.e. the next interval's diff starts clean
+ * without a gdsm_twin step. ids must be unique. A short release (<= 16 pages) is one kernel
+ * launch, re-twin included. Replaces the twin taken at the next write fault
+ * (resources/NUTSHELL.md:52-69: twin on the first write, diff at release). */
+#define GDSM_RELEASE_RETWIN 1u
+int gdsm_release(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* out, int target,
+                 const uint32_t* target_ids, uint32_t flags);
 /* One diff launch for a release with several destinations: arena pages [bounds[d],
  * bounds[d+1]) are diffed into out[d] (G <= 8 streams, each with its own buffers; record i of
  * out[d] is page bounds[d] + i; out[d].n is set). Every stream is exactly what gdsm_diff of that

@@ -918,3 +918,76 @@ def test_memcpy_batch():
         assert np.array_equal(got, want)
         assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, None, 1) == -22
         assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, None, 0) == 0
+
+
+@pytest.mark.parametrize("m", [1, 12, 16, 17, 700])
+@pytest.mark.parametrize("home", [False, True])
+def test_release_retwin(m, home):
+    """gdsm_release with GDSM_RELEASE_RETWIN: the stream is gdsm_diff's, the runs land at the
+    home copy (target ids) when asked, and afterwards TWIN == CURRENT for exactly the listed
+    pages (unlisted twins untouched), so a second release of the same pages is empty. m <= 16:
+    the one-workgroup kernel re-twins in place; m > 16: a second launch after the grid."""
+    n = 3000
+    rng = np.random.default_rng(100 + m)
+    twin, cur = oracle.gen_pages(n, seed=5, mode=1, ppm=100000)
+    cur[7] ^= 0x5A  # a dense page (every byte changed): a late record
+    ids = rng.choice(n, m, replace=False).astype(np.uint32)
+    if m > 1:
+        ids[1] = 7
+    tids = rng.permutation(n)[:m].astype(np.uint32)
+    with ga.Context(n) as c:
+        c.upload("twin", twin)
+        c.upload("current", cur)
+        base = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+        rep = base.copy()
+        rep[tids] = twin[ids]
+        c.upload("replica", rep)
+        if home:
+            r = c.release(c.ids(ids), apply_to="replica", target_ids=c.ids(tids))
+        else:
+            r = c.release(c.ids(ids))
+        c.sync()
+        h = r.to_host()
+        ro, data = oracle.diff_pages(twin, cur, ids)
+        assert np.array_equal(h.rec_off, ro) and np.array_equal(h.data[:int(ro[-1])], data)
+        want_t = twin.copy()
+        want_t[ids] = cur[ids]
+        assert np.array_equal(c.download("twin"), want_t)
+        want_r = rep.copy()
+        if home:
+            want_r[tids] = cur[ids]
+        assert np.array_equal(c.download("replica"), want_r)
+        r2 = c.release(c.ids(ids))
+        c.sync()
+        assert r2.total() == 0
+
+
+def test_release_retwin_keeps_pages_that_did_not_fit():
+    """A release whose stream overflows its capacity: the pages whose records were not stored
+    keep their old TWIN (they stay dirty), the stored ones are re-twinned; a second release with a
+    large enough stream ships exactly the rest (solo and grid paths)."""
+    for m in (10, 400):
+        n = 1000
+        twin, cur = oracle.gen_pages(n, seed=9, mode=1, ppm=100000)
+        ids = np.arange(0, 2 * m, 2, dtype=np.uint32)
+        ro, data = oracle.diff_pages(twin, cur, ids)
+        cap = int(ro[m // 2])  # the first half of the records fit
+        with ga.Context(n) as c:
+            c.upload("twin", twin)
+            c.upload("current", cur)
+            r = ga.Runs(c, m, cap=cap)
+            c.release(c.ids(ids), out=r)
+            with pytest.raises(GdsmError):
+                r.total()
+            got = c.download("twin")
+            stored = ro[1:] <= cap
+            assert stored.sum() == m // 2
+            want = twin.copy()
+            want[ids[stored]] = cur[ids[stored]]
+            assert np.array_equal(got, want), m
+            r2 = c.release(c.ids(ids), cap=m * 10244)
+            c.sync()
+            ro2, data2 = oracle.diff_pages(want, cur, ids)
+            h2 = r2.to_host()
+            assert np.array_equal(h2.rec_off, ro2) and np.array_equal(h2.data[:int(ro2[-1])], data2)
+            assert np.array_equal(c.download("twin")[ids], cur[ids])
