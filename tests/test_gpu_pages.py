@@ -920,20 +920,20 @@ def test_memcpy_batch():
         assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, None, 0) == 0
 
 
-@pytest.mark.parametrize("m", [1, 12, 16, 17, 700])
+@pytest.mark.parametrize("m", [1, 12, 16, 17, 31, 32, 33, 700])
 @pytest.mark.parametrize("home", [False, True])
 def test_release_retwin(m, home):
     """gdsm_release with GDSM_RELEASE_RETWIN: the stream is gdsm_diff's, the runs land at the
     home copy (target ids) when asked, and afterwards TWIN == CURRENT for exactly the listed
     pages (unlisted twins untouched), so a second release of the same pages is empty. m <= 16:
-    the one-workgroup kernel re-twins in place; m > 16: a second launch after the grid."""
+    the one-workgroup kernel, a page per wave, re-twins in place; m > 16: a guarded re-twin
+    launch after the grid. The first three listed pages are dense (every byte changed: late
+    records)."""
     n = 3000
     rng = np.random.default_rng(100 + m)
     twin, cur = oracle.gen_pages(n, seed=5, mode=1, ppm=100000)
-    cur[7] ^= 0x5A  # a dense page (every byte changed): a late record
     ids = rng.choice(n, m, replace=False).astype(np.uint32)
-    if m > 1:
-        ids[1] = 7
+    cur[ids[:3]] ^= 0x5A
     tids = rng.permutation(n)[:m].astype(np.uint32)
     with ga.Context(n) as c:
         c.upload("twin", twin)
@@ -966,7 +966,7 @@ def test_release_retwin_keeps_pages_that_did_not_fit():
     """A release whose stream overflows its capacity: the pages whose records were not stored
     keep their old TWIN (they stay dirty), the stored ones are re-twinned; a second release with a
     large enough stream ships exactly the rest (solo and grid paths)."""
-    for m in (10, 400):
+    for m in (10, 24, 400):
         n = 1000
         twin, cur = oracle.gen_pages(n, seed=9, mode=1, ppm=100000)
         ids = np.arange(0, 2 * m, 2, dtype=np.uint32)
