@@ -571,11 +571,12 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   uint32_t my_size = 0;   // lane j: record size of page j
   uint32_t my_src = 0;    // lane j: LDS byte offset of page j's record
   uint4 t[4], c[4];
-  // kSolo re-twin (gdsm_release): with room in the stream for every record of the launch, the
-  // twin's dirty bytes are stored with the first pass's other stores; otherwise at the end, for a
-  // page whose record was stored (kU = 1 and a late page is emitted from the registers, so the
-  // twin page is never read again by this wave)
-  const bool retwin_now = kSolo && retwin && cap >= (sp.first[1] - sp.first[0]) * GDSM_MAX_RECORD;
+  // Re-twin (gdsm_release), one-page units only (a late page is emitted from the registers, so
+  // the twin page is never read again by this wave): with room in the stream for every record of
+  // the launch, the twin's dirty chunks are stored with the first pass's other stores; otherwise
+  // (kSolo) at the end, for a page whose record was stored. (The grid gets `retwin` only when
+  // the stream has that room.)
+  const bool retwin_now = kU == 1 && retwin && cap >= (sp.first[1] - sp.first[0]) * GDSM_MAX_RECORD;
   uint64_t pj = ids ? (kSolo && g.ids ? guarded_id(ids, i0, g.n_pages, bad_id) : ids[i0]) : i0;
   load_page(twin, cur, pj, lane, t, c);
   for (uint32_t j = 0; j < cnt; ++j) {
@@ -1701,9 +1702,13 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
                        : v == 8 ? diff_single_kernel<1, 8192, 4, false>
                        : v == 2 ? diff_single_kernel<32, 8192, 4, false>
                                 : diff_single_kernel<16, 8192, 4, false>);
+  // one-page units with room for every record re-twin inside the kernel; otherwise a second
+  // launch once the diff has read every twin page (late pages of longer units are re-read)
+  const bool retwin_in = retwin && U == 1 && sp.cap[0] >= n * (uint64_t)GDSM_MAX_RECORD;
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,
-                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{}, nullptr);
-  if (retwin) {  // after the diff has read every twin page (late pages are re-read)
+                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{},
+                     retwin_in ? retwin : nullptr);
+  if (retwin && !retwin_in) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(retwin_kernel, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, retwin, cur,

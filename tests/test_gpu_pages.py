@@ -920,15 +920,16 @@ def test_memcpy_batch():
         assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, None, 0) == 0
 
 
-@pytest.mark.parametrize("m", [1, 12, 16, 17, 31, 32, 33, 700])
+@pytest.mark.parametrize("m", [1, 12, 16, 17, 31, 32, 33, 700, 3000])
 @pytest.mark.parametrize("home", [False, True])
 def test_release_retwin(m, home):
     """gdsm_release with GDSM_RELEASE_RETWIN: the stream is gdsm_diff's, the runs land at the
     home copy (target ids) when asked, and afterwards TWIN == CURRENT for exactly the listed
     pages (unlisted twins untouched), so a second release of the same pages is empty. m <= 16:
-    the one-workgroup kernel, a page per wave, re-twins in place; m > 16: a guarded re-twin
-    launch after the grid. The first three listed pages are dense (every byte changed: late
-    records)."""
+    the one-workgroup kernel, a page per wave, re-twins in place; up to 2048 pages the grid of
+    one-page waves does too (the stream has room for every record); 3000 pages (two-page units,
+    whose late pages are read again): a guarded re-twin launch after the grid. The first three
+    listed pages are dense (every byte changed: late records)."""
     n = 3000
     rng = np.random.default_rng(100 + m)
     twin, cur = oracle.gen_pages(n, seed=5, mode=1, ppm=100000)
