@@ -8,7 +8,7 @@ through the engine (coherence + diff propagation).
    (sizeheap.h:32-37), ZoneHeap bump-allocates 16368-B arenas behind a 24-B arena header, a new
    arena when the request does not fit (zoneheap.h:52-83), and SourceMmapHeap bumps arenas back
    to back inside one 32 MiB zone (source.h:15-38). Checked in tests/test_trace.py against the
-   reference heap itself (the application.h layers compiled in place by oracle/Makefile's
+   reference heap itself (libgallocy.cpp's custom_malloc compiled in place by oracle/Makefile's
    `layout` target: every object's zone offset at NDIM 4, 64, 1000, 1021 and the abort at 1022,
    tests/golden/ref_layout.npz) and SURVEY §8f's figures.
 2. `mmult_layout` allocates in test_mmult's order: init_matrix(a), (b), (c) — a row-pointer

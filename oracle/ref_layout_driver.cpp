@@ -1,14 +1,11 @@
 // TEST INFRASTRUCTURE ONLY. Driver for the REFERENCE application heap, compiled by oracle/Makefile
-// straight from the headers under /root/reference into oracle/_ref/ref_layout_driver. No
+// straight from the sources under /root/reference into oracle/_ref/ref_layout_driver. No
 // reference source is copied here.
 //
-// gallocy/libgallocy.cpp and heaplayers/application.h do not build in this image: both reach
-// gallocy/sqlite.h -> <sqlite3.h>, which is absent (libgallocy.h via allocators/shared.h;
-// application.h via pagetableheap.h -> models.h; PageTableHeap is not part of the heap type).
-// Everything custom_malloc (libgallocy.cpp:33-35) does is the heap type application.h:20-29
-// composes from the layer headers, which build alone: this driver includes those layers,
-// composes the same type in the same order, defines the heap object (libgallocy.cpp:16) and
-// the spin-lock flag (libgallocy.cpp:10-12) and calls heap.malloc.
+// Linked with gallocy/libgallocy.cpp (custom_malloc, libgallocy.cpp:33-35, over the
+// `ApplicationHeapType heap` of heaplayers/application.h:20-29) and allocators/internal.cpp, with
+// the reference's own vendored sqlite3 header directory on the include path (external/sqlite3:
+// libgallocy.h reaches sqlite.h), as SURVEY §8c's recipe does.
 //
 //   ref_layout_driver <NDIM>
 // makes test_mmult's allocations in its order (test/test_mmult.cpp:31-37 init_matrix for a, b,
@@ -26,31 +23,13 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "heaplayers/firstfitheap.h"
-#include "heaplayers/lockedheap.h"
-#include "heaplayers/sizeheap.h"
-#include "heaplayers/source.h"
-#include "heaplayers/spinlock.h"
-#include "heaplayers/stdlibheap.h"
-#include "heaplayers/zoneheap.h"
+#include "libgallocy.h"
 
 // constants.cpp:7 declares `extern char* main;`, which g++ >= 11 rejects; the Makefile compiles
 // it with -Dmain=__gallocy_main_anchor and this is the renamed variable's definition.
 extern "C" {
 char* __gallocy_main_anchor;
 }
-
-// the layers of heaplayers/application.h:20-29, in its order (DEFAULT_ZONE_SZ = 16384 - 16)
-typedef HL::LockedHeap<
-    HL::SpinLockType,
-    HL::StdlibHeap<HL::FirstFitHeap<HL::SizeHeap<
-        HL::ZoneHeap<HL::SourceMmapHeap<PURPOSE_APPLICATION_HEAP>, 16384 - 16> > > > >
-    AppHeapLayers;
-
-volatile int anyThreadCreated = 1;  // as libgallocy.cpp:12
-AppHeapLayers heap;                 // as libgallocy.cpp:16
-
-static void* custom_malloc(size_t sz) { return heap.malloc(sz); }  // libgallocy.cpp:33-35
 
 typedef struct {  // test_mmult.cpp:23-28
   int id;

@@ -22,8 +22,9 @@
                  rewritten) and the SPEC edge pages of pages.npz; keys '<set>_<field>'. Windows
                  whose reference alignment has gaps keep only L and the crc32s.
   ref_layout.npz zone offsets of test_mmult's objects (test/test_mmult.cpp:31-37, 152-154) as
-                 the REFERENCE application heap hands them out (heaplayers/application.h:20-29
-                 layers, compiled in place into oracle/_ref/ref_layout_driver) for NDIM 4, 64,
+                 the REFERENCE custom_malloc hands them out (libgallocy.cpp over
+                 heaplayers/application.h:20-29, compiled in place into
+                 oracle/_ref/ref_layout_driver) for NDIM 4, 64,
                  1000 and 1021, and the abort (---ENOMEM---, source.h:23-24) at NDIM 1022 with
                  the objects allocated before it.
   coherence.npz  a seeded event batch and its expected page table / totals from the C oracle

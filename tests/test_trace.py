@@ -12,9 +12,8 @@ from oracle import oracle
 @pytest.mark.parametrize("ndim", [4, 64, 1000, 1021])
 def test_layout_matches_the_reference_heap(ndim, golden):
     """Every object of test_mmult (a, b, c: row pointers and rows; threads; args) sits at the zone
-    offset the REFERENCE application heap hands out (tests/golden/ref_layout.npz, made by
-    oracle/_ref/ref_layout_driver from heaplayers/application.h:20-29's layers compiled in
-    place)."""
+    offset the REFERENCE custom_malloc hands out (tests/golden/ref_layout.npz, made by
+    oracle/_ref/ref_layout_driver, linked with libgallocy.cpp and internal.cpp in place)."""
     g = golden["ref_layout"]
     L = mmult_layout(ndim)
     assert [L.a_rp, L.b_rp, L.c_rp] == g[f"n{ndim}_rp"].tolist()
