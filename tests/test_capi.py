@@ -150,3 +150,15 @@ def test_tune_rejects_measurement_only_variants():
                     (b"coh_variant", 0), (b"coh_variant", 1), (b"coh_variant", 2)):
         assert L.gdsm_tune(key, ok) == 0
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0
+
+
+def test_release_argument_checks():
+    """gdsm_release refuses unknown flags and a target list without a target arena before it
+    touches a context (-EINVAL), like the other entry points on a NULL context."""
+    from gallocy_amd import _lib
+    lib = _lib.load()
+    runs = _lib.GdsmRuns()
+    assert lib.gdsm_release(None, None, 0, C.byref(runs), -1, None, 0) == -22      # no context
+    assert lib.gdsm_release(None, None, 0, C.byref(runs), 2, None, 2) == -22       # unknown flag
+    ids = (C.c_uint32 * 1)(0)
+    assert lib.gdsm_release(None, None, 0, C.byref(runs), -1, C.cast(ids, C.c_void_p), 1) == -22
