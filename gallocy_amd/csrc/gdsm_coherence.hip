@@ -199,7 +199,10 @@ __device__ __forceinline__ void fold_half(const uint32_t* __restrict__ tr, uint3
 }
 
 // kM (MEASUREMENT ONLY, -DGDSM_MEASURE builds, output invalid): 1 = no walk, 2 = no look-back,
-// 3 = no ordered look-back (no wave waits for the block holding its first segment's head).
+// 3 = no ordered look-back (no wave waits for the block holding its first segment's head),
+// 4 = events from a hot 64 MB window: block b loads the events of block b mod 4096 (kept in the
+// Infinity Cache) with their pages shifted by (b / 4096) * n_pages / 128, so the walk, the
+// page-table traffic and the look-back stay representative while the event loads hit in cache.
 template <bool kVec, bool kFull, bool kNodes, int kM = 0>
 __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                               const uint64_t* __restrict__ ev, uint64_t n,
@@ -209,6 +212,9 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
                                               uint32_t* __restrict__ tr) {
   const uint32_t lane = lane_id();
   const uint64_t lo = b * kFBlock;
+  constexpr uint64_t kHotBlocks = 4096;
+  const uint64_t lo_src = kM == 4 ? (b % kHotBlocks) * kFBlock : lo;  // where the events are read
+  const uint32_t padd = kM == 4 ? (uint32_t)((b / kHotBlocks) * (n_pages >> 7)) << 4 : 0u;
   const uint64_t g0 = lo + (uint64_t)lane * kFK;  // global index of this lane's first event
   const uint32_t nv =
       kFull ? kFK : (uint32_t)min((uint64_t)kFK, g0 < n ? n - g0 : (uint64_t)0);
@@ -227,12 +233,12 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     uint32_t e0 = 0, e1 = 0;  // events 1920 + 2 * lane and the one after it
 #pragma unroll
     for (uint32_t q = 0; q < kFBlock / 128; ++q) {
-      const uint4 v = ld_nt16(ev + lo + 128 * q + 2 * lane);
+      const uint4 v = ld_nt16(ev + lo_src + 128 * q + 2 * lane);
       hib |= v.y | v.w;
-      *reinterpret_cast<u32x2*>(tr + fold_slot(128 * q + 2 * lane)) = (u32x2){v.x, v.z};
+      *reinterpret_cast<u32x2*>(tr + fold_slot(128 * q + 2 * lane)) = (u32x2){v.x + padd, v.z + padd};
       if (q == kFBlock / 128 - 1) {
-        e0 = v.x;
-        e1 = v.z;
+        e0 = v.x + padd;
+        e1 = v.z + padd;
       }
     }
     // ---- early aggregate: when the block's last 128 events hold a write W and no head follows
@@ -266,9 +272,11 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   wave_lds_sync();
   COH_FSTAMP(1, __builtin_amdgcn_s_memtime());
   if ((GDSM_FOLD_PRIO & 5) == 1) __builtin_amdgcn_s_setprio(0);
-  const uint32_t xprev_w = lo > 0 ? (uint32_t)ev[lo - 1] : 0u;               // uniform
+  const uint32_t xprev_w = lo > 0 ? (uint32_t)ev[kM == 4 ? (lo_src ? lo_src - 1 : 0) : lo - 1] + padd
+                                  : 0u;  // uniform
   const bool has_next = lo + kFBlock < n;
-  const uint32_t xnext_w = has_next ? (uint32_t)ev[lo + kFBlock] : 0u;        // uniform
+  const uint32_t xnext_w =
+      has_next ? (uint32_t)ev[kM == 4 ? lo_src + kFBlock : lo + kFBlock] + padd : 0u;  // uniform
   const uint32_t xlast = nv ? tr[fold_slot(kFK * lane + nv - 1)] : 0u;       // last valid event
   uint32_t xp = from_prev_lane(tr[fold_slot(kFK * lane + kFK - 1)]);
   if (lane == 0) xp = xprev_w;
@@ -1132,10 +1140,11 @@ __global__ __launch_bounds__(256) void gen_events_kernel(uint64_t* __restrict__ 
 // single-pass fold at every size. All write the same page table and totals
 // (tests/test_gpu_coherence.py runs each). Measurement builds (-DGDSM_MEASURE,
 // scripts/dev/build_measure.sh; output invalid) add 4 / 5 / 6 = the fold without its walk /
-// without its look-back / without the ordered look-back. (1-3, the round-2 four-pass path, were
+// without its look-back / without the ordered look-back, and 7 = with its events read from a hot
+// 64 MB window (coh_fold_wave kM 4). (1-3, the round-2 four-pass path, were
 // removed in round 4; its last version is in git history, commit 585a356.)
 #ifdef GDSM_MEASURE
-constexpr int kCohVariants = 7;
+constexpr int kCohVariants = 8;
 static bool coh_variant_ok(int v) { return v <= 2 || (v >= 4 && v < kCohVariants); }
 #else
 static bool coh_variant_ok(int v) { return v >= 0 && v <= 2; }
@@ -1232,6 +1241,7 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
         if (vec && !nodes && cv == 4) kern = coh_fold_kernel<true, true, false, 1>;
         if (vec && !nodes && cv == 5) kern = coh_fold_kernel<true, true, false, 2>;
         if (vec && !nodes && cv == 6) kern = coh_fold_kernel<true, true, false, 3>;
+        if (vec && !nodes && cv == 7) kern = coh_fold_kernel<true, true, false, 4>;
 #endif
         hipLaunchKernelGGL(kern, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
                            events, n_events, full, fws, fpart, err, n_nodes);
