@@ -507,7 +507,7 @@ def run_twin(args):
     barrier(world)
 
 
-def mmult_cpu_baseline(ndim: int, nodes: int, seed: int) -> dict:
+def mmult_cpu_baseline(ndim: int, nodes: int, seed: int, min_seconds: float = 2.0) -> dict:
     """Config 5 on the host: the same trace replayed round by round on one thread through the C
     oracle (or_coherence of the round's events, the twin of the written pages, the row writes,
     or_diff_pages of those pages, or_apply of the stream to the home copies), P node views side
@@ -556,9 +556,9 @@ def mmult_cpu_baseline(ndim: int, nodes: int, seed: int) -> dict:
         "row_src": np.array([i for p in plan for _, i in p[1]], np.uint32),
         "row_off": np.concatenate([[0], np.cumsum([len(p[1]) for p in plan])]).astype(np.uint64),
     }
-    # the trace is short (tens of ms): replayed from a fresh state until 2 s of C time
+    # the trace is short (tens of ms): replayed from a fresh state until min_seconds of C time
     dt_c, reps, ok_c = 0.0, 0, True
-    while dt_c < 2.0 and reps < 500:
+    while (dt_c < min_seconds and reps < 500) or reps == 0:
         cur, twin, rep, st, fl = fresh()
         dt, _ = oracle.bench_mmult(st, fl, nodes, twin, cur, rep, flat_plan, rowvals)
         dt_c += dt

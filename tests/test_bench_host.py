@@ -115,3 +115,14 @@ def test_watchdog_ends_the_process_or_stays_quiet(disarm):
     else:
         assert r.returncode == 3 and "finished" not in r.stdout
         assert "rank 5: deadline passed in 'a test phase'" in r.stderr
+
+
+@pytest.mark.parametrize("nodes", [1, 3])
+def test_mmult_cpu_baseline_c_loop_and_python_loop_agree(nodes):
+    """Config 5's CPU baseline: the round loop in C (oracle or_bench_mmult over the precomputed
+    plan) and the same loop driven from Python both end with the home copy equal to the product
+    (test_mmult.cpp's c = a x b), and the line is labelled as timed in C."""
+    out = bench.mmult_cpu_baseline(48, nodes, 3, min_seconds=0.01)
+    assert out["home_copy_equals_product"] is True
+    assert out["python_driven"]["home_copy_equals_product"] is True
+    assert out["timed_in"].startswith("C") and out["value"] > 0 and out["cores"] == 1
