@@ -126,3 +126,26 @@ def test_legacy_diff_symbol_offloaded(ctx):
         assert ga.diff(a, b) == want  # gdsm_nw_diff takes the same route
     finally:
         ga.set_diff_device(None)
+
+
+@pytest.mark.parametrize("name", ["c1", "cl", "dense", "edge"])
+def test_page_windows_against_reference_alignments(ctx, golden, name):
+    """The GPU NW on every 1024-B page window the REFERENCE diff() aligned for the page-diff pins
+    (tests/golden/c1_windows.npz, ref_windows.npz; made by oracle/_ref): config 1's, config 3's
+    clustered, a dense set and the SPEC edge pages. Every window — the ones whose reference
+    alignment has gaps included — gives the reference's alignment length and the crc32 of both
+    alignment strings."""
+    import zlib
+
+    from tests.helpers import c1_windows, window_pages
+    if name == "c1":
+        g = golden["c1_windows"]
+        L, crc = g["L"], g["crc"]
+        t, c = c1_windows()
+    else:
+        L, crc = golden["ref_windows"][name + "_L"], golden["ref_windows"][name + "_crc"]
+        t, c = window_pages(name, golden)
+    tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+    got = ctx.nw_diff_batch([(tw[i].tobytes(), cw[i].tobytes()) for i in range(len(tw))])
+    for i, (o1, o2) in enumerate(got):
+        assert len(o1) == L[i] and [zlib.crc32(o1), zlib.crc32(o2)] == crc[i].tolist(), (name, i)
