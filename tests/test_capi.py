@@ -162,3 +162,22 @@ def test_release_argument_checks():
     assert lib.gdsm_release(None, None, 0, C.byref(runs), 2, None, 2) == -22       # unknown flag
     ids = (C.c_uint32 * 1)(0)
     assert lib.gdsm_release(None, None, 0, C.byref(runs), -1, C.cast(ids, C.c_void_p), 1) == -22
+
+
+def test_nw_diff_on_reference_page_windows(golden):
+    """libgdsm's CPU NW (the legacy diff()'s host path) on every 1024-B page window the REFERENCE
+    diff() aligned (c1_windows.npz, ref_windows.npz, oracle/_ref): same length and crc32 of both
+    alignment strings, windows with gaps included."""
+    import zlib
+
+    import gallocy_amd as ga
+    from tests.helpers import REF_WINDOW_SETS, c1_windows, window_pages
+    sets = [("c1", *c1_windows(), golden["c1_windows"]["L"], golden["c1_windows"]["crc"])]
+    for name in REF_WINDOW_SETS:
+        sets.append((name, *window_pages(name, golden), golden["ref_windows"][name + "_L"],
+                     golden["ref_windows"][name + "_crc"]))
+    for name, t, c, L, crc in sets:
+        tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+        for i in range(0, len(tw), 3 if name in ("c1", "cl") else 1):
+            o1, o2 = ga.diff(tw[i].tobytes(), cw[i].tobytes())
+            assert len(o1) == L[i] and [zlib.crc32(o1), zlib.crc32(o2)] == crc[i].tolist(), (name, i)
