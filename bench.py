@@ -874,6 +874,11 @@ def main():
         raise SystemExit("GDSM_BENCH_BACKEND must be nccl or gloo")
     if backend == "gloo":
         local = local % torch.cuda.device_count()
+    elif local >= torch.cuda.device_count():
+        # RCCL takes one rank per GPU ("Duplicate GPU detected" otherwise)
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local}, but {torch.cuda.device_count()} "
+                         f"GPU(s) are visible: --gpus N runs one rank per GPU over RCCL "
+                         f"(GDSM_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs)")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("gloo")
