@@ -508,13 +508,17 @@ __device__ __forceinline__ uint64_t guarded_id(const uint32_t* __restrict__ ids,
 }
 
 template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0,
-          bool kSolo = false>
+          bool kSolo = false, bool kRetwin = false>
 __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool,
-    const uint32_t* __restrict__ tids, const IdGuard g, uint8_t* __restrict__ retwin) {
+    const uint32_t* __restrict__ tids, const IdGuard g) {
   static_assert(kU <= 64 && (kU & (kU - 1)) == 0, "unit size");
+  static_assert(!kRetwin || kU == 1, "re-twin: one-page units");
+  // kRetwin (gdsm_release): TWIN is also written, through a pointer derived from `twin` itself,
+  // so the compiler never treats this kernel's twin loads as invariant
+  uint8_t* const twin_w = const_cast<uint8_t*>(twin);
   static_assert(!kSolo || (kU == 1 && kSpill == 0), "solo: one-page units, no spill slot");
   constexpr uint32_t kNW = kSolo ? kSoloUnits : 4;  // waves per workgroup
   __shared__ uint32_t sel_tab[16];
@@ -574,9 +578,9 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   // Re-twin (gdsm_release), one-page units only (a late page is emitted from the registers, so
   // the twin page is never read again by this wave): with room in the stream for every record of
   // the launch, the twin's dirty chunks are stored with the first pass's other stores; otherwise
-  // (kSolo) at the end, for a page whose record was stored. (The grid gets `retwin` only when
-  // the stream has that room.)
-  const bool retwin_now = kU == 1 && retwin && cap >= (sp.first[1] - sp.first[0]) * GDSM_MAX_RECORD;
+  // (kSolo) at the end, for a page whose record was stored. (The grid takes kRetwin only when the
+  // stream has that room.)
+  const bool retwin_now = kRetwin && cap >= (sp.first[1] - sp.first[0]) * GDSM_MAX_RECORD;
   uint64_t pj = ids ? (kSolo && g.ids ? guarded_id(ids, i0, g.n_pages, bad_id) : ids[i0]) : i0;
   load_page(twin, cur, pj, lane, t, c);
   for (uint32_t j = 0; j < cnt; ++j) {
@@ -600,7 +604,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
       if (kApply && m[k]) store_masked16(target + pt_ * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
       // (whole chunks: a chunk's clean bytes are equal in TWIN and CURRENT, and TWIN is this
       // writer's own, so no byte stores)
-      if (retwin_now && m[k]) *reinterpret_cast<uint4*>(retwin + pj * kPage + (k * 64 + lane) * 16u) = c[k];
+      if (retwin_now && m[k]) *reinterpret_cast<uint4*>(twin_w + pj * kPage + (k * 64 + lane) * 16u) = c[k];
     }
     if (j + 1 < cnt) {
       pj = ids ? ids[i0 + j + 1] : i0 + j + 1;
@@ -767,12 +771,12 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
     scan_page(t, c, lane, P);
     emit_bytes(P, c, lane, data + excl + tab[j]);
   }
-  if (kSolo && retwin && !retwin_now && excl + tab[1] <= cap) {
+  if (kSolo && kRetwin && !retwin_now && excl + tab[1] <= cap) {
     // gdsm_release's re-twin (TWIN := CURRENT, the dirty bytes only), once the record is out: the
     // registers still hold the unit's one page (kKeep: a late page was emitted from them)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (diffmask16(t[k], c[k])) *reinterpret_cast<uint4*>(retwin + pj * kPage + (k * 64 + lane) * 16u) = c[k];
+      if (diffmask16(t[k], c[k])) *reinterpret_cast<uint4*>(twin_w + pj * kPage + (k * 64 + lane) * 16u) = c[k];
     }
   }
   if (kSpill) {
@@ -1661,10 +1665,12 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
     // one workgroup, no workspace: the caller's lists are guarded by the kernel itself
     const IdGuard g = guard ? *guard : IdGuard{};
     ProfScope ps(prof, GDSM_PROF_DIFF, s);
-    auto kern = target ? diff_single_kernel<1, 4096, 4, true, 0, true>
-                       : diff_single_kernel<1, 4096, 4, false, 0, true>;
+    auto kern = retwin ? (target ? diff_single_kernel<1, 4096, 4, true, 0, true, true>
+                                 : diff_single_kernel<1, 4096, 4, false, 0, true, true>)
+                       : (target ? diff_single_kernel<1, 4096, 4, true, 0, true>
+                                 : diff_single_kernel<1, 4096, 4, false, 0, true>);
     hipLaunchKernelGGL(kern, dim3(1), dim3((unsigned)(64 * nunits)), 0, s, twin, cur, ids, sp,
-                       reinterpret_cast<uint64_t*>(ws), target, nullptr, nullptr, tids, g, retwin);
+                       reinterpret_cast<uint64_t*>(ws), target, nullptr, nullptr, tids, g);
     return hipGetLastError();
   }
   // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
@@ -1705,9 +1711,11 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
   // one-page units with room for every record re-twin inside the kernel; otherwise a second
   // launch once the diff has read every twin page (late pages of longer units are re-read)
   const bool retwin_in = retwin && U == 1 && sp.cap[0] >= n * (uint64_t)GDSM_MAX_RECORD;
+  if (retwin_in)
+    kern = target ? diff_single_kernel<1, 8192, 4, true, 0, false, true>
+                  : diff_single_kernel<1, 8192, 4, false, 0, false, true>;
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,
-                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{},
-                     retwin_in ? retwin : nullptr);
+                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{});
   if (retwin && !retwin_in) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
