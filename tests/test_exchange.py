@@ -90,3 +90,39 @@ def test_budget_covers_and_is_aligned():
     for b in (0, 1, 4, 1000, 123456, 1 << 30):
         x = exchange.budget(b)
         assert x >= b + 4096 and x % 256 == 0
+
+
+def _hang_worker(rank, world, port, deadline):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wd = exchange.Watchdog(rank).arm(deadline, "first exchange")
+    if rank == 1:
+        import time
+        time.sleep(600)  # the peer that hangs
+    n = 16
+    twin, cur = oracle.gen_pages(n, seed=1, mode=0, ppm=10000, first_page=rank, stride=world)
+    sids = exchange.send_ids(rank, world, n)
+    b = exchange.dest_bounds(rank, world, n)
+    send = []
+    for d in range(world):
+        ro, data = oracle.diff_pages(twin, cur, ids=np.arange(b[d], b[d + 1], dtype=np.uint32))
+        send.append((ro, sids[d], data))
+    exchange.GlooTransport().exchange(send)  # blocks: rank 1 never joins
+    wd.disarm()
+
+
+def test_watchdog_ends_ranks_blocked_on_a_hung_peer():
+    """World size 2 over gloo on the CPU: rank 1 hangs before the first exchange, rank 0 blocks
+    in it. Both ranks' watchdogs (exchange.Watchdog, the one bench.py --deadline arms) end their
+    processes with status 3 within about the deadline, instead of the job hanging."""
+    import time
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_hang_worker, args=(r, 2, port, 5.0)) for r in range(2)]
+    t0 = time.monotonic()
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=90)
+    assert all(p.exitcode == 3 for p in procs), [p.exitcode for p in procs]
+    assert time.monotonic() - t0 < 80
