@@ -85,7 +85,7 @@ def test_shard_pipelined_single_rank_rccl(mode, ppm):
             shard.close()
 
 
-@pytest.mark.parametrize("ranks,overlap", [(2, "on"), (3, "off")])
+@pytest.mark.parametrize("ranks,overlap", [(2, "on"), (3, "off"), (8, "on")])
 def test_bench_multi_rank_rehearsal_gloo(ranks, overlap):
     """bench.py's N > 1 step end to end with `ranks` processes sharing cuda:0 and exchanging over
     gloo (GDSM_BENCH_BACKEND=gloo, a rehearsal of the RCCL path: the same per-destination diffs,
