@@ -237,6 +237,7 @@ int gdsm_fini(gdsm_ctx* ctx) {
   for (void* p : ctx->allocs) (void)hipFree(p);
   if (ctx->err) (void)hipFree(ctx->err);
   if (ctx->diff_ws) (void)hipFree(ctx->diff_ws);
+  if (ctx->chain.ws) (void)hipFree(ctx->chain.ws);
   if (ctx->coh_ws) (void)hipFree(ctx->coh_ws);
   if (ctx->coh_pt) (void)hipFree(ctx->coh_pt);
   if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
@@ -614,12 +615,20 @@ static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* 
   if (!rc && tids && n) rc = safe_buf(ctx, n, 2, &guard.safe_tids);
   if (rc) return rc;
   if (!n) guard.ids = guard.tids = nullptr;
+  // a short list outside graph capture: the chained one-launch form (its granules and counters
+  // allocated once; without them the list takes the zeroing launch instead)
+  gdsm::DiffChain* chain = nullptr;
+  if (!ctx->capturing && n && n <= gdsm::kDiffChainUnits) {
+    if (!ctx->chain.ws && hipMalloc(&ctx->chain.ws, gdsm::diff_chain_bytes()) != hipSuccess)
+      ctx->chain.ws = nullptr;
+    if (ctx->chain.ws) chain = &ctx->chain;
+  }
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
                              ctx->stream, ctx->P(), target >= 0 ? ctx->arena[target] : nullptr,
                              ctx->diff_bpp, tids, &guard,
-                             retwin ? ctx->arena[GDSM_TWIN] : nullptr));
+                             retwin ? ctx->arena[GDSM_TWIN] : nullptr, chain));
   return 0;
 }
 

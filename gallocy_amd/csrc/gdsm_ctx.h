@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "gdsm.h"
+#include "gdsm_launch.h"
 #include "gdsm_prof.h"
 
 struct gdsm_ctx {
@@ -22,6 +23,7 @@ struct gdsm_ctx {
   uint32_t err_held = 0;
   uint8_t* diff_ws = nullptr;    // diff workspace
   uint64_t diff_ws_bytes = 0;
+  gdsm::DiffChain chain;         // short releases without a zeroing launch (allocated on first use)
   uint8_t* coh_ws = nullptr;
   uint64_t coh_ws_bytes = 0;
   uint64_t* coh_pt = nullptr;      // page table: state | faults << 32 per page

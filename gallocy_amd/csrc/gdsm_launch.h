@@ -36,13 +36,25 @@ struct IdGuard {
   uint64_t n_pages;
   uint32_t* err;
 };
+// A context's chain of zero-free diff launches: lists of at most kDiffChainUnits pages (one-page
+// units) take one launch, no workspace-zeroing launch before it. ws (diff_chain_bytes(), device)
+// holds two ticket counters and one epoch-tagged look-back granule per unit; it is zeroed once
+// (epoch 0: by the next launch, then epoch 1). Launch E draws its tickets from counter E & 1 and
+// zeroes counter (E + 1) & 1 for launch E + 1; a granule counts only when it carries E. Not for
+// graph capture (a replayed launch would repeat its epoch).
+constexpr uint64_t kDiffChainUnits = 2048;
+struct DiffChain {
+  uint64_t* ws = nullptr;
+  uint32_t epoch = 0;  // the next launch's epoch, 1 .. 2^30 - 1; 0 = zero ws first
+};
+uint64_t diff_chain_bytes();
 // With `guard`, the kernel reads guard->safe_ids / safe_tids in place of ids / tids.
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof = nullptr,
                        uint8_t* target = nullptr, uint32_t bpp_hint = 0,
                        const uint32_t* tids = nullptr, const IdGuard* guard = nullptr,
-                       uint8_t* retwin = nullptr);
+                       uint8_t* retwin = nullptr, DiffChain* chain = nullptr);
 // retwin (gdsm_release's GDSM_RELEASE_RETWIN; must be the `twin` arena): after the diff, TWIN :=
 // CURRENT for every listed page whose record fits the capacity (inside the one-workgroup kernel
 // of a short release, by a second launch otherwise).
@@ -57,6 +69,7 @@ struct DiffSplit {
   uint64_t first[kMaxSplit + 1];
   uint64_t ustart[kMaxSplit + 1];
   uint32_t G;
+  uint32_t epoch;  // a DiffChain launch's epoch (set by the launcher)
 };
 // One diff launch over arena pages [first[0], first[G]) (ids = identity) into sp's G streams.
 hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s);

@@ -507,8 +507,13 @@ __device__ __forceinline__ uint64_t guarded_id(const uint32_t* __restrict__ ids,
   return p < n_pages ? p : n_pages;
 }
 
+// kChain (a context's lists of at most kDiffTiny pages outside graph capture; DiffChain): the
+// grid form without a zeroing launch. ws = two ticket counters, then one granule per unit tagged
+// with the launch's epoch sp.epoch: launch E draws its tickets from counter E & 1 and zeroes
+// counter (E + 1) & 1 for the next launch, and the look-back counts a granule only when it carries
+// E (granule = flag << 62 | E << 32 | value). The caller's lists are guarded in the kernel (g).
 template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0,
-          bool kSolo = false, bool kRetwin = false>
+          bool kSolo = false, bool kRetwin = false, bool kChain = false>
 __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
@@ -520,6 +525,10 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   // so the compiler never treats this kernel's twin loads as invariant
   uint8_t* const twin_w = const_cast<uint8_t*>(twin);
   static_assert(!kSolo || (kU == 1 && kSpill == 0), "solo: one-page units, no spill slot");
+  static_assert(!kChain || (kU == 1 && kSpill == 0 && !kSolo), "chain: one-page grid units");
+  constexpr bool kGuard = kSolo || kChain;  // the caller's id lists are guarded in this kernel
+  const uint64_t tag = kChain ? (uint64_t)sp.epoch << 32 : 0ull;  // granule epoch (kChain)
+  constexpr uint64_t kVal = kChain ? 0xFFFFFFFFull : kStVal;
   constexpr uint32_t kNW = kSolo ? kSoloUnits : 4;  // waves per workgroup
   __shared__ uint32_t sel_tab[16];
   __shared__ uint32_t ent_all[kNW][64];
@@ -538,7 +547,11 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   // tickets would queue on it); unit = 4 * ticket + wave
   __shared__ uint32_t ticket, done_waves;
   if (!kSolo && threadIdx.x == 0) {
-    const uint32_t t = atomicAdd(reinterpret_cast<uint32_t*>(ws), 1u);
+    uint32_t* const ctr = reinterpret_cast<uint32_t*>(ws);
+    const uint32_t t = atomicAdd(ctr + (kChain ? sp.epoch & 1u : 0u), 1u);
+    if (kChain && blockIdx.x == 0)  // the next launch's counter (this launch never draws from it)
+      __hip_atomic_store(ctr + ((sp.epoch + 1u) & 1u), 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     ticket = t;
     done_waves = 0;
     if (kSpill && (uint64_t)t * 4 < nunits) {  // wait for the spill slot's previous user
@@ -551,7 +564,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   __syncthreads();
   const uint64_t u = kSolo ? (uint64_t)wave : (uint64_t)ticket * 4 + wave;
   if (u >= nunits) return;  // wave-uniform: the grid's spare waves (none in a solo launch)
-  uint32_t bad_id = 0;      // kSolo: a caller id out of range
+  uint32_t bad_id = 0;      // kGuard: a caller id out of range
   // the output stream this unit belongs to (units never straddle two of them) and its place in it
   uint32_t d = 0;
 #pragma unroll
@@ -581,11 +594,11 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   // (kSolo) at the end, for a page whose record was stored. (The grid takes kRetwin only when the
   // stream has that room.)
   const bool retwin_now = kRetwin && cap >= (sp.first[1] - sp.first[0]) * GDSM_MAX_RECORD;
-  uint64_t pj = ids ? (kSolo && g.ids ? guarded_id(ids, i0, g.n_pages, bad_id) : ids[i0]) : i0;
+  uint64_t pj = ids ? (kGuard && g.ids ? guarded_id(ids, i0, g.n_pages, bad_id) : ids[i0]) : i0;
   load_page(twin, cur, pj, lane, t, c);
   for (uint32_t j = 0; j < cnt; ++j) {
     const uint64_t pt_ =
-        kApply ? (tids ? (kSolo && g.tids ? guarded_id(tids, i0 + j, g.n_pages, bad_id)
+        kApply ? (tids ? (kGuard && g.tids ? guarded_id(tids, i0 + j, g.n_pages, bad_id)
                                           : (uint64_t)tids[i0 + j])
                        : pj)
                : 0;  // page at target
@@ -671,8 +684,9 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
     for (uint32_t w = 0; w < wave; ++w) excl += solo_agg[w];
     if (g.err && __ballot(bad_id != 0) && lane == 0) atomicOr(g.err, 8u);
   }
+  if (kChain && g.err && __ballot(bad_id != 0) && lane == 0) atomicOr(g.err, 8u);
   if (!kSolo && lane == 0)
-    __hip_atomic_store(status + u, (u == u0 ? kStIncl : kStAgg) | agg, __ATOMIC_RELAXED,
+    __hip_atomic_store(status + u, (u == u0 ? kStIncl : kStAgg) | tag | agg, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   if (!kSolo && u > u0) {
     int64_t pos = (int64_t)u - 1;
@@ -680,23 +694,27 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
       const int64_t q = pos - (int64_t)lane;
       uint64_t st = q >= (int64_t)u0
                         ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : kStIncl;  // before the stream's first unit: an inclusive prefix of 0
-      while (__ballot((st >> 62) == 0)) {  // a predecessor has not published yet
+                        : kStIncl | tag;  // before the stream's first unit: a prefix of 0
+      // unpublished: no flag yet (kChain: or a granule of an earlier launch)
+      auto unpub = [&](uint64_t w) {
+        return (w >> 62) == 0 || (kChain && ((w >> 32) & 0x3FFFFFFFull) != sp.epoch);
+      };
+      while (__ballot(unpub(st))) {  // a predecessor has not published yet
         __builtin_amdgcn_s_sleep(1);
-        if ((st >> 62) == 0)
+        if (unpub(st))
           st = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       const uint64_t im = __ballot((st >> 62) == 2);
       if (im) {
         const uint32_t k = (uint32_t)__builtin_ctzll(im);
-        excl += wave_sum_u64(lane <= k ? (st & kStVal) : 0ull);
+        excl += wave_sum_u64(lane <= k ? (st & kVal) : 0ull);
         break;
       }
-      excl += wave_sum_u64(st & kStVal);
+      excl += wave_sum_u64(st & kVal);
       pos -= 64;
     }
     if (lane == 0)
-      __hip_atomic_store(status + u, kStIncl | (excl + agg), __ATOMIC_RELAXED,
+      __hip_atomic_store(status + u, kStIncl | tag | (excl + agg), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
 
@@ -764,14 +782,14 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
     if (!(kKeep && first_late && j + 1 == cnt)) {
       uint32_t unused = 0;
       load_page(twin, cur,
-                ids ? (kSolo && g.ids ? guarded_id(ids, i, g.n_pages, unused) : ids[i]) : i, lane,
+                ids ? (kGuard && g.ids ? guarded_id(ids, i, g.n_pages, unused) : ids[i]) : i, lane,
                 t, c);
     }
     PageRuns P;
     scan_page(t, c, lane, P);
     emit_bytes(P, c, lane, data + excl + tab[j]);
   }
-  if (kSolo && kRetwin && !retwin_now && excl + tab[1] <= cap) {
+  if (kGuard && kRetwin && !retwin_now && excl + tab[1] <= cap) {
     // gdsm_release's re-twin (TWIN := CURRENT, the dirty bytes only), once the record is out: the
     // registers still hold the unit's one page (kKeep: a late page was emitted from them)
 #pragma unroll
@@ -1400,8 +1418,9 @@ __global__ __launch_bounds__(256) void apply_flat_kernel(uint8_t* __restrict__ t
 //   7  16 pages per wave, 8 KiB LDS buffer + 24 KiB global spill slot per wave
 //   8  1 page per wave (automatic for lists of <= kDiffTiny pages: a wave per page, and a dense
 //      page's record, ~4.6 KiB for a page of rewritten doubles, fits the LDS buffer instead of
-//      being re-read as the second page of a 2-page unit); up to kSoloUnits pages of one stream
-//      it is the one-workgroup kSolo launch
+//      being re-read as the second page of a 2-page unit); one stream of a context outside graph
+//      capture: the one-workgroup kSolo launch up to diff_solo_max pages, the chained grid launch
+//      (kChain, no zeroing launch) beyond; otherwise kSolo up to kSoloUnits pages
 // Measurement-only kernels (invalid output) are not part of the library.
 static int diff_variant_from_env() {
   const char* e = getenv("GDSM_DIFF_VARIANT");
@@ -1433,11 +1452,34 @@ static int apply_variant_from_env() {
   return (v >= 0 && v < kApplyVariants) ? v : 0;
 }
 static std::atomic<int> g_apply_variant{apply_variant_from_env()};
+// Short lists of one-page units (variant 8), gdsm_tune("diff_solo_max", k) and ("diff_chain", 0|1):
+// up to k units the one-workgroup kSolo launch, beyond it the kChain grid launch when the context
+// offers its DiffChain (else the grid with its zeroing launch). Default k = 4: config 5's rounds
+// (~12 dense pages, same box, alternating, rounds/s) 4 nodes 43.0k with k = 16 (every round one
+// workgroup: its waves' byte stores queue on one CU) -> 45.3k with k = 4 (45.5k with k = 0);
+// 8 nodes 32.5k behind the zeroing launch -> 34.1k chained; 1 node k = 4 best by ~1 %.
+constexpr int kSoloDefault = 4;
+// (also GDSM_DIFF_SOLO_MAX / GDSM_DIFF_CHAIN at load)
+static int env_int(const char* name, int lo, int hi, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : dflt;
+  return (e && v >= lo && v <= hi) ? v : dflt;
+}
+static std::atomic<int> g_solo_max{env_int("GDSM_DIFF_SOLO_MAX", 0, (int)kSoloUnits, kSoloDefault)};
+static std::atomic<int> g_chain{env_int("GDSM_DIFF_CHAIN", 0, 1, 1)};
 
 
 int tune(const char* key, int64_t value) {
   if (!strcmp(key, "diff_variant") && value >= 0 && value <= 8) {
     g_diff_variant.store((int)value, std::memory_order_relaxed);
+    return 0;
+  }
+  if (!strcmp(key, "diff_solo_max") && value >= 0 && value <= (int64_t)kSoloUnits) {
+    g_solo_max.store((int)value, std::memory_order_relaxed);
+    return 0;
+  }
+  if (!strcmp(key, "diff_chain") && (value == 0 || value == 1)) {
+    g_chain.store((int)value, std::memory_order_relaxed);
     return 0;
   }
   if (!strcmp(key, "apply_variant") && value >= 0 && value < kApplyVariants) {
@@ -1453,6 +1495,7 @@ int tune(const char* key, int64_t value) {
 // fewer workgroup slots of 4 x kDiffSpill bytes). Non-decreasing in n, so a workspace reserved
 // for n fits every shorter list.
 constexpr uint64_t kDiffShort = 32768, kDiffTiny = 2048;
+static_assert(kDiffChainUnits == kDiffTiny, "every automatic one-page list fits the chain");
 constexpr uint32_t kDiffSpill = 24576;
 // Densities (stream bytes per page) the automatic geometry switches at: up to kDense64, 64 pages
 // per wave (their records fill the 8 KiB buffer at 128 B); up to kDense16, 16 pages (8 KiB / 16
@@ -1588,13 +1631,16 @@ hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s) {
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
                                    Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
-                                   const uint32_t* tids, const IdGuard* guard, uint8_t* retwin);
+                                   const uint32_t* tids, const IdGuard* guard, uint8_t* retwin,
+                                   DiffChain* chain = nullptr);
+
+uint64_t diff_chain_bytes() { return 8 * (1 + kDiffChainUnits); }
 
 hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids, uint64_t n,
                        uint64_t* rec_off, uint8_t* data, uint64_t cap, uint8_t* ws,
                        uint64_t ws_bytes, hipStream_t s, Prof* prof, uint8_t* target,
                        uint32_t bpp_hint, const uint32_t* tids, const IdGuard* guard,
-                       uint8_t* retwin) {
+                       uint8_t* retwin, DiffChain* chain) {
   if (n == 0) return hipMemsetAsync(rec_off, 0, sizeof(uint64_t), s);
   DiffSplit sp{};
   sp.G = 1;
@@ -1604,7 +1650,7 @@ hipError_t launch_diff(const uint8_t* twin, const uint8_t* cur, const uint32_t* 
   sp.first[0] = 0;
   sp.first[1] = n;
   return launch_diff_impl(twin, cur, ids, sp, ws, ws_bytes, s, prof, target, bpp_hint, cap, tids,
-                          guard, retwin);
+                          guard, retwin, chain);
 }
 
 hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
@@ -1628,7 +1674,8 @@ hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit 
 static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                                    DiffSplit sp, uint8_t* ws, uint64_t ws_bytes, hipStream_t s,
                                    Prof* prof, uint8_t* target, uint32_t bpp_hint, uint64_t cap,
-                                   const uint32_t* tids, const IdGuard* guard, uint8_t* retwin) {
+                                   const uint32_t* tids, const IdGuard* guard, uint8_t* retwin,
+                                   DiffChain* chain) {
   const uint64_t n = sp.first[sp.G] - sp.first[0];
   if (retwin && sp.G != 1) return hipErrorInvalidValue;
   int v = diff_variant();
@@ -1661,7 +1708,13 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
   if (spill && (wgs < kSpillWGs ? wgs : kSpillWGs) * 4 * kDiffSpill > spill_pool_bytes(n))
     return hipErrorInvalidValue;
   uint32_t* gen = spill ? reinterpret_cast<uint32_t*>(ws + status_end) : nullptr;
-  if (v == 8 && sp.G == 1 && nunits <= kSoloUnits) {
+  // short lists: the chained launch (when the context offers it) from solo_max + 1 units, the
+  // one-workgroup launch below (up to kSoloUnits without the chain)
+  const bool chain_ok = v == 8 && sp.G == 1 && chain && chain->ws && nunits <= kDiffChainUnits &&
+                        g_chain.load(std::memory_order_relaxed);
+  const uint64_t solo_max =
+      chain_ok ? (uint64_t)g_solo_max.load(std::memory_order_relaxed) : (uint64_t)kSoloUnits;
+  if (v == 8 && sp.G == 1 && nunits <= solo_max) {
     // one workgroup, no workspace: the caller's lists are guarded by the kernel itself
     const IdGuard g = guard ? *guard : IdGuard{};
     ProfScope ps(prof, GDSM_PROF_DIFF, s);
@@ -1672,6 +1725,27 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
     hipLaunchKernelGGL(kern, dim3(1), dim3((unsigned)(64 * nunits)), 0, s, twin, cur, ids, sp,
                        reinterpret_cast<uint64_t*>(ws), target, nullptr, nullptr, tids, g);
     return hipGetLastError();
+  }
+  if (chain_ok) {
+    // one launch: epoch-tagged granules, the caller's lists guarded by the kernel (DiffChain)
+    if (chain->epoch == 0) {
+      const hipError_t e = hipMemsetAsync(chain->ws, 0, diff_chain_bytes(), s);
+      if (e != hipSuccess) return e;
+      chain->epoch = 1;
+    }
+    sp.epoch = chain->epoch;
+    const IdGuard g = guard ? *guard : IdGuard{};
+    ProfScope ps(prof, GDSM_PROF_DIFF, s);
+    auto kern = retwin ? (target ? diff_single_kernel<1, 8192, 4, true, 0, false, true, true>
+                                 : diff_single_kernel<1, 8192, 4, false, 0, false, true, true>)
+                       : (target ? diff_single_kernel<1, 8192, 4, true, 0, false, false, true>
+                                 : diff_single_kernel<1, 8192, 4, false, 0, false, false, true>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids,
+                       sp, chain->ws, target, nullptr, nullptr, tids, g);
+    const hipError_t e = hipGetLastError();
+    // a launch that did not run leaves its successor's counter unzeroed: start the chain over
+    chain->epoch = e != hipSuccess || chain->epoch + 1 >= (1u << 30) ? 0 : chain->epoch + 1;
+    return e;
   }
   // ticket counter + status granules (+ the spill slots' generation words), zeroed per launch
   // (outside the timed kernel), and the caller's lists checked, in one prep launch

@@ -920,16 +920,16 @@ def test_memcpy_batch():
         assert ga.gdsm.lib().gdsm_memcpy_batch(c.handle, None, 0) == 0
 
 
-@pytest.mark.parametrize("m", [1, 12, 16, 17, 31, 32, 33, 700, 3000])
+@pytest.mark.parametrize("m", [1, 4, 5, 12, 16, 17, 31, 32, 33, 700, 3000])
 @pytest.mark.parametrize("home", [False, True])
 def test_release_retwin(m, home):
     """gdsm_release with GDSM_RELEASE_RETWIN: the stream is gdsm_diff's, the runs land at the
     home copy (target ids) when asked, and afterwards TWIN == CURRENT for exactly the listed
-    pages (unlisted twins untouched), so a second release of the same pages is empty. m <= 16:
-    the one-workgroup kernel, a page per wave, re-twins in place; up to 2048 pages the grid of
-    one-page waves does too (the stream has room for every record); 3000 pages (two-page units,
-    whose late pages are read again): a guarded re-twin launch after the grid. The first three
-    listed pages are dense (every byte changed: late records)."""
+    pages (unlisted twins untouched), so a second release of the same pages is empty. m <= 4:
+    the one-workgroup kernel, a page per wave, re-twins in place; up to 2048 pages the chained
+    grid of one-page waves does too; 3000 pages (two-page units, whose late pages are read
+    again): a guarded re-twin launch after the grid. The first three listed pages are dense
+    (every byte changed: late records)."""
     n = 3000
     rng = np.random.default_rng(100 + m)
     twin, cur = oracle.gen_pages(n, seed=5, mode=1, ppm=100000)
@@ -966,8 +966,10 @@ def test_release_retwin(m, home):
 def test_release_retwin_keeps_pages_that_did_not_fit():
     """A release whose stream overflows its capacity: the pages whose records were not stored
     keep their old TWIN (they stay dirty), the stored ones are re-twinned; a second release with a
-    large enough stream ships exactly the rest (solo and grid paths)."""
-    for m in (10, 24, 400):
+    large enough stream ships exactly the rest (one-workgroup, chained and, inside a graph
+    capture, zeroing-launch paths)."""
+    for m, captured in ((4, False), (10, False), (24, False), (400, False), (10, True),
+                        (24, True), (400, True)):
         n = 1000
         twin, cur = oracle.gen_pages(n, seed=9, mode=1, ppm=100000)
         ids = np.arange(0, 2 * m, 2, dtype=np.uint32)
@@ -977,7 +979,18 @@ def test_release_retwin_keeps_pages_that_did_not_fit():
             c.upload("twin", twin)
             c.upload("current", cur)
             r = ga.Runs(c, m, cap=cap)
-            c.release(c.ids(ids), out=r)
+            d_ids = c.ids(ids)
+            if captured:
+                ga.gdsm.check(ga.gdsm.lib().gdsm_reserve(c.handle, m, 0), "gdsm_reserve")
+                c.sync()
+                c.capture_begin()
+                c.release(d_ids, out=r)
+                g = c.capture_end()
+                g.launch(c)
+                c.sync()
+                g.destroy()
+            else:
+                c.release(d_ids, out=r)
             with pytest.raises(GdsmError):
                 r.total()
             got = c.download("twin")
@@ -985,10 +998,91 @@ def test_release_retwin_keeps_pages_that_did_not_fit():
             assert stored.sum() == m // 2
             want = twin.copy()
             want[ids[stored]] = cur[ids[stored]]
-            assert np.array_equal(got, want), m
+            assert np.array_equal(got, want), (m, captured)
             r2 = c.release(c.ids(ids), cap=m * 10244)
             c.sync()
             ro2, data2 = oracle.diff_pages(want, cur, ids)
             h2 = r2.to_host()
             assert np.array_equal(h2.rec_off, ro2) and np.array_equal(h2.data[:int(ro2[-1])], data2)
             assert np.array_equal(c.download("twin")[ids], cur[ids])
+
+
+def test_chained_short_lists_across_launches_and_graphs():
+    """Lists of 17-2048 pages take the chained one-launch diff (DiffChain: epoch-tagged look-back
+    granules, ticket counters the previous launch zeroed, no zeroing launch). Forty launches in a
+    row of varying length and kind (diff, diff_apply_ids, release), mixed with one-workgroup
+    (<= 16 pages) and zeroing-launch (3000 pages) diffs, a graph of a short diff replayed between
+    them (captured launches take the zeroing form), the chain switched off and on again, and a
+    list with an out-of-range id (-EINVAL at the sync, the valid records still right): every
+    stream equals the oracle's and every home-copy page is right."""
+    n = 4096
+    rng = np.random.default_rng(77)
+    twin, cur = oracle.gen_pages(n, seed=21, mode=1, ppm=60000)
+    cur[rng.choice(n, 40, replace=False)] ^= 0x33  # some dense pages (late records)
+    L = ga.gdsm.lib()
+    with ga.Context(n) as c:
+        c.upload("twin", twin)
+        c.upload("current", cur)
+        c.upload("replica", twin)
+        gids = rng.choice(n, 100, replace=False).astype(np.uint32)
+        d_g = c.ids(gids)
+        g_runs = Runs(c, 100, cap=100 * 10244)
+        ga.gdsm.check(L.gdsm_reserve(c.handle, n, 0), "gdsm_reserve")  # no growth while capturing
+        c.sync()
+        c.capture_begin()
+        c.diff(d_g.ptr, n=100, out=g_runs)
+        graph = c.capture_end()
+        g_ro, g_data = oracle.diff_pages(twin, cur, gids)
+        sizes = [17, 2048, 1, 300, 3000, 64, 16, 1999, 33, 500] * 4
+        try:
+            for it, m in enumerate(sizes):
+                if it == 20:
+                    assert L.gdsm_tune(b"diff_chain", 0) == 0
+                if it == 26:
+                    assert L.gdsm_tune(b"diff_chain", 1) == 0
+                ids = rng.choice(n, m, replace=False).astype(np.uint32)
+                kind = it % 3
+                if kind == 0:
+                    r = c.diff(c.ids(ids))
+                elif kind == 1:
+                    tids = rng.permutation(n)[:m].astype(np.uint32)
+                    rep = twin.copy()
+                    rep[tids] = twin[ids]  # the home copy holds the pages' last release
+                    c.upload("replica", rep)
+                    r = c.diff(c.ids(ids), apply_to="replica", target_ids=c.ids(tids))
+                else:
+                    r = c.release(c.ids(ids), retwin=False)
+                c.sync()
+                h = r.to_host()
+                ro, data = oracle.diff_pages(twin, cur, ids)
+                assert np.array_equal(h.rec_off, ro), (it, m)
+                assert np.array_equal(h.data[:int(ro[-1])], data), (it, m)
+                if kind == 1:
+                    assert np.array_equal(c.download("replica")[tids], cur[ids]), (it, m)
+                r.free()
+                if it % 7 == 3:
+                    graph.launch(c)
+                    c.sync()
+                    hg = g_runs.to_host()
+                    assert np.array_equal(hg.rec_off, g_ro)
+                    assert np.array_equal(hg.data[:int(g_ro[-1])], g_data)
+            bad = rng.choice(n, 40, replace=False).astype(np.uint32)
+            bad[[5, 30]] = [n, 0xFFFFFFFF]
+            r = c.diff(c.ids(bad))
+            with pytest.raises(GdsmError) as ei:
+                c.sync()
+            assert ei.value.errno == 22
+            h = r.to_host()
+            for i in range(40):
+                if i not in (5, 30):
+                    want = oracle.diff_pages(twin[bad[i]][None], cur[bad[i]][None])[1].tobytes()
+                    assert h.record(i) == want, i
+            ids = rng.choice(n, 700, replace=False).astype(np.uint32)
+            r = c.diff(c.ids(ids))
+            c.sync()
+            ro, data = oracle.diff_pages(twin, cur, ids)
+            h = r.to_host()
+            assert np.array_equal(h.rec_off, ro) and np.array_equal(h.data[:int(ro[-1])], data)
+        finally:
+            L.gdsm_tune(b"diff_chain", 1)
+            graph.destroy()
