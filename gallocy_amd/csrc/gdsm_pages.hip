@@ -513,8 +513,8 @@ __device__ __forceinline__ uint64_t guarded_id(const uint32_t* __restrict__ ids,
 // counter (E + 1) & 1 for the next launch, and the look-back counts a granule only when it carries
 // E (granule = flag << 62 | E << 32 | value). The caller's lists are guarded in the kernel (g).
 template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0,
-          bool kSolo = false, bool kRetwin = false, bool kChain = false>
-__global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
+          bool kSolo = false, bool kRetwin = false, uint32_t kChainW = 0>
+__global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, uint32_t* __restrict__ gen, uint8_t* __restrict__ pool,
@@ -525,11 +525,12 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
   // so the compiler never treats this kernel's twin loads as invariant
   uint8_t* const twin_w = const_cast<uint8_t*>(twin);
   static_assert(!kSolo || (kU == 1 && kSpill == 0), "solo: one-page units, no spill slot");
+  constexpr bool kChain = kChainW != 0;  // kChainW: waves per workgroup of the chained form
   static_assert(!kChain || (kU == 1 && kSpill == 0 && !kSolo), "chain: one-page grid units");
   constexpr bool kGuard = kSolo || kChain;  // the caller's id lists are guarded in this kernel
   const uint64_t tag = kChain ? (uint64_t)sp.epoch << 32 : 0ull;  // granule epoch (kChain)
   constexpr uint64_t kVal = kChain ? 0xFFFFFFFFull : kStVal;
-  constexpr uint32_t kNW = kSolo ? kSoloUnits : 4;  // waves per workgroup
+  constexpr uint32_t kNW = kSolo ? kSoloUnits : kChain ? kChainW : 4;  // waves per workgroup
   __shared__ uint32_t sel_tab[16];
   __shared__ uint32_t ent_all[kNW][64];
   __shared__ uint4 dat_all[kNW][64];
@@ -562,7 +563,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : 256) __attribute__((amdgp
     }
   }
   __syncthreads();
-  const uint64_t u = kSolo ? (uint64_t)wave : (uint64_t)ticket * 4 + wave;
+  const uint64_t u = kSolo ? (uint64_t)wave : (uint64_t)ticket * kNW + wave;
   if (u >= nunits) return;  // wave-uniform: the grid's spare waves (none in a solo launch)
   uint32_t bad_id = 0;      // kGuard: a caller id out of range
   // the output stream this unit belongs to (units never straddle two of them) and its place in it
@@ -1452,9 +1453,13 @@ static int apply_variant_from_env() {
   return (v >= 0 && v < kApplyVariants) ? v : 0;
 }
 static std::atomic<int> g_apply_variant{apply_variant_from_env()};
-// Short lists of one-page units (variant 8), gdsm_tune("diff_solo_max", k) and ("diff_chain", 0|1):
-// up to k units the one-workgroup kSolo launch, beyond it the kChain grid launch when the context
-// offers its DiffChain (else the grid with its zeroing launch). Default k = 4: config 5's rounds
+// Short lists of one-page units (variant 8), gdsm_tune("diff_solo_max", k) and ("diff_chain", W):
+// up to k units the one-workgroup kSolo launch, beyond it the kChain grid launch of W (1 or 4)
+// waves per workgroup when the context offers its DiffChain (W = 0: the grid with its zeroing
+// launch; default 2 = automatic: one wave per workgroup up to kChainOneWave units, spreading a
+// round's byte stores over more CUs, four beyond, where per-wave tickets would queue on the
+// counter). Config 5 at 4 / 8 nodes, same box: 45.3k / 33.7k rounds/s with W = 4, 46.2k / 34.9k
+// with W = 1. Default k = 4: config 5's rounds
 // (~12 dense pages, same box, alternating, rounds/s) 4 nodes 43.0k with k = 16 (every round one
 // workgroup: its waves' byte stores queue on one CU) -> 45.3k with k = 4 (45.5k with k = 0);
 // 8 nodes 32.5k behind the zeroing launch -> 34.1k chained; 1 node k = 4 best by ~1 %.
@@ -1466,7 +1471,8 @@ static int env_int(const char* name, int lo, int hi, int dflt) {
   return (e && v >= lo && v <= hi) ? v : dflt;
 }
 static std::atomic<int> g_solo_max{env_int("GDSM_DIFF_SOLO_MAX", 0, (int)kSoloUnits, kSoloDefault)};
-static std::atomic<int> g_chain{env_int("GDSM_DIFF_CHAIN", 0, 1, 1)};
+constexpr uint64_t kChainOneWave = 64;
+static std::atomic<int> g_chain{env_int("GDSM_DIFF_CHAIN", 0, 4, 2)};
 
 
 int tune(const char* key, int64_t value) {
@@ -1478,7 +1484,7 @@ int tune(const char* key, int64_t value) {
     g_solo_max.store((int)value, std::memory_order_relaxed);
     return 0;
   }
-  if (!strcmp(key, "diff_chain") && (value == 0 || value == 1)) {
+  if (!strcmp(key, "diff_chain") && (value == 0 || value == 1 || value == 2 || value == 4)) {
     g_chain.store((int)value, std::memory_order_relaxed);
     return 0;
   }
@@ -1736,12 +1742,18 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
     sp.epoch = chain->epoch;
     const IdGuard g = guard ? *guard : IdGuard{};
     ProfScope ps(prof, GDSM_PROF_DIFF, s);
-    auto kern = retwin ? (target ? diff_single_kernel<1, 8192, 4, true, 0, false, true, true>
-                                 : diff_single_kernel<1, 8192, 4, false, 0, false, true, true>)
-                       : (target ? diff_single_kernel<1, 8192, 4, true, 0, false, false, true>
-                                 : diff_single_kernel<1, 8192, 4, false, 0, false, false, true>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids,
-                       sp, chain->ws, target, nullptr, nullptr, tids, g);
+    const int cw = g_chain.load(std::memory_order_relaxed);
+    const uint32_t W = cw == 1 || (cw == 2 && nunits <= kChainOneWave) ? 1 : 4;  // waves / group
+    auto kern = W == 1 ? (retwin ? (target ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1>
+                                           : diff_single_kernel<1, 8192, 4, false, 0, false, true, 1>)
+                                 : (target ? diff_single_kernel<1, 8192, 4, true, 0, false, false, 1>
+                                           : diff_single_kernel<1, 8192, 4, false, 0, false, false, 1>))
+                       : (retwin ? (target ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 4>
+                                           : diff_single_kernel<1, 8192, 4, false, 0, false, true, 4>)
+                                 : (target ? diff_single_kernel<1, 8192, 4, true, 0, false, false, 4>
+                                           : diff_single_kernel<1, 8192, 4, false, 0, false, false, 4>));
+    hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + W - 1) / W)), dim3(64 * W), 0, s, twin, cur,
+                       ids, sp, chain->ws, target, nullptr, nullptr, tids, g);
     const hipError_t e = hipGetLastError();
     // a launch that did not run leaves its successor's counter unzeroed: start the chain over
     chain->epoch = e != hipSuccess || chain->epoch + 1 >= (1u << 30) ? 0 : chain->epoch + 1;

@@ -3,10 +3,11 @@ each, was one diff_single_kernel<..., kSolo> launch of ~13 us, the round's criti
 
 Pages of doubles holding integers (C = A x B of test_mmult: two or three nonzero high bytes per
 double, ~500 runs a page) against zero twins, m pages per launch, `reps` launches per case:
-gdsm_diff, and gdsm_release applying to the home copy with re-twin (TWIN zeroed again by an upload
-between launches), each under three launch forms: `auto` (the library's choice), `chain`
-(gdsm_tune diff_solo_max 0: the chained grid launch from one page up) and `prep` (diff_chain 0:
-past 16 pages the grid behind its zeroing launch). m = 9 is the clean case (CURRENT == TWIN),
+gdsm_diff, and gdsm_release applying to the home copy with re-twin (TWIN zeroed again by a
+gdsm_memcpy_batch copy kernel between launches), each under the launch forms named: `auto` (the library's choice), `chain`,
+`chain1`, `chain4` (gdsm_tune diff_solo_max 0: the chained grid launch from one page up, one
+wave per workgroup up to 128 pages / always one / always four) and `prep` (diff_chain 0: past 16
+pages the grid behind its zeroing launch). m = 9 is the clean case (CURRENT == TWIN),
 m = 11 the sparse one (one double a page). Run under rocprofv3 --kernel-trace and read with
 scripts/dev/kstats.py (the cases differ by kernel, grid or workgroup size).
 
@@ -37,9 +38,11 @@ def main():
     n = 2048
     ctx = ga.Context(n, arenas=("twin", "current", "replica"))
     zeros = np.zeros((n, PAGE), np.uint8)
+    d_zero = ctx.buffer(n * PAGE).upload(zeros)
+    twin_ptr = ctx.arena_ptr("twin")
     for form in forms:
-        L.gdsm_tune(b"diff_solo_max", 0 if form == "chain" else 16)
-        L.gdsm_tune(b"diff_chain", 0 if form == "prep" else 1)
+        L.gdsm_tune(b"diff_solo_max", 0 if form.startswith("chain") else 4)
+        L.gdsm_tune(b"diff_chain", {"prep": 0, "chain1": 1, "chain4": 4}.get(form, 2))
         for m, kind in CASES:
             if form != "auto" and m in (9, 11):
                 continue
@@ -54,19 +57,22 @@ def main():
             ctx.upload("current", cur)
             ids = ctx.ids(np.arange(m, dtype=np.uint32))
             out = ga.Runs(ctx, m, m * 10244)
+            # TWIN zeroed again between releases by a copy kernel, as config 5's row writes are
+            d_desc = ctx.buffer(24).upload(np.array([twin_ptr, d_zero.ptr, m * PAGE], np.uint64))
             for op in ("diff", "release"):
                 for _ in range(reps):
                     if op == "diff":
                         ctx.diff(ids, out=out)
                     else:
                         ctx.release(ids, out=out, apply_to="replica", target_ids=ids)
-                        ctx.upload("twin", zeros[:m])
+                        L.gdsm_memcpy_batch(ctx.handle, d_desc.ptr, 1)
                 ctx.sync()
             print(form, m, kind, out.total(), flush=True)
             out.free()
             ids.free()
-    L.gdsm_tune(b"diff_solo_max", 16)
-    L.gdsm_tune(b"diff_chain", 1)
+            d_desc.free()
+    L.gdsm_tune(b"diff_solo_max", 4)
+    L.gdsm_tune(b"diff_chain", 2)
     ctx.close()
 
 

@@ -1012,7 +1012,8 @@ def test_chained_short_lists_across_launches_and_graphs():
     granules, ticket counters the previous launch zeroed, no zeroing launch). Forty launches in a
     row of varying length and kind (diff, diff_apply_ids, release), mixed with one-workgroup
     (<= 16 pages) and zeroing-launch (3000 pages) diffs, a graph of a short diff replayed between
-    them (captured launches take the zeroing form), the chain switched off and on again, and a
+    them (captured launches take the zeroing form), the chain switched off, to four-wave workgroups
+    and back to automatic (one wave per workgroup up to 64 pages), and a
     list with an out-of-range id (-EINVAL at the sync, the valid records still right): every
     stream equals the oracle's and every home-copy page is right."""
     n = 4096
@@ -1036,10 +1037,8 @@ def test_chained_short_lists_across_launches_and_graphs():
         sizes = [17, 2048, 1, 300, 3000, 64, 16, 1999, 33, 500] * 4
         try:
             for it, m in enumerate(sizes):
-                if it == 20:
-                    assert L.gdsm_tune(b"diff_chain", 0) == 0
-                if it == 26:
-                    assert L.gdsm_tune(b"diff_chain", 1) == 0
+                if it in (20, 26, 33):  # the zeroing form, four-wave workgroups, then automatic
+                    assert L.gdsm_tune(b"diff_chain", {20: 0, 26: 4, 33: 2}[it]) == 0
                 ids = rng.choice(n, m, replace=False).astype(np.uint32)
                 kind = it % 3
                 if kind == 0:
@@ -1084,5 +1083,5 @@ def test_chained_short_lists_across_launches_and_graphs():
             h = r.to_host()
             assert np.array_equal(h.rec_off, ro) and np.array_equal(h.data[:int(ro[-1])], data)
         finally:
-            L.gdsm_tune(b"diff_chain", 1)
+            L.gdsm_tune(b"diff_chain", 2)
             graph.destroy()
