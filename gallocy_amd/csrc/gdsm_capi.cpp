@@ -238,6 +238,7 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->err) (void)hipFree(ctx->err);
   if (ctx->diff_ws) (void)hipFree(ctx->diff_ws);
   if (ctx->chain.ws) (void)hipFree(ctx->chain.ws);
+  if (ctx->coh_chain.ws) (void)hipFree(ctx->coh_chain.ws);
   if (ctx->coh_ws) (void)hipFree(ctx->coh_ws);
   if (ctx->coh_pt) (void)hipFree(ctx->coh_pt);
   if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
@@ -813,9 +814,16 @@ int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n
   if (g.rc) return g.rc;
   int rc = ensure(ctx, &ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
   if (rc) return rc;
+  gdsm::CohChainState* chain = nullptr;  // (outside graph capture, see launch_coherence)
+  if (!ctx->capturing) {
+    if (!ctx->coh_chain.ws &&
+        hipMalloc(&ctx->coh_chain.ws, gdsm::coh_chain_bytes()) != hipSuccess)
+      ctx->coh_chain.ws = nullptr;
+    if (ctx->coh_chain.ws) chain = &ctx->coh_chain;
+  }
   GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, ctx->n_nodes, events, n_events,
                                   totals_dev, ctx->coh_ws, ctx->coh_ws_bytes, ctx->err,
-                                  ctx->stream, ctx->P()));
+                                  ctx->stream, ctx->P(), chain));
   return 0;
 }
 

@@ -747,13 +747,29 @@ __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popc
 
 // totals != nullptr (small batches): the span's totals are added to the batch totals directly
 // (10 atomics per span) instead of a partial row for coh_reduce_kernel: one launch fewer.
-template <uint32_t kSC, bool kFull>
+// kChain (CohChain: a context's small batches without a zeroing launch): the status granules
+// carry the launch's epoch (bits 32-60; a granule of an earlier launch reads as unpublished),
+// `totals` is the chain's accumulator row of this launch, and the wave that completes the last
+// span copies it to the caller's totals (ch.out).
+struct CohChain {
+  uint32_t epoch;             // 1 .. 2^29 - 1
+  uint32_t* done;             // spans completed in this launch (zeroed by the previous launch)
+  unsigned long long* out;    // the caller's batch totals
+};
+template <uint32_t kSC, bool kFull, bool kChain = false>
 __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                 const uint64_t* __restrict__ ev, uint64_t n,
                                                 uint64_t b, uint64_t* __restrict__ status,
                                                 uint32_t* __restrict__ partial,
                                                 uint32_t* __restrict__ err, uint32_t n_nodes,
-                                                unsigned long long* __restrict__ totals) {
+                                                unsigned long long* __restrict__ totals,
+                                                const CohChain ch = CohChain{}, uint64_t nb = 0) {
+  const uint64_t tag = kChain ? (uint64_t)ch.epoch << 32 : 0ull;
+  // a status granule as this launch sees it (kChain: an earlier launch's reads as unpublished)
+  auto ld_status = [&](int64_t q) {
+    const uint64_t x = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (kChain && ((x >> 32) & 0x1FFFFFFFull) != ch.epoch) ? 0ull : x;
+  };
   constexpr uint32_t kSpan = 64 * kSC;
   const uint32_t lane = lane_id();
   const uint64_t lo = b * kSpan;
@@ -943,7 +959,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (lane == 0)
-    __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (any_head ? kFHead : 0ull) | agg,
+    __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (any_head ? kFHead : 0ull) | tag | agg,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool ordered = has_d;
   uint32_t cur = 0;
@@ -951,8 +967,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
     int64_t pos = (int64_t)b - 1;
     for (;;) {
       const int64_t q = pos - (int64_t)lane;
-      uint64_t stv = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                            : kFIncl;
+      uint64_t stv = q >= 0 ? ld_status(q) : kFIncl;
       uint32_t sidx, spins = 0;
       for (;;) {
         const uint64_t pub = __ballot((stv >> 62) != 0);
@@ -968,8 +983,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        if ((stv >> 62) == 0 && q >= 0)
-          stv = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((stv >> 62) == 0 && q >= 0) stv = ld_status(q);
       }
       uint32_t part;
       if (sidx == 0)
@@ -981,7 +995,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       pos -= 64;
     }
     if (lane == 0)
-      __hip_atomic_store(status + b, kFIncl | (any_head ? kFHead : 0ull) | tcompose(cur, agg),
+      __hip_atomic_store(status + b, kFIncl | (any_head ? kFHead : 0ull) | tag | tcompose(cur, agg),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
@@ -1047,11 +1061,30 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
     partial[b * 10 + lane] = mine;
   }
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
+  if (kChain) {
+    // the last span to complete copies the accumulated row to the caller's totals
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // (agent scope) this wave's adds before its count
+    uint32_t d = 0;
+    if (lane == 0)
+      d = __hip_atomic_fetch_add(ch.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    d = __builtin_amdgcn_readfirstlane(d);
+    if (d + 1 == nb) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      if (lane < 10)
+        ch.out[lane] = __hip_atomic_load(totals + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Spans [0, nfull) are whole; a partial last span (nb > nfull) is walked by the wave that draws
 // it, in the same launch (a separate tail launch was one more dependent launch per batch).
-template <uint32_t kSC>
+// The chained small-batch workspace (kChain): two sets of the kFoldCtrs ticket-counter lines,
+// two accumulator rows of totals and two completion counters (launch E uses set E & 1; its
+// workgroup 0 zeroes set (E + 1) & 1 for launch E + 1), then the epoch-tagged status granules.
+constexpr uint64_t kCohChainAcc = 2 * kFoldStatus;         // u64 index: accumulator row set s at + 16 s
+constexpr uint64_t kCohChainDone = kCohChainAcc + 32;      // u64 index: done counter set s at + 32 s
+constexpr uint64_t kCohChainStatus = kCohChainDone + 64;   // u64 index of span 0's granule
+template <uint32_t kSC, bool kChain = false>
 __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ pt,
                                                          uint64_t n_pages,
                                                          const uint64_t* __restrict__ ev,
@@ -1060,22 +1093,41 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
                                                          uint32_t* __restrict__ partial,
                                                          uint32_t* __restrict__ err,
                                                          uint32_t n_nodes,
-                                                         unsigned long long* __restrict__ totals) {
+                                                         unsigned long long* __restrict__ totals,
+                                                         uint32_t epoch = 0) {
   __shared__ uint32_t tk;
   // tickets as coh_fold_kernel
   const uint32_t cls = blockIdx.x % kFoldCtrs;
-  if (threadIdx.x == 0) tk = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
+  const uint32_t set = kChain ? epoch & 1u : 0u;
+  if (threadIdx.x == 0)
+    tk = atomicAdd(reinterpret_cast<uint32_t*>(ws + (set * kFoldCtrs + cls) * 32), 1u);
+  if (kChain && blockIdx.x == 0) {  // launch E + 1's counters, accumulator row and done counter
+    const uint32_t nx = set ^ 1u, t = threadIdx.x;
+    if (t < kFoldCtrs)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(ws + (nx * kFoldCtrs + t) * 32), 0u,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (t < kFoldCtrs + 10)
+      __hip_atomic_store(ws + kCohChainAcc + 16 * nx + (t - kFoldCtrs), 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else if (t == kFoldCtrs + 10)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(ws + kCohChainDone + 32 * nx), 0u,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   const uint32_t ticket = __builtin_amdgcn_readfirstlane(tk);
   const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
   const uint64_t b = w * 4 + (threadIdx.x >> 6);
   if (b >= nb) return;
+  uint64_t* const status = ws + (kChain ? kCohChainStatus : kFoldStatus);
+  unsigned long long* const acc =
+      kChain ? reinterpret_cast<unsigned long long*>(ws + kCohChainAcc + 16 * set) : totals;
+  const CohChain ch{epoch, reinterpret_cast<uint32_t*>(ws + kCohChainDone + 32 * set), totals};
   if (b < nfull)
-    coh_stream_wave<kSC, true>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes,
-                               totals);
+    coh_stream_wave<kSC, true, kChain>(pt, n_pages, ev, n, b, status, partial, err, n_nodes, acc,
+                                       ch, nb);
   else
-    coh_stream_wave<kSC, false>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial, err, n_nodes,
-                                totals);
+    coh_stream_wave<kSC, false, kChain>(pt, n_pages, ev, n, b, status, partial, err, n_nodes,
+                                        acc, ch, nb);
 }
 
 // The small-batch path's zeroing (batch totals and the tickets + status granules) in one launch.
@@ -1155,7 +1207,14 @@ static int coh_variant_from_env() {
   return coh_variant_ok(v) ? v : 0;
 }
 static std::atomic<int> g_coh_variant{coh_variant_from_env()};
+// Small batches of a context outside graph capture: the chained one-launch form (CohChain) unless
+// gdsm_tune("coh_chain", 0) or GDSM_COH_CHAIN=0 at load (then the zeroing launch before the fold).
+static std::atomic<int> g_coh_chain{getenv("GDSM_COH_CHAIN") && atoi(getenv("GDSM_COH_CHAIN")) == 0 ? 0 : 1};
 int coh_tune(const char* key, int64_t value) {
+  if (!strcmp(key, "coh_chain") && (value == 0 || value == 1)) {
+    g_coh_chain.store((int)value, std::memory_order_relaxed);
+    return 0;
+  }
   if (!strcmp(key, "coh_variant") && value >= 0 && value < 8 && coh_variant_ok((int)value)) {
     g_coh_variant.store((int)value, std::memory_order_relaxed);
     return 0;
@@ -1187,13 +1246,36 @@ hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hip
   return hipGetLastError();
 }
 
+uint64_t coh_chain_bytes() {
+  return 8 * (kCohChainStatus + (kCohSmall + 64 * kSCSmall - 1) / (64 * kSCSmall));
+}
+
 hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                             const uint64_t* events, uint64_t n_events, uint64_t* totals,
                             uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
-                            Prof* prof) {
+                            Prof* prof, CohChainState* chain) {
   const int cv = g_coh_variant.load(std::memory_order_relaxed);
   const bool small = cv == 0 && n_events <= kCohSmall;
   if (n_events == 0) return hipMemsetAsync(totals, 0, 10 * sizeof(uint64_t), s);
+  if (small && chain && chain->ws && g_coh_chain.load(std::memory_order_relaxed)) {
+    // one launch: epoch-tagged granules, counters and totals row the previous launch zeroed
+    if (chain->epoch == 0) {
+      const hipError_t e = hipMemsetAsync(chain->ws, 0, coh_chain_bytes(), s);
+      if (e != hipSuccess) return e;
+      chain->epoch = 1;
+    }
+    const uint64_t span = 64ull * kSCSmall;
+    const uint64_t ns = (n_events + span - 1) / span, full = n_events / span;
+    ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
+    hipLaunchKernelGGL((coh_stream_kernel<kSCSmall, true>), dim3((unsigned)((ns + 3) / 4)),
+                       dim3(256), 0, s, pt, n_pages, events, n_events, ns, full, chain->ws,
+                       nullptr, err, n_nodes, reinterpret_cast<unsigned long long*>(totals),
+                       chain->epoch);
+    const hipError_t e = hipGetLastError();
+    // a launch that did not run leaves its successor's set unzeroed: start the chain over
+    chain->epoch = e != hipSuccess || chain->epoch + 1 >= (1u << 29) ? 0 : chain->epoch + 1;
+    return e;
+  }
   if (coh_workspace_bytes(n_events) > ws_bytes) return hipErrorInvalidValue;
   hipError_t r;
   if (cv == 1 || small) {
@@ -1211,7 +1293,7 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
       auto kern = small ? coh_stream_kernel<kSCSmall> : coh_stream_kernel<kSCBig>;
       unsigned long long* direct = small ? reinterpret_cast<unsigned long long*>(totals) : nullptr;
       hipLaunchKernelGGL(kern, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, s, pt, n_pages,
-                         events, n_events, ns, full, fws, fpart, err, n_nodes, direct);
+                         events, n_events, ns, full, fws, fpart, err, n_nodes, direct, 0u);
     }
     if (small) return hipGetLastError();
     uint64_t g = (ns + 255) / 256;

@@ -28,6 +28,7 @@ struct gdsm_ctx {
   uint64_t coh_ws_bytes = 0;
   uint64_t* coh_pt = nullptr;      // page table: state | faults << 32 per page
   uint64_t* coh_totals = nullptr;  // device 10 x u64
+  gdsm::CohChainState coh_chain;   // small batches without a zeroing launch (allocated on first use)
   uint32_t n_nodes = 0;
   uint32_t diff_bpp = 0;         // stream bytes per page the host last learned (diff geometry)
   std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks

@@ -97,11 +97,19 @@ hipError_t launch_check_ids(const uint32_t* ids, uint64_t n, uint64_t n_pages, u
 uint64_t coh_workspace_bytes(uint64_t n_events);
 // Page table: one u64 per page, state | faults << 32.
 hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hipStream_t s);
+// A context's chain of zero-free small coherence batches (as DiffChain): ws (coh_chain_bytes(),
+// device) holds two sets of ticket counters, totals rows and completion counters, then
+// epoch-tagged status granules; zeroed once (epoch 0: by the next launch). Not for graph capture.
+struct CohChainState {
+  uint64_t* ws = nullptr;
+  uint32_t epoch = 0;
+};
+uint64_t coh_chain_bytes();
 // Events naming a page >= n_pages or a node >= n_nodes reject the batch (err |= 2).
 hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                             const uint64_t* events, uint64_t n_events, uint64_t* totals,
                             uint8_t* ws, uint64_t ws_bytes, uint32_t* err, hipStream_t s,
-                            Prof* prof = nullptr);
+                            Prof* prof = nullptr, CohChainState* chain = nullptr);
 hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,
                              uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,
                              hipStream_t s);

@@ -513,7 +513,7 @@ __device__ __forceinline__ uint64_t guarded_id(const uint32_t* __restrict__ ids,
 // counter (E + 1) & 1 for the next launch, and the look-back counts a granule only when it carries
 // E (granule = flag << 62 | E << 32 | value). The caller's lists are guarded in the kernel (g).
 template <uint32_t kU, uint32_t kBuf, int kWaves, bool kApply, uint32_t kSpill = 0,
-          bool kSolo = false, bool kRetwin = false, uint32_t kChainW = 0>
+          bool kSolo = false, bool kRetwin = false, uint32_t kChainW = 0, uint32_t kSkip = 0>
 __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 256) __attribute__((amdgpu_waves_per_eu(kWaves))) void diff_single_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
@@ -526,6 +526,9 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
   uint8_t* const twin_w = const_cast<uint8_t*>(twin);
   static_assert(!kSolo || (kU == 1 && kSpill == 0), "solo: one-page units, no spill slot");
   constexpr bool kChain = kChainW != 0;  // kChainW: waves per workgroup of the chained form
+  // kSkip (MEASUREMENT ONLY, -DGDSM_MEASURE builds, output invalid): 1 = no home-apply stores,
+  // 2 = no late-record stores (still scanned), 4 = no re-twin stores, 8 = no late path at all,
+  // 16 = no look-back (every unit at offset 0), 32 = no copy of buffered records
   static_assert(!kChain || (kU == 1 && kSpill == 0 && !kSolo), "chain: one-page grid units");
   constexpr bool kGuard = kSolo || kChain;  // the caller's id lists are guarded in this kernel
   const uint64_t tag = kChain ? (uint64_t)sp.epoch << 32 : 0ull;  // granule epoch (kChain)
@@ -615,10 +618,10 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
         dat[rank] = c[k];
       }
       D += (uint32_t)__popcll(B);
-      if (kApply && m[k]) store_masked16(target + pt_ * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
+      if (kApply && !(kSkip & 1) && m[k]) store_masked16(target + pt_ * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
       // (whole chunks: a chunk's clean bytes are equal in TWIN and CURRENT, and TWIN is this
       // writer's own, so no byte stores)
-      if (retwin_now && m[k]) *reinterpret_cast<uint4*>(twin_w + pj * kPage + (k * 64 + lane) * 16u) = c[k];
+      if (!(kSkip & 4) && retwin_now && m[k]) *reinterpret_cast<uint4*>(twin_w + pj * kPage + (k * 64 + lane) * 16u) = c[k];
     }
     if (j + 1 < cnt) {
       pj = ids ? ids[i0 + j + 1] : i0 + j + 1;
@@ -689,7 +692,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
   if (!kSolo && lane == 0)
     __hip_atomic_store(status + u, (u == u0 ? kStIncl : kStAgg) | tag | agg, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-  if (!kSolo && u > u0) {
+  if (!kSolo && !(kSkip & 16) && u > u0) {
     int64_t pos = (int64_t)u - 1;
     for (;;) {
       const int64_t q = pos - (int64_t)lane;
@@ -742,7 +745,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
   // previous user)
   if (kSpill && spilled) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the flushes landed
   const uint64_t all = cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull);
-  for (uint64_t rest = all & ~late; rest;) {  // wave-uniform
+  for (uint64_t rest = (kSkip & 32) ? 0ull : all & ~late; rest;) {  // wave-uniform
     const uint32_t j0 = (uint32_t)__builtin_ctzll(rest);
     const uint64_t above = j0 < 63 ? late & ~((2ull << j0) - 1ull) : 0ull;
     const uint32_t j1 = above ? (uint32_t)__builtin_ctzll(above) : cnt;  // first late page after
@@ -774,7 +777,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
   // that no earlier late page displaced is emitted without reading it again — two dependent
   // round trips less for a dense page of a small release)
   constexpr bool kKeep = kU <= 2;
-  for (uint64_t rem = late; rem;) {  // wave-uniform
+  for (uint64_t rem = (kSkip & 8) ? 0ull : late; rem;) {  // wave-uniform
     const uint32_t j = (uint32_t)__builtin_ctzll(rem);
     const bool first_late = rem == late;
     rem &= rem - 1;
@@ -788,9 +791,13 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
     }
     PageRuns P;
     scan_page(t, c, lane, P);
-    emit_bytes(P, c, lane, data + excl + tab[j]);
+    if (kSkip & 2) {
+      if (P.NR == 12345u) data[lane] = 0;  // keep the scan
+    } else {
+      emit_bytes(P, c, lane, data + excl + tab[j]);
+    }
   }
-  if (kGuard && kRetwin && !retwin_now && excl + tab[1] <= cap) {
+  if (kGuard && kRetwin && !(kSkip & 4) && !retwin_now && excl + tab[1] <= cap) {
     // gdsm_release's re-twin (TWIN := CURRENT, the dirty bytes only), once the record is out: the
     // registers still hold the unit's one page (kKeep: a late page was emitted from them)
 #pragma unroll
@@ -810,6 +817,136 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
       __hip_atomic_store(gen + ticket % kSpillWGs, ticket / kSpillWGs + 1, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// ---- chained release, a page per workgroup (DiffChain lists of up to kChainPerPage pages).
+// A few dense pages are latency: one wave per page issues its page's ~80 home-apply and ~36
+// record store instructions one after another, four cycles per wave64 VALU step. Here the four
+// waves of a workgroup take a quarter of the page each (wave w: chunks 64w .. 64w + 63, one
+// 16-B chunk per lane), so the stores and the run scan of a page are spread over the CU's four
+// SIMDs. The quarters meet through LDS: the edge chunks' masks (a run may cross a quarter),
+// each quarter's run / payload counts and last run start (the record's prefix), and the
+// record's offset in the stream, which wave 0 finds by the decoupled look-back over the chained
+// epoch-tagged granules (as diff_single_kernel<..., kChainW> does; ticket per workgroup, the
+// next launch's counter zeroed). Records are written straight from the registers (run headers
+// and payload bytes, emit_chunk), the home copy's changed bytes with store_masked16, the twin's
+// dirty chunks whole (kRetwin). Same stream, apply and re-twin as every other diff form.
+template <bool kApply, bool kRetwin>
+__global__ __launch_bounds__(256) void release_page_kernel(
+    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
+    uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard g) {
+  uint8_t* const twin_w = const_cast<uint8_t*>(twin);  // (kRetwin: see diff_single_kernel)
+  __shared__ uint32_t edge_first[4], edge_last[4], tot[4], lastst[4];
+  __shared__ uint32_t ticket;
+  __shared__ uint64_t rec_at;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t E = sp.epoch;
+  const uint64_t tag = (uint64_t)E << 32;
+  uint32_t* const ctr = reinterpret_cast<uint32_t*>(ws);
+  if (threadIdx.x == 0) {
+    ticket = atomicAdd(ctr + (E & 1u), 1u);
+    if (blockIdx.x == 0)
+      __hip_atomic_store(ctr + ((E + 1u) & 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint64_t u = ticket;  // one page per workgroup (one stream: first[0] = 0)
+  const uint64_t n = sp.first[1] - sp.first[0];
+  if (u >= n) return;  // workgroup-uniform
+  uint32_t bad = 0;
+  const uint64_t i = sp.first[0] + u;
+  const uint64_t pj = ids ? (g.ids ? guarded_id(ids, i, g.n_pages, bad) : ids[i]) : i;
+  const uint64_t cap = sp.cap[0];
+  const bool ample = kRetwin && cap >= n * GDSM_MAX_RECORD;
+  const uint32_t ch = w * 64 + lane;  // this lane's chunk of the page
+  const uint4 t = ld_nt16(twin + pj * kPage + ch * 16u);
+  const uint4 c = ld_nt16(cur + pj * kPage + ch * 16u);
+  const uint32_t m = diffmask16(t, c);
+  const uint64_t pt = kApply ? (tids ? (g.tids ? guarded_id(tids, i, g.n_pages, bad) : tids[i]) : pj)
+                             : 0;  // page at target
+  if (kApply && m) store_masked16(target + pt * kPage + ch * 16u, m, c);
+  if (ample && m) *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
+  if (lane == 0) edge_first[w] = m;
+  if (lane == 63) edge_last[w] = m;
+  __syncthreads();
+  // run starts / ends with the neighbour chunks' edge bytes (across quarters through LDS)
+  uint32_t up = from_prev_lane(m), dn = from_next_lane(m);
+  if (lane == 0) up = w > 0 ? edge_last[w - 1] : 0u;
+  if (lane == 63) dn = w < 3 ? edge_first[w + 1] : 0u;
+  const uint32_t st = m & ~((m << 1) | ((up >> 15) & 1u)) & 0xFFFFu;
+  const uint32_t en = m & ~((m >> 1) | ((dn & 1u) << 15)) & 0xFFFFu;
+  const uint32_t v = (uint32_t)__popc(en) | ((uint32_t)__popc(m) << 16);  // runs | bytes << 16
+  const uint32_t inc = wave_incl_sum(v);
+  const uint32_t ls = st ? ch * 16u + 32u - (uint32_t)__builtin_clz(st) : 0u;  // last start + 1
+  const uint32_t mx = wave_incl_max(ls);
+  if (lane == 63) {
+    tot[w] = inc;
+    lastst[w] = mx;
+  }
+  __syncthreads();
+  uint32_t carry = 0, cmax = 0, all = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) {
+    if (q < w) {
+      carry += tot[q];
+      cmax = max(cmax, lastst[q]);
+    }
+    all += tot[q];
+  }
+  const uint32_t NR = all & 0xFFFFu, NP = all >> 16;
+  const uint32_t size = NR ? 4u + 4u * NR + ((NP + 3u) & ~3u) : 0u;
+  if (w == 0) {
+    if (g.err && __ballot(bad != 0) && lane == 0) atomicOr(g.err, 8u);
+    uint64_t* status = ws + 1;
+    if (lane == 0)
+      __hip_atomic_store(status + u, (u == 0 ? kStIncl : kStAgg) | tag | size, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    if (u > 0) {
+      int64_t pos = (int64_t)u - 1;
+      auto unpub = [&](uint64_t x) { return (x >> 62) == 0 || ((x >> 32) & 0x3FFFFFFFull) != E; };
+      for (;;) {
+        const int64_t q = pos - (int64_t)lane;
+        uint64_t sw = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : kStIncl | tag;  // before the first page: a prefix of 0
+        while (__ballot(unpub(sw))) {
+          __builtin_amdgcn_s_sleep(1);
+          if (unpub(sw))
+            sw = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint64_t im = __ballot((sw >> 62) == 2);
+        if (im) {
+          const uint32_t kk = (uint32_t)__builtin_ctzll(im);
+          excl += wave_sum_u64(lane <= kk ? (sw & 0xFFFFFFFFull) : 0ull);
+          break;
+        }
+        excl += wave_sum_u64(sw & 0xFFFFFFFFull);
+        pos -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(status + u, kStIncl | tag | (excl + size), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      sp.rec_off[0][u + 1] = excl + size;
+      if (u == 0) sp.rec_off[0][0] = 0;
+      rec_at = excl;
+    }
+  }
+  __syncthreads();
+  const uint64_t at = rec_at;
+  if (at + size > cap) return;  // only records that end inside the capacity are stored (SPEC §3)
+  if (size) {
+    uint8_t* rec = sp.data[0] + at;
+    if (threadIdx.x == 0) {
+      *reinterpret_cast<uint32_t*>(rec) = NR;
+      for (uint32_t q = NP; q & 3u; ++q) rec[4 + 4 * NR + q] = 0;
+    }
+    emit_chunk(ch, st, en, m, max(cmax, from_prev_lane(mx)), carry + inc - v, c,
+               reinterpret_cast<uint32_t*>(rec + 4), rec + 4 + 4 * NR);
+  }
+  if (kRetwin && !ample && m) *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
 }
 
 // ------------------------------------------------------------------------- apply (SPEC §4)
@@ -1453,17 +1590,18 @@ static int apply_variant_from_env() {
   return (v >= 0 && v < kApplyVariants) ? v : 0;
 }
 static std::atomic<int> g_apply_variant{apply_variant_from_env()};
-// Short lists of one-page units (variant 8), gdsm_tune("diff_solo_max", k) and ("diff_chain", W):
-// up to k units the one-workgroup kSolo launch, beyond it the kChain grid launch of W (1 or 4)
-// waves per workgroup when the context offers its DiffChain (W = 0: the grid with its zeroing
-// launch; default 2 = automatic: one wave per workgroup up to kChainOneWave units, spreading a
-// round's byte stores over more CUs, four beyond, where per-wave tickets would queue on the
-// counter). Config 5 at 4 / 8 nodes, same box: 45.3k / 33.7k rounds/s with W = 4, 46.2k / 34.9k
-// with W = 1. Default k = 4: config 5's rounds
-// (~12 dense pages, same box, alternating, rounds/s) 4 nodes 43.0k with k = 16 (every round one
-// workgroup: its waves' byte stores queue on one CU) -> 45.3k with k = 4 (45.5k with k = 0);
-// 8 nodes 32.5k behind the zeroing launch -> 34.1k chained; 1 node k = 4 best by ~1 %.
-constexpr int kSoloDefault = 4;
+// Short lists of one-page units (variant 8), gdsm_tune("diff_solo_max", k) and ("diff_chain", c):
+// up to k units the one-workgroup kSolo launch, beyond it a chained launch when the context
+// offers its DiffChain: c = 1 / 4: diff_single_kernel<..., kChainW> with 1 / 4 waves (pages) per
+// workgroup, c = 3: release_page_kernel (a page per four-wave workgroup), c = 2 (default):
+// release_page_kernel up to kChainPerPage pages, four pages per workgroup beyond (per-page
+// tickets would queue on the counter); c = 0: the grid with its zeroing launch. Release of m
+// dense pages (profiles/r05_release_chain_probe.txt), us per launch, one-workgroup / one page per
+// wave / page per workgroup: m = 1 8.2 / 9.1 / 3.6; m = 10 11.9 / 12.0 / 6.1; m = 200 (four
+// pages per workgroup 12.5) / 13.2 / 8.5; m = 2048 four per workgroup 30.7, page per workgroup
+// 45.1. Default k = 0: the one-workgroup form (up to kSoloUnits pages) serves graph capture,
+// which has no chain, and callers without a context.
+constexpr int kSoloDefault = 0;
 // (also GDSM_DIFF_SOLO_MAX / GDSM_DIFF_CHAIN at load)
 static int env_int(const char* name, int lo, int hi, int dflt) {
   const char* e = getenv(name);
@@ -1471,8 +1609,11 @@ static int env_int(const char* name, int lo, int hi, int dflt) {
   return (e && v >= lo && v <= hi) ? v : dflt;
 }
 static std::atomic<int> g_solo_max{env_int("GDSM_DIFF_SOLO_MAX", 0, (int)kSoloUnits, kSoloDefault)};
-constexpr uint64_t kChainOneWave = 64;
+constexpr uint64_t kChainPerPage = 512;
 static std::atomic<int> g_chain{env_int("GDSM_DIFF_CHAIN", 0, 4, 2)};
+#ifdef GDSM_MEASURE
+static std::atomic<int> g_diff_skip{0};  // the chained release's kSkip (measurement builds)
+#endif
 
 
 int tune(const char* key, int64_t value) {
@@ -1484,7 +1625,13 @@ int tune(const char* key, int64_t value) {
     g_solo_max.store((int)value, std::memory_order_relaxed);
     return 0;
   }
-  if (!strcmp(key, "diff_chain") && (value == 0 || value == 1 || value == 2 || value == 4)) {
+#ifdef GDSM_MEASURE
+  if (!strcmp(key, "diff_skip") && value >= 0 && value < 64) {
+    g_diff_skip.store((int)value, std::memory_order_relaxed);
+    return 0;
+  }
+#endif
+  if (!strcmp(key, "diff_chain") && value >= 0 && value <= 4) {
     g_chain.store((int)value, std::memory_order_relaxed);
     return 0;
   }
@@ -1743,7 +1890,35 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
     const IdGuard g = guard ? *guard : IdGuard{};
     ProfScope ps(prof, GDSM_PROF_DIFF, s);
     const int cw = g_chain.load(std::memory_order_relaxed);
-    const uint32_t W = cw == 1 || (cw == 2 && nunits <= kChainOneWave) ? 1 : 4;  // waves / group
+    if (cw == 3 || (cw == 2 && nunits <= kChainPerPage)) {  // a page per four-wave workgroup
+      auto kp = retwin ? (target ? release_page_kernel<true, true> : release_page_kernel<false, true>)
+                       : (target ? release_page_kernel<true, false> : release_page_kernel<false, false>);
+      hipLaunchKernelGGL(kp, dim3((unsigned)nunits), dim3(256), 0, s, twin, cur, ids, sp, chain->ws,
+                         target, tids, g);
+      const hipError_t e = hipGetLastError();
+      chain->epoch = e != hipSuccess || chain->epoch + 1 >= (1u << 30) ? 0 : chain->epoch + 1;
+      return e;
+    }
+    const uint32_t W = cw == 1 ? 1 : 4;  // waves per workgroup
+#ifdef GDSM_MEASURE
+    if (g_diff_skip.load(std::memory_order_relaxed) && retwin && target && W == 1) {
+      const int k = g_diff_skip.load(std::memory_order_relaxed);
+      auto km = k == 1   ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 1>
+                : k == 2  ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 2>
+                : k == 4  ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 4>
+                : k == 5  ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 5>
+                : k == 8  ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 8>
+                : k == 13 ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 13>
+                : k == 16 ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 16>
+                : k == 32 ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 32>
+                          : diff_single_kernel<1, 8192, 4, true, 0, false, true, 1, 61>;
+      hipLaunchKernelGGL(km, dim3((unsigned)nunits), dim3(64), 0, s, twin, cur, ids, sp, chain->ws,
+                         target, nullptr, nullptr, tids, g);
+      const hipError_t e = hipGetLastError();
+      chain->epoch = e != hipSuccess || chain->epoch + 1 >= (1u << 30) ? 0 : chain->epoch + 1;
+      return e;
+    }
+#endif
     auto kern = W == 1 ? (retwin ? (target ? diff_single_kernel<1, 8192, 4, true, 0, false, true, 1>
                                            : diff_single_kernel<1, 8192, 4, false, 0, false, true, 1>)
                                  : (target ? diff_single_kernel<1, 8192, 4, true, 0, false, false, 1>

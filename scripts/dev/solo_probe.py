@@ -4,10 +4,11 @@ each, was one diff_single_kernel<..., kSolo> launch of ~13 us, the round's criti
 Pages of doubles holding integers (C = A x B of test_mmult: two or three nonzero high bytes per
 double, ~500 runs a page) against zero twins, m pages per launch, `reps` launches per case:
 gdsm_diff, and gdsm_release applying to the home copy with re-twin (TWIN zeroed again by a
-gdsm_memcpy_batch copy kernel between launches), each under the launch forms named: `auto` (the library's choice), `chain`,
-`chain1`, `chain4` (gdsm_tune diff_solo_max 0: the chained grid launch from one page up, one
-wave per workgroup up to 128 pages / always one / always four) and `prep` (diff_chain 0: past 16
-pages the grid behind its zeroing launch). m = 9 is the clean case (CURRENT == TWIN),
+gdsm_memcpy_batch copy kernel between launches), under the launch forms named: `auto` (the
+library's choice), `chain1` / `chain4` / `page` (the chained launch from one page up: one page
+per one-wave workgroup / four pages per workgroup / a page per four-wave workgroup), `solo` (the
+one-workgroup launch up to 16 pages, then automatic) and `prep` (one workgroup up to 16 pages,
+then the grid behind its zeroing launch). m = 9 is the clean case (CURRENT == TWIN),
 m = 11 the sparse one (one double a page). Run under rocprofv3 --kernel-trace and read with
 scripts/dev/kstats.py (the cases differ by kernel, grid or workgroup size).
 
@@ -22,7 +23,8 @@ import gallocy_amd as ga  # noqa: E402
 
 PAGE = 4096
 CASES = ((1, "dense"), (4, "dense"), (10, "dense"), (16, "dense"), (9, "clean"), (11, "sparse"),
-         (20, "dense"), (32, "dense"), (64, "dense"), (200, "dense"), (2048, "dense"))
+         (20, "dense"), (32, "dense"), (64, "dense"), (200, "dense"), (512, "dense"),
+         (1024, "dense"), (2048, "dense"))
 
 
 def dense_pages(m, seed):
@@ -41,8 +43,9 @@ def main():
     d_zero = ctx.buffer(n * PAGE).upload(zeros)
     twin_ptr = ctx.arena_ptr("twin")
     for form in forms:
-        L.gdsm_tune(b"diff_solo_max", 0 if form.startswith("chain") else 4)
-        L.gdsm_tune(b"diff_chain", {"prep": 0, "chain1": 1, "chain4": 4}.get(form, 2))
+        L.gdsm_tune(b"diff_solo_max", 16 if form in ("prep", "solo") else 0)
+        L.gdsm_tune(b"diff_chain", {"prep": 0, "chain1": 1, "chain4": 4, "page": 3,
+                                     "solo": 2}.get(form, 2))
         for m, kind in CASES:
             if form != "auto" and m in (9, 11):
                 continue
@@ -71,7 +74,7 @@ def main():
             out.free()
             ids.free()
             d_desc.free()
-    L.gdsm_tune(b"diff_solo_max", 4)
+    L.gdsm_tune(b"diff_solo_max", 0)
     L.gdsm_tune(b"diff_chain", 2)
     ctx.close()
 

@@ -322,3 +322,68 @@ def test_coherence_at_the_maximum_table_size():
     with ga.Context(n + 1, arenas=()) as c:
         with pytest.raises(GdsmError):
             c.coh_init(8)
+
+
+def test_chained_small_batches_across_launches_and_graphs():
+    """Batches of up to 2^20 events take the chained one-launch fold (CohChain: epoch-tagged
+    status granules; ticket counters, totals row and completion counter zeroed by the previous
+    launch; the last span to finish copies the totals out). Twenty-odd batches in a row of varying
+    size, mixed with whole-GPU batches (> 2^20 events, the zeroing path), a graph of a small batch
+    replayed between them (captured launches take the zeroing form), the chain switched off and
+    on, and a rejected batch: every batch's totals and the final page table equal the oracle's."""
+    n, nodes = 6000, 8
+    rng = np.random.default_rng(31)
+    L = ga.gdsm.lib()
+
+    def batch(k, seed):
+        counts = np.bincount(rng.integers(0, n, k), minlength=n).astype(np.uint64)
+        return oracle.gen_events(counts, seed=seed, n_nodes=nodes, write_pct=25)
+
+    with ga.Context(n, arenas=()) as c:
+        c.coh_init(nodes)
+        st, fl = oracle.coh_init(n, nodes)
+        gev = batch(3000, 7)
+        d_gev = c.buffer(gev.nbytes).upload(gev)
+        d_gtot = c.buffer(80)
+        ga.gdsm.check(L.gdsm_reserve(c.handle, 0, 1 << 21), "gdsm_reserve")
+        c.sync()
+        c.capture_begin()
+        ga.gdsm.check(L.gdsm_coherence_batch_async(c.handle, d_gev.ptr, len(gev), d_gtot.ptr),
+                      "coherence")
+        graph = c.capture_end()
+        sizes = [1, 300, 8000, 257, 256, 70000, 1 << 20, 4096, (1 << 20) + 5, 50000, 12, 9000]
+        try:
+            for it, k in enumerate(sizes * 2):
+                if it == 6:
+                    assert L.gdsm_tune(b"coh_chain", 0) == 0
+                if it == 9:
+                    assert L.gdsm_tune(b"coh_chain", 1) == 0
+                ev = batch(k, 100 + it)
+                tot = c.coherence_batch(ev)
+                rc, otot = oracle.coherence(st, fl, ev, n_nodes=nodes)
+                assert rc == 0 and tot == otot, (it, k)
+                if it % 5 == 2:
+                    graph.launch(c)
+                    c.sync()
+                    rc, otot = oracle.coherence(st, fl, gev, n_nodes=nodes)
+                    got = d_gtot.download(np.uint64, 10)
+                    assert rc == 0
+                    assert got.tolist() == [otot["invalidations"], otot["transfers"],
+                                            *otot["node_faults"]], it
+            gst, gfl = c.coh_download()
+            assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+            with pytest.raises(GdsmError) as ei:  # rejected inside the chain, which goes on
+                c.coherence_batch(np.array([5 << 4, 2 << 4], np.uint64))
+            assert ei.value.errno == 22
+            c.coh_init(nodes)
+            st, fl = oracle.coh_init(n, nodes)
+            for it in range(5):
+                ev = batch(1000 * (it + 1), 500 + it)
+                tot = c.coherence_batch(ev)
+                rc, otot = oracle.coherence(st, fl, ev, n_nodes=nodes)
+                assert rc == 0 and tot == otot, it
+            gst, gfl = c.coh_download()
+            assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+        finally:
+            L.gdsm_tune(b"coh_chain", 1)
+            graph.destroy()

@@ -1012,8 +1012,9 @@ def test_chained_short_lists_across_launches_and_graphs():
     granules, ticket counters the previous launch zeroed, no zeroing launch). Forty launches in a
     row of varying length and kind (diff, diff_apply_ids, release), mixed with one-workgroup
     (<= 16 pages) and zeroing-launch (3000 pages) diffs, a graph of a short diff replayed between
-    them (captured launches take the zeroing form), the chain switched off, to four-wave workgroups
-    and back to automatic (one wave per workgroup up to 64 pages), and a
+    them (captured launches take the zeroing form), every chained form in turn (gdsm_tune
+    "diff_chain": zeroing grid, one or four pages per workgroup, a page per four-wave workgroup,
+    automatic), and a
     list with an out-of-range id (-EINVAL at the sync, the valid records still right): every
     stream equals the oracle's and every home-copy page is right."""
     n = 4096
@@ -1037,8 +1038,11 @@ def test_chained_short_lists_across_launches_and_graphs():
         sizes = [17, 2048, 1, 300, 3000, 64, 16, 1999, 33, 500] * 4
         try:
             for it, m in enumerate(sizes):
-                if it in (20, 26, 33):  # the zeroing form, four-wave workgroups, then automatic
-                    assert L.gdsm_tune(b"diff_chain", {20: 0, 26: 4, 33: 2}[it]) == 0
+                # every chained form: the zeroing grid, one / four pages per workgroup, a page
+                # per four-wave workgroup at every length, then automatic
+                toggles = {20: 0, 24: 1, 28: 4, 32: 3, 37: 2}
+                if it in toggles:
+                    assert L.gdsm_tune(b"diff_chain", toggles[it]) == 0
                 ids = rng.choice(n, m, replace=False).astype(np.uint32)
                 kind = it % 3
                 if kind == 0:
