@@ -82,6 +82,9 @@ def parse():
                          "per round); off = a twin launch before the round's writes (round 4)")
     ap.add_argument("--graph", action="store_true",
                     help="mmult: replay one HIP graph of every round instead of eager launches")
+    ap.add_argument("--driver", choices=["native", "python"], default="native",
+                    help="mmult: rounds issued by the C++ loop over the C ABI "
+                         "(gallocy_amd/native/replay.cpp) or from Python")
     ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
     ap.add_argument("--coh-pages", type=int, default=16 << 20, help="coherence: pages")
     ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
@@ -658,18 +661,32 @@ def run_mmult(args):
     # (the kernels' code objects loaded and the host paths warm: a cold first replay in a fresh
     # process takes ~1.5x as long per round); the timed replay starts from a fresh state again
     warm_rounds = 0
+    def replay(driver):
+        return MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed,
+                           retwin=args.retwin == "on", driver=driver)
+
     if args.warmup > 0:
-        R0 = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed,
-                         retwin=args.retwin == "on")
+        R0 = replay(args.driver)
         R0.run(graph=args.graph)
         warm_rounds = R0.T.rounds
         R0.close()
-    R = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed, retwin=args.retwin == "on")
+    R = replay(args.driver)
     dt = R.run(graph=args.graph)
+    # the same replay (warm, fresh state) with every round issued from Python, reported beside
+    other = None
+    if not args.graph and args.driver == "native":
+        R3 = replay("python")
+        dt3 = R3.run()
+        ok3 = bool(np.array_equal(R3.home_copy(), R3.final_image()))
+        R3.close()
+        other = {"value": round(R.T.rounds / dt3, 1), "unit": "rounds/s",
+                 "note": "the same warm replay with each round's calls issued from Python "
+                         "(MmultReplay.round, ~1 us of interpreter per call)",
+                 "home_copy_equals_product": ok3}
     ok = bool(np.array_equal(R.home_copy(), R.final_image()))
     # latency breakdown: the same replay again on a fresh state with per-launch HIP events (a
     # separate run, so the events do not weigh on `value`)
-    R2 = MmultReplay(ndim=args.ndim, nodes=args.nodes, seed=args.seed, retwin=args.retwin == "on")
+    R2 = replay(args.driver)
     R2.data.prof_enable(True)
     R2.pt.prof_enable(True)
     dt2 = R2.run(graph=False)
@@ -707,7 +724,11 @@ def run_mmult(args):
                       "events": R.events_total, "pages_diffed": R.pages_diffed},
            "seconds_total": round(dt, 4),
            "launch": f"one HIP graph of every round (recorded in {R.graph_build_s:.2f} s, untimed)"
-                     if args.graph else "eager, two streams",
+                     if args.graph else ("eager, two streams, rounds issued by the C++ loop over "
+                                         "the C ABI (gallocy_amd/native/replay.cpp)"
+                                         if args.driver == "native" else
+                                         "eager, two streams, rounds issued from Python"),
+           "python_rounds": other,
            "round": ("coherence batch | the round's row writes (one batched copy), the release "
                      "applying its runs to the home copies and re-twinning its pages "
                      "(gdsm_release)") if args.retwin == "on" else

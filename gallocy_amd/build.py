@@ -101,6 +101,24 @@ def build_sanitized(verbose: bool = False) -> Path:
     return lib
 
 
+REPLAY = LIBDIR / "libgdsm_replay.so"
+
+
+def build_replay(verbose: bool = False) -> Path:
+    """The C++ round loop of config 5's replay (gallocy_amd/native/replay.cpp) over libgdsm.so's
+    C ABI, for bench.py / replay.py (a bench driver, not part of libgdsm)."""
+    src = PKG / "native" / "replay.cpp"
+    if not _stale(REPLAY, [src, ROOT / "include" / "gdsm.h", LIB]):
+        return REPLAY
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-fPIC", "-shared",
+           "-I", str(ROOT / "include"), str(src), "-L", str(LIBDIR), "-lgdsm",
+           "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined", "-o", str(REPLAY)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return REPLAY
+
+
 def build_test_drivers(verbose: bool = False) -> None:
     """Compiled C++ callers of libgdsm.so used by the tests (tests/cpp/, output in _build/)."""
     subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "cpp")], check=True,
@@ -121,6 +139,7 @@ if __name__ == "__main__":
         print(build_sanitized(verbose=True))
         sys.exit(0)
     build_lib(force="--force" in sys.argv, verbose=True)
+    build_replay(verbose=True)
     build_test_drivers(verbose=True)
     build_oracle(verbose=True)
     print(LIB)

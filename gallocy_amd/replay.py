@@ -21,23 +21,55 @@ Per round (one row per node, gallocy_amd/trace.py):
      read-modify-write race.
 The trace, the rows' values and the page lists are prepared on the host before the timed
 replay; a round is then only asynchronous launches on two streams (page table, page data),
-or, with run(graph=True), one HIP graph of all rounds recorded beforehand.
+issued by the C++ round loop (driver="native", gallocy_amd/native/replay.cpp: the host side of a
+C++ DSM runtime over the C ABI) or by Python (driver="python", round()), or, with
+run(graph=True), one HIP graph of all rounds recorded beforehand.
 At the end the home copies must equal the zone after the whole multiplication, and the page
 table / totals must equal the oracle's sequential fold of the same events.
 """
 from __future__ import annotations
 
+import ctypes as C
 import time
+from pathlib import Path
 
 import numpy as np
 
-from . import gdsm
+from . import _lib, gdsm
 from .trace import PAGE_SZ, MmultTrace, c_row_values, mmult_layout, zone_image
+
+
+_NATIVE = None
+
+
+def native_driver():
+    """gallocy_amd/lib/libgdsm_replay.so (gallocy_amd/native/replay.cpp), which links the in-tree
+    libgdsm.so: only with that library loaded (not a GDSM_LIB build: two copies of the library in
+    one process would not share contexts)."""
+    global _NATIVE
+    if _NATIVE is None:
+        libdir = Path(_lib.__file__).resolve().parent / "lib"
+        if _lib.LIB_PATH.resolve() != (libdir / "libgdsm.so").resolve():
+            raise RuntimeError(f"driver='native' needs the in-tree libgdsm.so, not {_lib.LIB_PATH}")
+        _lib.load()
+        path = libdir / "libgdsm_replay.so"
+        if not path.exists():
+            raise RuntimeError(f"{path} is missing: build it (python -m gallocy_amd.build)")
+        d = C.CDLL(str(path))
+        vp, i64p = C.c_void_p, C.c_void_p
+        d.gdsm_replay_mmult.restype = C.c_int
+        d.gdsm_replay_mmult.argtypes = [vp, vp, C.c_uint32, C.c_uint32, vp, i64p, vp, vp, vp, i64p,
+                                        vp, i64p, vp, C.c_int]
+        _NATIVE = d
+    return _NATIVE
 
 
 class MmultReplay:
     def __init__(self, ndim: int = 1000, nodes: int = 4, seed: int = 0, device: int = 0,
-                 fused: bool = True, retwin: bool = True):
+                 fused: bool = True, retwin: bool = True, driver: str = "native"):
+        if driver not in ("native", "python"):
+            raise ValueError(driver)
+        self.driver = driver
         self.fused = fused
         # retwin: every release refreshes its pages' twins (gdsm_release, GDSM_RELEASE_RETWIN), so
         # a round needs no twin step: TWIN == CURRENT from the upload on, as after a release
@@ -148,6 +180,21 @@ class MmultReplay:
             self.data.sync()
             dt = time.perf_counter() - t0
             g.destroy()
+        elif self.driver == "native" and self.fused:
+            drv = native_driver()
+            ev_off = np.ascontiguousarray(self.ev_off, np.int64)
+            id_off = np.ascontiguousarray(self.id_off, np.int64)
+            desc_off = np.ascontiguousarray(self.desc_off, np.int64)
+            t0 = time.perf_counter()
+            rc = drv.gdsm_replay_mmult(self.data.handle, self.pt.handle, 0, self.T.rounds,
+                                       self.d_events.ptr, ev_off.ctypes.data, self.d_tot.ptr,
+                                       self.d_ids.ptr, self.d_home.ptr, id_off.ctypes.data,
+                                       self.d_desc.ptr, desc_off.ctypes.data,
+                                       C.byref(self._runs.s), int(self.retwin))
+            gdsm.check(rc, "gdsm_replay_mmult")
+            self.data.sync()
+            self.pt.sync()
+            dt = time.perf_counter() - t0
         else:
             t0 = time.perf_counter()
             for r in range(self.T.rounds):

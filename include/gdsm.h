@@ -429,7 +429,11 @@ int gdsm_coherence_notify(gdsm_ctx* ctx, gdsm_comm* comm, const uint64_t* batch,
                           uint64_t* n_notices);
 
 const char* gdsm_version(void);
-/* Process-wide kernel-variant knobs for measurement, e.g. ("diff_variant", 0..4). */
+/* Process-wide kernel-variant knobs for measurement (every value produces the same results):
+ * "diff_variant" 0..8 (diff geometry), "apply_variant" 0..7, "diff_solo_max" 0..16 and
+ * "diff_chain" 0..4 (short lists: one-workgroup / chained forms), "coh_variant" 0..2,
+ * "coh_chain" 0|1 (small coherence batches without the zeroing launch). Returns 0, or -EINVAL
+ * for an unknown key or value. */
 int gdsm_tune(const char* key, int64_t value);
 /* Test hook: the nth next growth of one of ctx's internal workspaces fails with -ENOMEM (0 = off).
  * Used to show that a collective call refuses on every rank together when one rank fails. */

@@ -150,6 +150,23 @@ def test_tune_rejects_measurement_only_variants():
                     (b"coh_variant", 0), (b"coh_variant", 1), (b"coh_variant", 2)):
         assert L.gdsm_tune(key, ok) == 0
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0
+    # the short-list and small-batch launch forms (all valid); kSkip only in measurement builds
+    for key, bad in ((b"diff_skip", 1), (b"diff_solo_max", 17), (b"diff_chain", 5),
+                     (b"coh_chain", 2)):
+        assert L.gdsm_tune(key, bad) == -22, (key, bad)
+    for key, ok, default in ((b"diff_solo_max", 16, 0), (b"diff_chain", 3, 2), (b"coh_chain", 0, 1)):
+        assert L.gdsm_tune(key, ok) == 0 and L.gdsm_tune(key, default) == 0
+
+
+def test_native_replay_driver_exports_its_loop():
+    """libgdsm_replay.so (gallocy_amd/native/replay.cpp, config 5's C++ round loop over the C ABI)
+    links the in-tree libgdsm.so and exports gdsm_replay_mmult, which refuses null contexts
+    before touching any."""
+    from gallocy_amd.replay import native_driver
+    d = native_driver()
+    z = np.zeros(2, np.int64)
+    assert d.gdsm_replay_mmult(None, None, 0, 1, None, z.ctypes.data, None, None, None,
+                               z.ctypes.data, None, z.ctypes.data, None, 1) == -22
 
 
 def test_release_argument_checks():

@@ -18,10 +18,21 @@ pytestmark = pytest.mark.gpu
 def test_mmult_replay_end_to_end(ndim, nodes, graph, fused):
     """NDIM = 1000 is BASELINE config 5's size (test/test_mmult.cpp:103-180 uses
     NDIM up to 1021 before the reference heap aborts). graph: every round recorded into one HIP
-    graph (gdsm_capture_*) and replayed by one launch, or issued eagerly (the default). fused:
-    the diff kernel applies the runs to the home copies (gdsm_diff_apply_ids), or a separate
-    apply of the stream does."""
-    R = MmultReplay(ndim=ndim, nodes=nodes, seed=7, fused=fused)
+    graph (gdsm_capture_*) and replayed by one launch, or issued eagerly (the default: the C++
+    round loop, gallocy_amd/native/replay.cpp). fused: the diff kernel applies the runs to the
+    home copies (gdsm_diff_apply_ids), or a separate apply of the stream does (Python rounds)."""
+    _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, fused=fused), nodes, graph)
+
+
+@pytest.mark.parametrize("ndim,nodes,retwin", [(1000, 4, True), (257, 3, False), (64, 8, True)])
+def test_mmult_replay_python_rounds(ndim, nodes, retwin):
+    """The same replay with every round issued from Python (MmultReplay.round, driver="python"),
+    with and without the re-twinning release: the same home copies, totals and page table."""
+    _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, retwin=retwin, driver="python"),
+                  nodes, False)
+
+
+def _check_replay(R, nodes, graph):
     try:
         R.run(graph=graph)
         assert np.array_equal(R.home_copy(), R.final_image())
