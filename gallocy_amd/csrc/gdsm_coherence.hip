@@ -1210,7 +1210,20 @@ static std::atomic<int> g_coh_variant{coh_variant_from_env()};
 // Small batches of a context outside graph capture: the chained one-launch form (CohChain) unless
 // gdsm_tune("coh_chain", 0) or GDSM_COH_CHAIN=0 at load (then the zeroing launch before the fold).
 static std::atomic<int> g_coh_chain{getenv("GDSM_COH_CHAIN") && atoi(getenv("GDSM_COH_CHAIN")) == 0 ? 0 : 1};
+// the chained fold's span (gdsm_tune("coh_span", 1 | 2 | 4) 64-event chunks, GDSM_COH_SPAN).
+// Config 5, same box, rounds/s, span 4 / 2 / 1 (and 8, not kept): 4 nodes 93.6k / 95.4k / 85.0k
+// (71.6k); 8 nodes 83.1k / 73.8k / 60.8k (66.3k); 1 node 94.3k / 96.2k (71.2k).
+static int coh_span_from_env() {
+  const char* e = getenv("GDSM_COH_SPAN");
+  const int v = e ? atoi(e) : 4;
+  return (v == 1 || v == 2 || v == 4) ? v : 4;
+}
+static std::atomic<int> g_coh_span{coh_span_from_env()};
 int coh_tune(const char* key, int64_t value) {
+  if (!strcmp(key, "coh_span") && (value == 1 || value == 2 || value == 4)) {
+    g_coh_span.store((int)value, std::memory_order_relaxed);
+    return 0;
+  }
   if (!strcmp(key, "coh_chain") && (value == 0 || value == 1)) {
     g_coh_chain.store((int)value, std::memory_order_relaxed);
     return 0;
@@ -1247,7 +1260,7 @@ hipError_t launch_coh_init(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes, hip
 }
 
 uint64_t coh_chain_bytes() {
-  return 8 * (kCohChainStatus + (kCohSmall + 64 * kSCSmall - 1) / (64 * kSCSmall));
+  return 8 * (kCohChainStatus + kCohSmall / 64);  // spans of at least one 64-event chunk
 }
 
 hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
@@ -1264,13 +1277,16 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
       if (e != hipSuccess) return e;
       chain->epoch = 1;
     }
-    const uint64_t span = 64ull * kSCSmall;
+    const uint32_t sc = (uint32_t)g_coh_span.load(std::memory_order_relaxed);  // chunks per span
+    const uint64_t span = 64ull * sc;
     const uint64_t ns = (n_events + span - 1) / span, full = n_events / span;
     ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
-    hipLaunchKernelGGL((coh_stream_kernel<kSCSmall, true>), dim3((unsigned)((ns + 3) / 4)),
-                       dim3(256), 0, s, pt, n_pages, events, n_events, ns, full, chain->ws,
-                       nullptr, err, n_nodes, reinterpret_cast<unsigned long long*>(totals),
-                       chain->epoch);
+    auto kern = sc == 1   ? coh_stream_kernel<1, true>
+                : sc == 2 ? coh_stream_kernel<2, true>
+                          : coh_stream_kernel<kSCSmall, true>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, s, pt, n_pages, events,
+                       n_events, ns, full, chain->ws, nullptr, err, n_nodes,
+                       reinterpret_cast<unsigned long long*>(totals), chain->epoch);
     const hipError_t e = hipGetLastError();
     // a launch that did not run leaves its successor's set unzeroed: start the chain over
     chain->epoch = e != hipSuccess || chain->epoch + 1 >= (1u << 29) ? 0 : chain->epoch + 1;

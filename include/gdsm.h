@@ -432,7 +432,8 @@ const char* gdsm_version(void);
 /* Process-wide kernel-variant knobs for measurement (every value produces the same results):
  * "diff_variant" 0..8 (diff geometry), "apply_variant" 0..7, "diff_solo_max" 0..16 and
  * "diff_chain" 0..4 (short lists: one-workgroup / chained forms), "coh_variant" 0..2,
- * "coh_chain" 0|1 (small coherence batches without the zeroing launch). Returns 0, or -EINVAL
+ * "coh_chain" 0|1 (small coherence batches without the zeroing launch), "coh_span" 1|2|4 (their
+ * span, in 64-event chunks). Returns 0, or -EINVAL
  * for an unknown key or value. */
 int gdsm_tune(const char* key, int64_t value);
 /* Test hook: the nth next growth of one of ctx's internal workspaces fails with -ENOMEM (0 = off).
