@@ -711,9 +711,10 @@ def run_mmult(args):
                "stages": stages,
                "note": "a round is ~10 dense pages (~500 runs each) and ~8000 fault events: "
                        "every operation is a few microseconds of dependent latency, so the round "
-                       "is its operation count on the longer of two streams (page data: twin, "
-                       "row writes, diff+apply; page table: the coherence batch). No HBM or "
-                       "MFMA roofline applies."}
+                       "is the longer of two streams (page data: the row writes' batched copy, "
+                       "then one release launch that diffs, applies to the home copies and "
+                       "re-twins; page table: one coherence fold launch) or the host's issue "
+                       "time for the three calls. No HBM or MFMA roofline applies."}
     res = {"metric": "mmult trace replay rounds/sec", "value": round(R.T.rounds / dt, 1),
            "unit": "rounds/s", "n_gpus": 1, "steps": R.T.rounds, "warmup": warm_rounds,
            "ms_per_step": round(dt / R.T.rounds * 1e3, 4), "higher_is_better": True,
