@@ -2,7 +2,7 @@
 on fresh states: issue time of the whole round loop (no sync inside) against the time to the end
 of the GPU work, and the host time spent in each call of a round (perf_counter around it).
 
-    python scripts/dev/mmult_host_probe.py [nodes]"""
+    python scripts/dev/mmult_host_probe.py [nodes] [native]"""
 import json
 import sys
 import time
@@ -13,8 +13,41 @@ from gallocy_amd import gdsm  # noqa: E402
 from gallocy_amd.replay import MmultReplay  # noqa: E402
 
 
+def native(nodes):
+    """The C++ round loop: time until gdsm_replay_mmult returns (issue) and until both streams
+    drain (end)."""
+    import ctypes as C
+
+    import numpy as np
+    from gallocy_amd.replay import native_driver
+    drv = native_driver()
+    for rep in range(4):
+        R = MmultReplay(ndim=1000, nodes=nodes, seed=1, retwin=True)
+        R.data.sync()
+        R.pt.sync()
+        ev_off = np.ascontiguousarray(R.ev_off, np.int64)
+        id_off = np.ascontiguousarray(R.id_off, np.int64)
+        desc_off = np.ascontiguousarray(R.desc_off, np.int64)
+        t0 = time.perf_counter()
+        rc = drv.gdsm_replay_mmult(R.data.handle, R.pt.handle, 0, R.T.rounds, R.d_events.ptr,
+                                   ev_off.ctypes.data, R.d_tot.ptr, R.d_ids.ptr, R.d_home.ptr,
+                                   id_off.ctypes.data, R.d_desc.ptr, desc_off.ctypes.data,
+                                   C.byref(R._runs.s), 1)
+        t_issue = time.perf_counter() - t0
+        R.data.sync()
+        R.pt.sync()
+        t_all = time.perf_counter() - t0
+        assert rc == 0
+        print(json.dumps({"driver": "native", "nodes": nodes, "rep": rep,
+                          "issue_us_per_round": round(t_issue / R.T.rounds * 1e6, 2),
+                          "end_us_per_round": round(t_all / R.T.rounds * 1e6, 2)}), flush=True)
+        R.close()
+
+
 def main():
     nodes = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    if len(sys.argv) > 2 and sys.argv[2] == "native":
+        return native(nodes)
     for rep in range(3):
         R = MmultReplay(ndim=1000, nodes=nodes, seed=1, retwin=True)
         R.data.sync()
