@@ -152,9 +152,10 @@ def test_tune_rejects_measurement_only_variants():
     assert L.gdsm_tune(b"diff_variant", 0) == 0 and L.gdsm_tune(b"coh_variant", 0) == 0
     # the short-list and small-batch launch forms (all valid); kSkip only in measurement builds
     for key, bad in ((b"diff_skip", 1), (b"diff_solo_max", 17), (b"diff_chain", 5),
-                     (b"coh_chain", 2)):
+                     (b"coh_chain", 2), (b"coh_span", 8)):
         assert L.gdsm_tune(key, bad) == -22, (key, bad)
-    for key, ok, default in ((b"diff_solo_max", 16, 0), (b"diff_chain", 3, 2), (b"coh_chain", 0, 1)):
+    for key, ok, default in ((b"diff_solo_max", 16, 0), (b"diff_chain", 3, 2), (b"coh_chain", 0, 1),
+                             (b"coh_span", 2, 4)):
         assert L.gdsm_tune(key, ok) == 0 and L.gdsm_tune(key, default) == 0
 
 

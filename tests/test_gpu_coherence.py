@@ -324,13 +324,15 @@ def test_coherence_at_the_maximum_table_size():
             c.coh_init(8)
 
 
-def test_chained_small_batches_across_launches_and_graphs():
+@pytest.mark.parametrize("span", [4, 1])
+def test_chained_small_batches_across_launches_and_graphs(span):
     """Batches of up to 2^20 events take the chained one-launch fold (CohChain: epoch-tagged
     status granules; ticket counters, totals row and completion counter zeroed by the previous
     launch; the last span to finish copies the totals out). Twenty-odd batches in a row of varying
     size, mixed with whole-GPU batches (> 2^20 events, the zeroing path), a graph of a small batch
     replayed between them (captured launches take the zeroing form), the chain switched off and
-    on, and a rejected batch: every batch's totals and the final page table equal the oracle's."""
+    on, and a rejected batch: every batch's totals and the final page table equal the oracle's.
+    span: the chained fold's 64-event chunks per span (gdsm_tune "coh_span"; 4 is the default)."""
     n, nodes = 6000, 8
     rng = np.random.default_rng(31)
     L = ga.gdsm.lib()
@@ -339,6 +341,7 @@ def test_chained_small_batches_across_launches_and_graphs():
         counts = np.bincount(rng.integers(0, n, k), minlength=n).astype(np.uint64)
         return oracle.gen_events(counts, seed=seed, n_nodes=nodes, write_pct=25)
 
+    assert L.gdsm_tune(b"coh_span", span) == 0
     with ga.Context(n, arenas=()) as c:
         c.coh_init(nodes)
         st, fl = oracle.coh_init(n, nodes)
@@ -386,4 +389,5 @@ def test_chained_small_batches_across_launches_and_graphs():
             assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
         finally:
             L.gdsm_tune(b"coh_chain", 1)
+            L.gdsm_tune(b"coh_span", 4)
             graph.destroy()
