@@ -82,9 +82,10 @@ def parse():
                          "per round); off = a twin launch before the round's writes (round 4)")
     ap.add_argument("--graph", action="store_true",
                     help="mmult: replay one HIP graph of every round instead of eager launches")
-    ap.add_argument("--driver", choices=["native", "python"], default="native",
+    ap.add_argument("--driver", choices=["native", "native2", "python"], default="native",
                     help="mmult: rounds issued by the C++ loop over the C ABI "
-                         "(gallocy_amd/native/replay.cpp) or from Python")
+                         "(gallocy_amd/native/replay.cpp; native2: two host threads, one per "
+                         "context) or from Python")
     ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
     ap.add_argument("--coh-pages", type=int, default=16 << 20, help="coherence: pages")
     ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
@@ -674,7 +675,7 @@ def run_mmult(args):
     dt = R.run(graph=args.graph)
     # the same replay (warm, fresh state) with every round issued from Python, reported beside
     other = None
-    if not args.graph and args.driver == "native":
+    if not args.graph and args.driver != "python":
         R3 = replay("python")
         dt3 = R3.run()
         ok3 = bool(np.array_equal(R3.home_copy(), R3.final_image()))
@@ -728,6 +729,9 @@ def run_mmult(args):
                      if args.graph else ("eager, two streams, rounds issued by the C++ loop over "
                                          "the C ABI (gallocy_amd/native/replay.cpp)"
                                          if args.driver == "native" else
+                                         "eager, two streams, rounds issued by two C++ threads, one "
+                                         "per context (gallocy_amd/native/replay.cpp)"
+                                         if args.driver == "native2" else
                                          "eager, two streams, rounds issued from Python"),
            "python_rounds": other,
            "round": ("coherence batch | the round's row writes (one batched copy), the release "

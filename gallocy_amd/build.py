@@ -112,7 +112,7 @@ def build_replay(verbose: bool = False) -> Path:
         return REPLAY
     cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-fPIC", "-shared",
            "-I", str(ROOT / "include"), str(src), "-L", str(LIBDIR), "-lgdsm",
-           "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined", "-o", str(REPLAY)]
+           "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined", "-pthread", "-o", str(REPLAY)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -57,9 +57,10 @@ def native_driver():
             raise RuntimeError(f"{path} is missing: build it (python -m gallocy_amd.build)")
         d = C.CDLL(str(path))
         vp, i64p = C.c_void_p, C.c_void_p
-        d.gdsm_replay_mmult.restype = C.c_int
-        d.gdsm_replay_mmult.argtypes = [vp, vp, C.c_uint32, C.c_uint32, vp, i64p, vp, vp, vp, i64p,
-                                        vp, i64p, vp, C.c_int]
+        for fn in (d.gdsm_replay_mmult, d.gdsm_replay_mmult_threads):
+            fn.restype = C.c_int
+            fn.argtypes = [vp, vp, C.c_uint32, C.c_uint32, vp, i64p, vp, vp, vp, i64p, vp, i64p,
+                           vp, C.c_int]
         _NATIVE = d
     return _NATIVE
 
@@ -67,7 +68,7 @@ def native_driver():
 class MmultReplay:
     def __init__(self, ndim: int = 1000, nodes: int = 4, seed: int = 0, device: int = 0,
                  fused: bool = True, retwin: bool = True, driver: str = "native"):
-        if driver not in ("native", "python"):
+        if driver not in ("native", "native2", "python"):
             raise ValueError(driver)
         self.driver = driver
         self.fused = fused
@@ -180,17 +181,17 @@ class MmultReplay:
             self.data.sync()
             dt = time.perf_counter() - t0
             g.destroy()
-        elif self.driver == "native" and self.fused:
-            drv = native_driver()
+        elif self.driver in ("native", "native2") and self.fused:
+            d = native_driver()
+            drv_fn = d.gdsm_replay_mmult_threads if self.driver == "native2" else d.gdsm_replay_mmult
             ev_off = np.ascontiguousarray(self.ev_off, np.int64)
             id_off = np.ascontiguousarray(self.id_off, np.int64)
             desc_off = np.ascontiguousarray(self.desc_off, np.int64)
             t0 = time.perf_counter()
-            rc = drv.gdsm_replay_mmult(self.data.handle, self.pt.handle, 0, self.T.rounds,
-                                       self.d_events.ptr, ev_off.ctypes.data, self.d_tot.ptr,
-                                       self.d_ids.ptr, self.d_home.ptr, id_off.ctypes.data,
-                                       self.d_desc.ptr, desc_off.ctypes.data,
-                                       C.byref(self._runs.s), int(self.retwin))
+            rc = drv_fn(self.data.handle, self.pt.handle, 0, self.T.rounds, self.d_events.ptr,
+                        ev_off.ctypes.data, self.d_tot.ptr, self.d_ids.ptr, self.d_home.ptr,
+                        id_off.ctypes.data, self.d_desc.ptr, desc_off.ctypes.data,
+                        C.byref(self._runs.s), int(self.retwin))
             gdsm.check(rc, "gdsm_replay_mmult")
             self.data.sync()
             self.pt.sync()
