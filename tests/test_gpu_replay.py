@@ -24,11 +24,14 @@ def test_mmult_replay_end_to_end(ndim, nodes, graph, fused):
     _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, fused=fused), nodes, graph)
 
 
-@pytest.mark.parametrize("ndim,nodes,retwin", [(1000, 4, True), (257, 3, False), (64, 8, True)])
-def test_mmult_replay_python_rounds(ndim, nodes, retwin):
-    """The same replay with every round issued from Python (MmultReplay.round, driver="python"),
-    with and without the re-twinning release: the same home copies, totals and page table."""
-    _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, retwin=retwin, driver="python"),
+@pytest.mark.parametrize("ndim,nodes,retwin,driver", [
+    (1000, 4, True, "python"), (257, 3, False, "python"), (64, 8, True, "python"),
+    (1000, 4, True, "native2"), (257, 3, False, "native2")])
+def test_mmult_replay_other_drivers(ndim, nodes, retwin, driver):
+    """The same replay with every round issued from Python (MmultReplay.round, driver="python") or
+    by two C++ threads, one per context (driver="native2"), with and without the re-twinning
+    release: the same home copies, totals and page table."""
+    _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, retwin=retwin, driver=driver),
                   nodes, False)
 
 
