@@ -64,10 +64,12 @@ def test_edge_pages_golden(golden):
         assert np.array_equal(c.download("replica"), g["edge_cur"])
 
 
+@pytest.mark.parametrize("n", [700, 300])
 @pytest.mark.parametrize("density", [0.001, 0.05, 0.3, 0.5, 0.9, 1.0])
-def test_random_byte_density(density):
-    rng = np.random.default_rng(int(density * 1000) + 1)
-    n = 700  # not a multiple of the 64-page block
+def test_random_byte_density(density, n):
+    """n = 700: not a multiple of the 64-page block (four pages per workgroup, chained); n = 300:
+    the page-per-workgroup release kernel."""
+    rng = np.random.default_rng(int(density * 1000) + n)
     twin = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
     cur = twin.copy()
     mask = rng.random((n, 4096)) < density
