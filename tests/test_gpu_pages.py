@@ -1091,3 +1091,52 @@ def test_chained_short_lists_across_launches_and_graphs():
         finally:
             L.gdsm_tune(b"diff_chain", 2)
             graph.destroy()
+
+
+def test_chained_releases_from_concurrent_host_threads():
+    """Three contexts, each driven by its own host thread (a context is driven by one thread at a
+    time; gallocy's runtime is threaded), each issuing thirty chained releases of 5-2048 pages
+    with home applies and re-twins back to back, CURRENT moving on between some of them: every
+    context's streams, home copies and twins equal the oracle's."""
+    import threading
+
+    n = 2600
+    twin0, cur0 = oracle.gen_pages(n, seed=41, mode=1, ppm=80000)
+    errors = []
+
+    def worker(k):
+        try:
+            rng = np.random.default_rng(900 + k)
+            twin, cur, rep = twin0.copy(), cur0.copy(), twin0.copy()
+            with ga.Context(n) as c:
+                c.upload("twin", twin)
+                c.upload("current", cur)
+                c.upload("replica", rep)
+                for it in range(30):
+                    m = int(rng.choice([5, 40, 300, 513, 2048]))
+                    ids = rng.choice(n, m, replace=False).astype(np.uint32)
+                    r = c.release(c.ids(ids), apply_to="replica")
+                    c.sync()
+                    ro, data = oracle.diff_pages(twin, cur, ids)
+                    h = r.to_host()
+                    assert np.array_equal(h.rec_off, ro), (k, it)
+                    assert np.array_equal(h.data[:int(ro[-1])], data), (k, it)
+                    twin[ids] = cur[ids]
+                    rep[ids] = cur[ids]
+                    r.free()
+                    if it % 10 == 9:
+                        assert np.array_equal(c.download("twin"), twin), (k, it)
+                        assert np.array_equal(c.download("replica"), rep), (k, it)
+                    if it % 7 == 6:  # new writes: CURRENT moves on for some pages
+                        cur[rng.choice(n, 64, replace=False)] ^= 0x11
+                        c.upload("current", cur)
+        except Exception as e:  # surfaced below
+            errors.append((k, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(3)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in threads)
+    assert not errors, errors
