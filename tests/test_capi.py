@@ -163,13 +163,14 @@ def test_tune_rejects_measurement_only_variants():
                     reason="the driver links the in-tree libgdsm.so, not a GDSM_LIB build")
 def test_native_replay_driver_exports_its_loop():
     """libgdsm_replay.so (gallocy_amd/native/replay.cpp, config 5's C++ round loop over the C ABI)
-    links the in-tree libgdsm.so and exports gdsm_replay_mmult, which refuses null contexts
-    before touching any."""
+    links the in-tree libgdsm.so and exports gdsm_replay_mmult and its two-thread form, which
+    refuse null contexts before touching any."""
     from gallocy_amd.replay import native_driver
     d = native_driver()
     z = np.zeros(2, np.int64)
-    assert d.gdsm_replay_mmult(None, None, 0, 1, None, z.ctypes.data, None, None, None,
-                               z.ctypes.data, None, z.ctypes.data, None, 1) == -22
+    for fn in (d.gdsm_replay_mmult, d.gdsm_replay_mmult_threads):
+        assert fn(None, None, 0, 1, None, z.ctypes.data, None, None, None, z.ctypes.data, None,
+                  z.ctypes.data, None, 1) == -22
 
 
 def test_release_argument_checks():
