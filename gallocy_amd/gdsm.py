@@ -305,7 +305,8 @@ class Context:
                 cap: int = 0, apply_to: Optional[str] = None, target_ids=None,
                 retwin: bool = True) -> Runs:
         """gdsm_release: the diff of the listed pages (applied to `apply_to` at target_ids as
-        diff() does) and, with retwin, TWIN := CURRENT for every page whose record fit."""
+        diff() does) and, with retwin, TWIN := CURRENT for every page whose record fit. Up to
+        2048 pages this is one kernel launch (outside graph capture: no zeroing launch)."""
         n = self._count(ids, n)
         out = out or Runs(self, n, cap)
         check(lib().gdsm_release(self.handle, self._ptr(ids), n, C.byref(out.s),
