@@ -74,7 +74,9 @@ def parse():
                          "on the GPU over configs[0]-shaped page pairs; twin: the twin step "
                          "(TWIN := CURRENT) of the north-star pages, beside the writer-side "
                          "re-twin of only the dirty bytes (the release's stream applied to TWIN)")
-    ap.add_argument("--nw-pairs", type=int, default=512, help="nw: 4 KiB page pairs per batch")
+    ap.add_argument("--nw-pairs", type=int, default=2048,
+                    help="nw: 4 KiB page pairs per batch (2048: 8 fill waves per SIMD, the "
+                         "fill's serial max3 chain needs them; 512 left it at 4)")
     ap.add_argument("--ndim", type=int, default=1000, help="mmult: matrix size (<= 1021)")
     ap.add_argument("--nodes", type=int, default=4, help="mmult: simulated DSM nodes (1-8)")
     ap.add_argument("--retwin", choices=["on", "off"], default="on",
@@ -91,10 +93,16 @@ def parse():
     ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
     ap.add_argument("--coh-nodes", type=int, default=8,
                     help="coherence: DSM nodes of the batch (BASELINE config 4: 8)")
+    ap.add_argument("--same-run-ref", choices=["on", "off"], default="on",
+                    help="pages workload, N > 1: after the N-rank run rank 0 times the N = 1 step "
+                         "of the same total workload on its own GPU (outside `value`) and reports "
+                         "efficiency_same_run")
     ap.add_argument("--deadline", type=float, default=300.0,
-                    help="N > 1: seconds each phase (setup + first release, the timed releases) "
-                         "may take before a rank exits non-zero (a peer died or hangs; "
-                         "exchange.Watchdog); 0 = off")
+                    help="N > 1: seconds each phase may take before a rank exits non-zero (a "
+                         "peer died or hangs; exchange.Watchdog). The pages workload re-arms it "
+                         "per phase (setup + first release, the timed releases, the link timing, "
+                         "verification, the same-run N = 1 reference, teardown); the other "
+                         "workloads arm it once for their whole run. 0 = off")
     return ap.parse_args()
 
 
@@ -265,6 +273,87 @@ def read_coh_traffic(dist: str, pages: int, events: int):
     return None, None
 
 
+def box_ceilings(ctx, n: int, read=None, copy=None, reps: int = 5) -> dict:
+    """This GPU's own streaming ceilings over the workload's arenas, measured in this process
+    before the timed region (gdsm_probe_ceiling, gallocy_amd/csrc/gdsm_probe.hip): `read` = two
+    device pointers of n pages each read once (the diff's input), `copy` = (src, dst) n pages
+    copied (dst is overwritten: the caller regenerates it). Best of `reps` launches (HIP events);
+    the medians beside. A line's frac_of_box = achieved / the matching ceiling: the kernel's
+    fraction of the box it ran on, where frac is against the 8 TB/s spec."""
+    import ctypes as C
+
+    import gallocy_amd as ga
+    L = ga.gdsm.lib()
+    out = {}
+    for key, kind, args in (("read", 0, read), ("copy", 1, copy)):
+        if args is None:
+            continue
+        a, b, dst = (args[0], args[1], None) if kind == 0 else (args[0], None, args[1])
+        best, med = C.c_float(), C.c_float()
+        rc = L.gdsm_probe_ceiling(ctx.handle, kind, a, b, dst, n, reps, C.byref(best),
+                                  C.byref(med))
+        if rc:
+            raise RuntimeError(f"gdsm_probe_ceiling({key}) {rc}")
+        moved = 2 * n * 4096  # read: both arenas; copy: read + write of one
+        out[f"box_{key}_gbs"] = round(moved / (best.value * 1e-3) / 1e9, 1)
+        out[f"box_{key}_gbs_median"] = round(moved / (med.value * 1e-3) / 1e9, 1)
+    out["box_probe"] = (f"gdsm_probe_ceiling over this run's own arenas ({n} pages), best of "
+                        f"{reps} launches: read = two page arenas read once with 16-B "
+                        f"nontemporal loads (the diff's input), copy = a flat 16-B copy; "
+                        f"frac_of_box = achieved / the ceiling matching the kernel")
+    return out
+
+
+def with_box(roof: dict, box: dict, which: str) -> dict:
+    """roofline + the box ceilings and the kernel's fraction of the `which` ceiling."""
+    if not box:
+        return roof
+    r = dict(roof, **box)
+    r["frac_of_box"] = round(roof["achieved"] / box[f"box_{which}_gbs"], 4)
+    r["frac_of_box_against"] = f"box_{which}_gbs"
+    return r
+
+
+def n1_reference(args, total: int, mode: int, ppm: int, device: int) -> dict:
+    """--gpus N > 1, after the N-rank run (its arenas freed): rank 0 times the N = 1 step of the
+    SAME total workload on its own GPU (all `total` pages in one shard, diff + apply, serial, as
+    bench.py --gpus 1 runs it), so parallel efficiency comes from one sweep and one box. Outside
+    `value`. Skipped when the three arenas do not fit the free HBM."""
+    import torch
+
+    import gallocy_amd as ga
+    cap_pp = 128 if mode == ga.GEN_UNIFORM else 1024
+    need = 3 * (total + 1) * 4096 + total * cap_pp + 16 * (total + 1) + (2 << 30)
+    free, _ = torch.cuda.mem_get_info(device)
+    if free < need:
+        return {"skipped": f"{need / 2**30:.1f} GiB needed for the N = 1 arenas, "
+                           f"{free / 2**30:.1f} GiB free"}
+    ctx = ga.Context(total, device=device)
+    try:
+        ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=0, stride=1,
+                      arenas=("twin", "current"))
+        ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=0, stride=1,
+                      arenas=("replica",))
+        runs = ga.Runs(ctx, total, cap=total * cap_pp)
+        for _ in range(args.warmup):
+            ctx.diff(out=runs)
+            ctx.apply(runs)
+        ctx.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.diff(out=runs)
+            ctx.apply(runs)
+        ctx.sync()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        runs.free()
+    finally:
+        ctx.close()
+    return {"ms_per_step": round(dt / args.steps * 1e3, 4), "pages": total,
+            "steps": args.steps, "warmup": args.warmup}
+
+
 def watchdog(args, rank: int, world: int, what: str):
     """N > 1: (re)arms the rank's deadline for the phase `what` (exchange.Watchdog: a rank
     blocked on a dead or hung peer exits non-zero instead of hanging the job)."""
@@ -337,6 +426,9 @@ def run_coherence(args):
         raise SystemExit("--coh-nodes must be 1-8")
     ev = ctx.gen_events(counts, seed=args.seed + rank, n_nodes=nn, write_pct=20)
     touched = int((counts > 0).sum())
+    # this box's read ceiling over the event buffer itself (its two halves as the probe's arenas)
+    half = (ev.count * 8) // 2 // 4096
+    box = box_ceilings(ctx, half, read=(ev.ptr, ev.ptr + half * 4096)) if half else {}
     ctx.coh_init(nn)
     tot_dev = ctx.buffer(80)
     L = ga.gdsm.lib()
@@ -385,11 +477,12 @@ def run_coherence(args):
                                   + (f", page table sharded over {world} GPUs (rank 0's shard: "
                                      f"{n} pages, {ev.count} events)" if world > 1 else ""),
                       "touched_pages": touched},
-           "roofline": {"bound": "hbm", "kernel": "gdsm::coh_fold_kernel", "achieved": round(achieved, 1),
-                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": traffic, "traffic_source": traffic_src,
-                        "algorithmic_bytes_per_launch": int(alg),
-                        "avg_launch_ms": round(main_ms, 4)},
+           "roofline": with_box({"bound": "hbm", "kernel": "gdsm::coh_fold_kernel",
+                                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                 "traffic": traffic, "traffic_source": traffic_src,
+                                 "algorithmic_bytes_per_launch": int(alg),
+                                 "avg_launch_ms": round(main_ms, 4)}, box, "read"),
            "stages": stages,
            "last_batch_totals": {"invalidations": int(totals[0]), "transfers": int(totals[1]),
                                  "node_faults": [int(x) for x in totals[2:]]},
@@ -430,6 +523,9 @@ def run_twin(args):
     mode = ga.GEN_UNIFORM if (args.mode or "uniform") == "uniform" else ga.GEN_CLUSTERED
     ppm = args.ppm if args.ppm is not None else (10000 if mode == ga.GEN_UNIFORM else 100000)
     ctx = ga.Context(n, device=local, arenas=("twin", "current"))
+    # this box's ceilings over the two arenas (the copy probe writes TWIN: generated after it)
+    box = box_ceilings(ctx, n, read=(ctx.arena_ptr("twin"), ctx.arena_ptr("current")),
+                       copy=(ctx.arena_ptr("current"), ctx.arena_ptr("twin")))
     ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n,
                   arenas=("twin", "current"))
     runs = ctx.diff(cap=n * (128 if mode == ga.GEN_UNIFORM else 1024))
@@ -474,11 +570,12 @@ def run_twin(args):
                "config": {"workload": f"{n} x 4 KiB pages per GPU, gdsm_twin of every page"
                                       + (f", {world} replicas" if world > 1 else ""),
                           "pages_per_gpu": n, "seed": args.seed},
-               "roofline": {"bound": "hbm", "kernel": "gdsm::twin_kernel",
-                            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                            "traffic_source": traffic_src,
-                            "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(twin_ms, 4)},
+               "roofline": with_box({"bound": "hbm", "kernel": "gdsm::twin_kernel",
+                                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                     "traffic": traffic, "traffic_source": traffic_src,
+                                     "algorithmic_bytes_per_launch": alg,
+                                     "avg_launch_ms": round(twin_ms, 4)}, box, "copy"),
                "twin_equals_current": bool(ok_full),
                "retwin_by_stream": {
                    "kernel": "gdsm::apply_flat_kernel (target TWIN)",
@@ -511,14 +608,18 @@ def run_twin(args):
     barrier(world)
 
 
-def mmult_cpu_baseline(ndim: int, nodes: int, seed: int, min_seconds: float = 2.0) -> dict:
+def mmult_cpu_baseline(ndim: int, nodes: int, seed: int, min_seconds: float = 2.0,
+                       retwin: bool = True) -> dict:
     """Config 5 on the host: the same trace replayed round by round on one thread through the C
-    oracle (or_coherence of the round's events, the twin of the written pages, the row writes,
-    or_diff_pages of those pages, or_apply of the stream to the home copies), P node views side
-    by side as on the GPU. The round loop runs in C (oracle/gdsm_oracle_bench.c:or_bench_mmult,
-    CLOCK_MONOTONIC around the loop) over a plan precomputed here; the same loop driven from
-    Python (numpy + ctypes per round) is reported beside it, labelled. The home copies are
-    checked against the product afterwards, for both."""
+    oracle (or_coherence of the round's events, the row writes, or_diff_pages of the written
+    pages, or_apply of the stream to the home copies), P node views side by side as on the GPU.
+    The per-round twin work matches the GPU line's: with `retwin` (gdsm_release, the default)
+    the round's stream is applied to the twin views after the diff (only the dirty bytes move,
+    as in the release), else the written pages are twinned before the writes (round 4's
+    workflow). The other workflow is timed beside it. The round loop runs in C
+    (oracle/gdsm_oracle_bench.c:or_bench_mmult, CLOCK_MONOTONIC around the loop) over a plan
+    precomputed here; the same loop driven from Python (numpy + ctypes per round) is reported
+    beside it, labelled. The home copies are checked against the product afterwards."""
     from gallocy_amd.trace import PAGE_SZ, MmultTrace, c_row_values, mmult_layout, zone_image
     from oracle import oracle
     L = mmult_layout(ndim)
@@ -561,13 +662,19 @@ def mmult_cpu_baseline(ndim: int, nodes: int, seed: int, min_seconds: float = 2.
         "row_off": np.concatenate([[0], np.cumsum([len(p[1]) for p in plan])]).astype(np.uint64),
     }
     # the trace is short (tens of ms): replayed from a fresh state until min_seconds of C time
-    dt_c, reps, ok_c = 0.0, 0, True
-    while (dt_c < min_seconds and reps < 500) or reps == 0:
-        cur, twin, rep, st, fl = fresh()
-        dt, _ = oracle.bench_mmult(st, fl, nodes, twin, cur, rep, flat_plan, rowvals)
-        dt_c += dt
-        reps += 1
-        ok_c = ok_c and bool(np.array_equal(rep.reshape(-1), z))
+    def c_loop(rt: bool, seconds: float):
+        dt_c, reps, ok_c = 0.0, 0, True
+        while (dt_c < seconds and reps < 500) or reps == 0:
+            cur, twin, rep, st, fl = fresh()
+            dt, _ = oracle.bench_mmult(st, fl, nodes, twin, cur, rep, flat_plan, rowvals,
+                                       retwin=rt)
+            dt_c += dt
+            reps += 1
+            ok_c = ok_c and bool(np.array_equal(rep.reshape(-1), z))
+        return dt_c, reps, ok_c
+
+    dt_c, reps, ok_c = c_loop(retwin, min_seconds)
+    dt_o, reps_o, ok_o = c_loop(not retwin, min_seconds / 2)
     # 2. the same loop driven from Python, per round
     cur, twin, rep, st, fl = fresh()
     flat = cur.reshape(-1)
@@ -585,15 +692,23 @@ def mmult_cpu_baseline(ndim: int, nodes: int, seed: int, min_seconds: float = 2.
     return {"value": round(reps * T.rounds / dt_c, 1), "unit": "rounds/s", "cores": 1,
             "kind": "port",
             "sample": f"the whole NDIM={ndim} trace ({T.rounds} rounds, {nodes} nodes) replayed "
-                      f"{reps} times from a fresh state through the C oracle (coherence, twin, row "
-                      f"writes, diff, apply), the round loop in C over a precomputed plan "
-                      f"(or_bench_mmult), {dt_c:.3f} s timed in C",
+                      f"{reps} times from a fresh state through the C oracle (coherence, "
+                      + ("row writes, diff, apply, re-twin of the dirty bytes (the stream "
+                         "applied to the twin views, as gdsm_release)" if retwin else
+                         "twin, row writes, diff, apply")
+                      + f"), the round loop in C over a precomputed plan (or_bench_mmult), "
+                        f"{dt_c:.3f} s timed in C",
+            "twin_workflow": "re-twin after the diff" if retwin else "twin before the writes",
+            "other_twin_workflow": {
+                "twin_workflow": "twin before the writes" if retwin else "re-twin after the diff",
+                "value": round(reps_o * T.rounds / dt_o, 1), "unit": "rounds/s",
+                "home_copy_equals_product": ok_o},
             "timed_in": "C (CLOCK_MONOTONIC)",
             "python_driven": {"value": round(T.rounds / dt_py, 1), "unit": "rounds/s",
                               "note": "the same loop with Python numpy/ctypes per round "
                                       "(round 4's figure)", "seconds": round(dt_py, 4),
                               "home_copy_equals_product": ok_py},
-            "home_copy_equals_product": ok_c and ok_py, **host_info()}
+            "home_copy_equals_product": ok_c and ok_py and ok_o, **host_info()}
 
 
 def run_mmult_ranks(args, rank: int, world: int):
@@ -746,7 +861,8 @@ def run_mmult(args):
                       "node_faults": [int(x) for x in R.totals[2:]]},
            "roofline": None, "latency": latency,
            "cpu_baseline": None if args.no_cpu else mmult_cpu_baseline(args.ndim, args.nodes,
-                                                                       args.seed)}
+                                                                       args.seed,
+                                                                       retwin=args.retwin == "on")}
     print(json.dumps(res), flush=True)
     R.close()
 
@@ -942,6 +1058,13 @@ def main():
         # Two diff streams: release k+1 may be diffed while release k is applied
         runs = [ga.Runs(ctx, n, cap=n * cap_pp) for _ in range(2)]
 
+    # this box's read and copy ceilings over the shard's own arenas (REPLICA is the copy's
+    # destination, then generated again)
+    box = box_ceilings(ctx, n, read=(ctx.arena_ptr("twin"), ctx.arena_ptr("current")),
+                       copy=(ctx.arena_ptr("current"), ctx.arena_ptr("replica")))
+    ctx.gen_pages(seed=args.seed, mode=mode, ppm=ppm, first_global=rank * n, stride=1,
+                  arenas=("replica",))
+
     def steps(k: int, pipelined: bool):
         if shard is not None:
             shard.run(k, pipelined)
@@ -1017,6 +1140,7 @@ def main():
     watchdog(args, rank, world, "timed releases")
     dt_other = timed(not pipelined, False)[0] if args.compare_overlap else None
     dt, prof = timed(pipelined, True)
+    watchdog(args, rank, world, "link timing")
     # The xGMI link alone: the same releases again (untimed for `value`) with GDSM_XCHG_TIMED, a
     # device-side barrier before each transfer, so the exchange stage starts once every rank's
     # streams are ready and times the RCCL group, not the wait for the peers' diffs.
@@ -1028,11 +1152,13 @@ def main():
         finally:
             shard.flags &= ~exchange.XCHG_TIMED
         link = [plink["exchange"][0] / args.steps, plink["exchange_wait"][0] / args.steps]
+        watchdog(args, rank, world, "link timing: the stats all-reduce")
         t = torch.tensor(link, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         link = t.tolist()
 
     # correctness of the measured work: REPLICA == CURRENT afterwards (diff of the two is empty)
+    watchdog(args, rank, world, "verification and the stats all-reduces")
     if shard is None:
         chk = ga.Runs(ctx, n, cap=1 << 20)
         ws = ctx.buffer(ga.gdsm.lib().gdsm_diff_workspace_bytes(n))
@@ -1089,6 +1215,31 @@ def main():
                         "GB/s (all of an MI355X's xGMI); peak_links_used: the N-1 links one "
                         "rank's peers use"}
     ref_ms, ref_src = efficiency_ref(world * n, mode_name, ppm) if world > 1 else (None, None)
+    exch = None if shard is None else {
+        "transport": shard.transport, "fixed_budgets": bool(shard.flags),
+        "comm_ranks": shard.comm.size()[0] if shard.comm is not None else None,
+        "recoveries": shard.recoveries,
+        "sent_remote_bytes_per_step": shard.sent_remote,
+        "received_bytes_per_step": shard.received}
+    same = None
+    if world > 1 and args.same_run_ref == "on":
+        # the N-rank run's arenas and communicator go first, then rank 0 alone runs the N = 1
+        # step of the same total workload (the other ranks wait at the barrier)
+        watchdog(args, rank, world, "teardown of the N-rank run")
+        shard.close()
+        shard = None
+        ctx.close()
+        ctx = None
+        barrier()
+        watchdog(args, rank, world, "the same-run N = 1 reference")
+        if rank == 0:
+            same = n1_reference(args, world * n, mode, ppm, local)
+            if "ms_per_step" in same:
+                same["efficiency"] = round(same["ms_per_step"] / (world * ms_step), 4)
+            same["note"] = ("rank 0 alone, after the N-rank run and its teardown: the N = 1 step "
+                            "(diff + apply of all pages on one GPU) of the same total workload; "
+                            "efficiency = ms_per_step(N = 1) / (N x ms_per_step(N))")
+        barrier()
 
     if rank == 0:
         stages = {k: {"ms_per_launch": round(v[0] / v[1], 4), "launches": v[1]}
@@ -1125,22 +1276,21 @@ def main():
             "fused_apply": fused,
             ("serial_ms_per_step" if pipelined else "pipelined_ms_per_step"):
                 None if dt_other is None else round(dt_other / args.steps * 1e3, 4),
-            "roofline": {"bound": "hbm", "kernel": DIFF_KERNEL,
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": int(diff_bytes),
-                         "avg_launch_ms": round(avg_diff_ms, 4)},
+            "roofline": with_box({"bound": "hbm", "kernel": DIFF_KERNEL,
+                                  "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                  "traffic": traffic, "traffic_source": traffic_src,
+                                  "algorithmic_bytes_per_launch": int(diff_bytes),
+                                  "avg_launch_ms": round(avg_diff_ms, 4)}, box, "read"),
+            "step_frac_of_box_read": round(step_bytes * args.steps / dt / 1e9
+                                           / box["box_read_gbs"], 4),
             "stages": stages,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
-            "exchange": None if shard is None else {
-                "transport": shard.transport, "fixed_budgets": bool(shard.flags),
-                "comm_ranks": shard.comm.size()[0] if shard.comm is not None else None,
-                "recoveries": shard.recoveries,
-                "sent_remote_bytes_per_step": shard.sent_remote,
-                "received_bytes_per_step": shard.received},
+            "exchange": exch,
             **({"roofline_xgmi": xgmi} if xgmi else {}),
-            **({"efficiency_ref_ms": ref_ms, "efficiency_ref_source": ref_src}
+            **({"efficiency_ref_ms": ref_ms, "efficiency_ref_source": ref_src,
+                "efficiency_same_run": None if same is None else same.get("efficiency"),
+                "same_run_reference": same}
                if world > 1 else {}),
             "replica_equals_current": bool(replica_ok),
             "cpu_baseline": None,
@@ -1148,12 +1298,16 @@ def main():
         if not args.no_cpu and world == 1:  # the host baseline is a 1-GPU figure (rank 0, N = 1)
             res["cpu_baseline"] = cpu_baseline(mode, ppm, args.seed, args.cpu_seconds)
         print(json.dumps(res), flush=True)
+    watchdog(args, rank, world, "teardown")
     if shard is not None:
         shard.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
+    if WATCHDOG is not None:
+        WATCHDOG.disarm()
 
 
 if __name__ == "__main__":

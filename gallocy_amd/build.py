@@ -17,7 +17,7 @@ CSRC = PKG / "csrc"
 LIBDIR = PKG / "lib"
 LIB = LIBDIR / "libgdsm.so"
 SOURCES = ["gdsm_pages.hip", "gdsm_coherence.hip", "gdsm_capi.cpp", "legacy_diff.cpp",
-           "gdsm_track.cpp", "gdsm_nw.hip", "gdsm_wire.hip", "gdsm_exchange.cpp", "gdsm_route.hip"]
+           "gdsm_track.cpp", "gdsm_nw.hip", "gdsm_wire.hip", "gdsm_exchange.cpp", "gdsm_route.hip", "gdsm_probe.hip"]
 HEADERS = ["gdsm_common.h", "gdsm_launch.h", "gdsm_prof.h", "gdsm_track.h", "gdsm_ctx.h"]
 ARCH = os.environ.get("GDSM_ARCH", "gfx950")
 
@@ -45,7 +45,7 @@ def build_lib(force: bool = False, verbose: bool = False) -> Path:
     for s in SOURCES:
         obj = LIBDIR / (Path(s).stem + ".o")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
-               "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s), "-o", str(obj)]
+               "-Werror=inline-asm", "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s), "-o", str(obj)]
         if s.endswith(".cpp"):
             cmd[1:1] = ["-x", "hip"]
         if verbose:

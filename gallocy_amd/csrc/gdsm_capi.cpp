@@ -49,11 +49,21 @@ int ensure_aux(gdsm_ctx* ctx) {
   return 0;
 }
 
+// The context's stream is being recorded into a graph: by gdsm_capture_begin / _join, or by a
+// caller that captures gdsm_stream() itself (hipStreamBeginCapture). A recorded launch replays
+// with the arguments it was recorded with, so the chained forms (one epoch per launch, DiffChain /
+// CohChainState) are not used then: the zeroing forms replay correctly.
+bool recording(const gdsm_ctx* ctx) {
+  if (ctx->capturing) return true;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(ctx->stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone;
+}
+
 // A context whose calls are being recorded (gdsm_capture_begin / _join) may not move its
 // workspaces, since the recorded kernels keep their addresses; other contexts are unaffected.
 int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need) {
   if (*have >= need) return 0;
-  if (ctx && ctx->capturing) return -EBUSY;  // size workspaces with gdsm_reserve before capturing
+  if (ctx && recording(ctx)) return -EBUSY;  // size workspaces with gdsm_reserve before capturing
   if (ctx && ctx->fail_alloc > 0 && --ctx->fail_alloc == 0) return -ENOMEM;  // test hook
   // kernels queued on the context's streams (main or aux, e.g. an exchange's applies reading the
   // checked id lists) may still use the old buffer: drain them before it goes (stated here rather
@@ -209,6 +219,15 @@ int gdsm_init(gdsm_ctx** out, int device, uint64_t n_pages, uint32_t flags) {
     // still holding an earlier context's error bits)
     if (hipMemsetAsync(ctx->err, 0, 256, ctx->stream) != hipSuccess) {
       rc = -EIO;
+      break;
+    }
+    // the chained forms' workspaces (short releases, small coherence batches; zeroed by their
+    // first launch): allocated here, so that no later call allocates outside ensure()
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->chain.ws), gdsm::diff_chain_bytes()) !=
+            hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&ctx->coh_chain.ws), gdsm::coh_chain_bytes()) !=
+            hipSuccess) {
+      rc = -ENOMEM;
       break;
     }
     for (int a = 0; a < 3 && !rc; ++a) {
@@ -617,13 +636,9 @@ static int diff_impl(gdsm_ctx* ctx, const uint32_t* ids, uint64_t n, gdsm_runs* 
   if (rc) return rc;
   if (!n) guard.ids = guard.tids = nullptr;
   // a short list outside graph capture: the chained one-launch form (its granules and counters
-  // allocated once; without them the list takes the zeroing launch instead)
+  // allocated by gdsm_init)
   gdsm::DiffChain* chain = nullptr;
-  if (!ctx->capturing && n && n <= gdsm::kDiffChainUnits) {
-    if (!ctx->chain.ws && hipMalloc(&ctx->chain.ws, gdsm::diff_chain_bytes()) != hipSuccess)
-      ctx->chain.ws = nullptr;
-    if (ctx->chain.ws) chain = &ctx->chain;
-  }
+  if (n && n <= gdsm::kDiffChainUnits && ctx->chain.ws && !recording(ctx)) chain = &ctx->chain;
   out->n = n;
   GDSM_TRY(gdsm::launch_diff(ctx->arena[GDSM_TWIN], ctx->arena[GDSM_CURRENT], ids, n,
                              out->rec_off, out->data, out->cap, ctx->diff_ws, ctx->diff_ws_bytes,
@@ -814,13 +829,9 @@ int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n
   if (g.rc) return g.rc;
   int rc = ensure(ctx, &ctx->coh_ws, &ctx->coh_ws_bytes, gdsm::coh_workspace_bytes(n_events));
   if (rc) return rc;
-  gdsm::CohChainState* chain = nullptr;  // (outside graph capture, see launch_coherence)
-  if (!ctx->capturing) {
-    if (!ctx->coh_chain.ws &&
-        hipMalloc(&ctx->coh_chain.ws, gdsm::coh_chain_bytes()) != hipSuccess)
-      ctx->coh_chain.ws = nullptr;
-    if (ctx->coh_chain.ws) chain = &ctx->coh_chain;
-  }
+  // (outside graph capture, see launch_coherence; allocated by gdsm_init)
+  gdsm::CohChainState* chain = nullptr;
+  if (ctx->coh_chain.ws && !recording(ctx)) chain = &ctx->coh_chain;
   GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, ctx->n_nodes, events, n_events,
                                   totals_dev, ctx->coh_ws, ctx->coh_ws_bytes, ctx->err,
                                   ctx->stream, ctx->P(), chain));

@@ -23,12 +23,12 @@ struct gdsm_ctx {
   uint32_t err_held = 0;
   uint8_t* diff_ws = nullptr;    // diff workspace
   uint64_t diff_ws_bytes = 0;
-  gdsm::DiffChain chain;         // short releases without a zeroing launch (allocated on first use)
+  gdsm::DiffChain chain;         // short releases without a zeroing launch (allocated by gdsm_init)
   uint8_t* coh_ws = nullptr;
   uint64_t coh_ws_bytes = 0;
   uint64_t* coh_pt = nullptr;      // page table: state | faults << 32 per page
   uint64_t* coh_totals = nullptr;  // device 10 x u64
-  gdsm::CohChainState coh_chain;   // small batches without a zeroing launch (allocated on first use)
+  gdsm::CohChainState coh_chain;   // small batches without a zeroing launch (allocated by gdsm_init)
   uint32_t n_nodes = 0;
   uint32_t diff_bpp = 0;         // stream bytes per page the host last learned (diff geometry)
   std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks
@@ -83,6 +83,8 @@ constexpr uint32_t kErrStream = 16;      // exchanged stream with malformed offs
 constexpr uint32_t kErrOverBudget = 32;  // fixed-budget exchanged stream over its budget
 
 int map_err(hipError_t e);
+// ctx->stream is being recorded into a graph (gdsm_capture_* or a caller's own capture of it).
+bool recording(const gdsm_ctx* ctx);
 // hipMalloc-backed buffer that only grows (contents are not kept); -EBUSY while ctx (the owner of
 // the buffer, or NULL) is recording a graph.
 int ensure(const gdsm_ctx* ctx, uint8_t** buf, uint64_t* have, uint64_t need);

@@ -37,6 +37,10 @@
 #include "gdsm_common.h"
 #include "gdsm_launch.h"
 
+// v_writelane_b32 as the compiler's own intrinsic (this clang has no __builtin for it): the
+// compiler then picks M0 for the lane select and knows it is written.
+extern "C" __device__ int nw_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 namespace gdsm {
 namespace {
 
@@ -374,11 +378,9 @@ __global__ __launch_bounds__(64 * kTW) void nw_trace_kernel(
   auto put = [&](uint32_t v, uint32_t dr) {
     uint32_t j = nrow & 63;
     asm volatile("" : "+s"(v), "+s"(j));  // both in SGPRs (a literal is no writelane operand)
-    // One scalar operand per VALU on gfx950: the lane select goes through M0.
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0"
-                 : "+v"(rbuf)
-                 : "s"(j), "s"(v)
-                 : "m0");
+    // One scalar operand per VALU on gfx950: the compiler routes the lane select through M0
+    // itself (it owns M0, so nothing it keeps there is clobbered behind its back).
+    rbuf = (uint32_t)nw_writelane((int)v, (int)j, (int)rbuf);
     nrow += dr;
     if ((j + dr) & 64) rr[ystart - (nrow - 64) - lane] = rbuf;  // slot 63 filled: 64 rows out
   };

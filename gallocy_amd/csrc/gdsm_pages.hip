@@ -114,12 +114,13 @@ __global__ __launch_bounds__(256) void retwin_kernel(uint8_t* __restrict__ twin,
                                                      const uint8_t* __restrict__ cur,
                                                      const uint32_t* __restrict__ ids, uint64_t n,
                                                      const uint64_t* __restrict__ rec_off,
-                                                     uint64_t cap) {
+                                                     uint64_t cap, uint64_t n_pages) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n;
        i += (uint64_t)gridDim.x * 4) {
     if (rec_off[i + 1] > cap) continue;  // wave-uniform
     const uint64_t pg = ids ? ids[i] : i;
+    if (n_pages && pg >= n_pages) continue;  // the guard page (a bad entry): left alone
     const u32x4* src = reinterpret_cast<const u32x4*>(cur + pg * kPage);
     u32x4 v[4];
 #pragma unroll
@@ -500,6 +501,14 @@ constexpr uint32_t kSpillWGs = 1280;  // > the workgroups of this kernel one MI3
 // (g, as diff_prep_kernel does), so the release is this one launch (config 5's rounds).
 constexpr uint32_t kSoloUnits = 16;
 
+// A re-twin store may go to page pj: not the guard page, where every out-of-range entry of a
+// checked list points (those workgroups would write the guard page's TWIN while others read it,
+// and the records emitted for the bad entries would depend on the race). g.n_pages == 0: the
+// launch has no checked list, so no entry names the guard page.
+__device__ __forceinline__ bool twin_ok(const IdGuard& g, uint64_t pj) {
+  return g.n_pages == 0 || pj < g.n_pages;
+}
+
 __device__ __forceinline__ uint64_t guarded_id(const uint32_t* __restrict__ ids, uint64_t i,
                                                uint64_t n_pages, uint32_t& bad) {
   const uint32_t p = ids[i];
@@ -621,7 +630,8 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
       if (kApply && !(kSkip & 1) && m[k]) store_masked16(target + pt_ * kPage + (k * 64 + lane) * 16u, m[k], c[k]);
       // (whole chunks: a chunk's clean bytes are equal in TWIN and CURRENT, and TWIN is this
       // writer's own, so no byte stores)
-      if (!(kSkip & 4) && retwin_now && m[k]) *reinterpret_cast<uint4*>(twin_w + pj * kPage + (k * 64 + lane) * 16u) = c[k];
+      if (!(kSkip & 4) && retwin_now && m[k] && twin_ok(g, pj))
+        *reinterpret_cast<uint4*>(twin_w + pj * kPage + (k * 64 + lane) * 16u) = c[k];
     }
     if (j + 1 < cnt) {
       pj = ids ? ids[i0 + j + 1] : i0 + j + 1;
@@ -797,7 +807,7 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
       emit_bytes(P, c, lane, data + excl + tab[j]);
     }
   }
-  if (kGuard && kRetwin && !(kSkip & 4) && !retwin_now && excl + tab[1] <= cap) {
+  if (kGuard && kRetwin && !(kSkip & 4) && !retwin_now && excl + tab[1] <= cap && twin_ok(g, pj)) {
     // gdsm_release's re-twin (TWIN := CURRENT, the dirty bytes only), once the record is out: the
     // registers still hold the unit's one page (kKeep: a late page was emitted from them)
 #pragma unroll
@@ -865,7 +875,7 @@ __global__ __launch_bounds__(256) void release_page_kernel(
   const uint64_t pt = kApply ? (tids ? (g.tids ? guarded_id(tids, i, g.n_pages, bad) : tids[i]) : pj)
                              : 0;  // page at target
   if (kApply && m) store_masked16(target + pt * kPage + ch * 16u, m, c);
-  if (ample && m) *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
+  if (ample && m && twin_ok(g, pj)) *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
   if (lane == 0) edge_first[w] = m;
   if (lane == 63) edge_last[w] = m;
   __syncthreads();
@@ -946,7 +956,8 @@ __global__ __launch_bounds__(256) void release_page_kernel(
     emit_chunk(ch, st, en, m, max(cmax, from_prev_lane(mx)), carry + inc - v, c,
                reinterpret_cast<uint32_t*>(rec + 4), rec + 4 + 4 * NR);
   }
-  if (kRetwin && !ample && m) *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
+  if (kRetwin && !ample && m && twin_ok(g, pj))
+    *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
 }
 
 // ------------------------------------------------------------------------- apply (SPEC §4)
@@ -1975,13 +1986,15 @@ static hipError_t launch_diff_impl(const uint8_t* twin, const uint8_t* cur, cons
   if (retwin_in)
     kern = target ? diff_single_kernel<1, 8192, 4, true, 0, false, true>
                   : diff_single_kernel<1, 8192, 4, false, 0, false, true>;
+  // (the lists are checked already: the kernel only learns n_pages, for twin_ok)
+  const IdGuard gn{nullptr, nullptr, nullptr, nullptr, g.n_pages, nullptr};
   hipLaunchKernelGGL(kern, dim3((unsigned)((nunits + 3) / 4)), dim3(256), 0, s, twin, cur, ids, sp,
-                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, IdGuard{});
+                     reinterpret_cast<uint64_t*>(ws), target, gen, pool, tids, gn);
   if (retwin && !retwin_in) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(retwin_kernel, dim3(grid_for(n, 4, 16384)), dim3(256), 0, s, retwin, cur,
-                       ids, n, sp.rec_off[0], sp.cap[0]);
+                       ids, n, sp.rec_off[0], sp.cap[0], g.n_pages);
   }
   return hipGetLastError();
 }

@@ -127,7 +127,11 @@ int gdsm_memcpy_batch(gdsm_ctx* ctx, const uint64_t* desc, uint64_t n);
  *   fail too.
  * - gdsm_graph_launch enqueues the whole graph on ctx's stream; gdsm_sync reports its
  *   device-side failures as usual. Every recorded pointer must stay valid while the graph
- *   lives. */
+ *   lives.
+ * - A caller may also capture gdsm_stream(ctx) itself (hipStreamBeginCapture): every call checks
+ *   hipStreamIsCapturing and then records the forms that replay correctly (a zeroing launch
+ *   before each short diff / small coherence batch instead of the one-launch chained forms,
+ *   whose per-launch epoch a replay would repeat). The same sizing rule applies. */
 typedef struct gdsm_graph gdsm_graph;
 int gdsm_capture_begin(gdsm_ctx* ctx);
 int gdsm_capture_join(gdsm_ctx* ctx, gdsm_ctx* other);
@@ -140,6 +144,15 @@ int gdsm_graph_destroy(gdsm_graph* g);
  * counts per stage (arrays of GDSM_PROF_STAGES), then clears them. */
 int gdsm_prof_enable(gdsm_ctx* ctx, int on);
 int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches);
+
+/* Box ceilings (measurement support for bench.py, gdsm_probe.hip; no reference counterpart): how
+ * fast this GPU streams given page arenas, `reps` launches timed by HIP events on ctx's stream
+ * (best and median ms per launch). GDSM_PROBE_READ: arenas a and b (n_pages each) read once, the
+ * diff's input pattern; GDSM_PROBE_COPY: dst := a over n_pages pages (dst is overwritten). */
+#define GDSM_PROBE_READ 0
+#define GDSM_PROBE_COPY 1
+int gdsm_probe_ceiling(gdsm_ctx* ctx, int kind, const void* a, const void* b, void* dst,
+                       uint64_t n_pages, int reps, float* best_ms, float* median_ms);
 
 /* ---- synthetic inputs (SPEC §6) ------------------------------------------------------- */
 /* Fills the arenas named in `arenas` (bit 1<<GDSM_TWIN | 1<<GDSM_CURRENT | 1<<GDSM_REPLICA,

@@ -84,7 +84,7 @@ int or_bench_mmult(uint32_t* state, uint32_t* faults, uint64_t zone_pages, uint3
                    const uint64_t* events, const uint64_t* ev_off, const uint32_t* ids,
                    const uint32_t* home, const uint64_t* ids_off, const uint64_t* row_dst,
                    const uint32_t* row_src, const uint64_t* row_off, const uint8_t* rowvals,
-                   uint64_t row_bytes, uint64_t* totals, double* elapsed);
+                   uint64_t row_bytes, uint64_t* totals, double* elapsed, int retwin);
 
 #ifdef __cplusplus
 }

@@ -171,7 +171,7 @@ int or_bench_mmult(uint32_t* state, uint32_t* faults, uint64_t zone_pages, uint3
                    const uint64_t* events, const uint64_t* ev_off, const uint32_t* ids,
                    const uint32_t* home, const uint64_t* ids_off, const uint64_t* row_dst,
                    const uint32_t* row_src, const uint64_t* row_off, const uint8_t* rowvals,
-                   uint64_t row_bytes, uint64_t* totals, double* elapsed) {
+                   uint64_t row_bytes, uint64_t* totals, double* elapsed, int retwin) {
   uint64_t max_ids = 0;
   for (uint64_t r = 0; r < rounds; ++r)
     if (ids_off[r + 1] - ids_off[r] > max_ids) max_ids = ids_off[r + 1] - ids_off[r];
@@ -197,11 +197,14 @@ int or_bench_mmult(uint32_t* state, uint32_t* faults, uint64_t zone_pages, uint3
     for (int k = 0; k < 10; ++k) totals[k] += tot[k];
     const uint64_t n = ids_off[r + 1] - ids_off[r];
     const uint32_t* id = ids + ids_off[r];
-    or_twin(twin, cur, id, n);
+    if (!retwin) or_twin(twin, cur, id, n);
     for (uint64_t k = row_off[r]; k < row_off[r + 1]; ++k)
       memcpy(cur + row_dst[k], rowvals + (uint64_t)row_src[k] * row_bytes, row_bytes);
     or_diff_pages(twin, cur, id, n, rec_off, data, cap);
     if (!rc) rc = or_apply(rep, home + ids_off[r], n, rec_off, data);
+    /* gdsm_release's re-twin: TWIN := CURRENT for the released pages, the dirty bytes only
+       (the stream applied to the twin views) */
+    if (!rc && retwin) rc = or_apply(twin, id, n, rec_off, data);
   }
   clock_gettime(CLOCK_MONOTONIC, &b);
   *elapsed = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);

@@ -40,7 +40,8 @@ def lib():
         L.or_bench_coherence.argtypes = [C.c_void_p, C.c_void_p, u64, C.c_uint32, C.c_double,
                                          C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]
         L.or_bench_mmult.argtypes = [vp, vp, u64, C.c_uint32, vp, vp, vp, u64, vp, vp, vp, vp,
-                                     vp, vp, vp, vp, vp, u64, vp, C.POINTER(C.c_double)]
+                                     vp, vp, vp, vp, vp, u64, vp, C.POINTER(C.c_double),
+                                     C.c_int]
         L.or_check_stream.restype = C.c_int64
         L.or_check_stream.argtypes = [vp, vp, u64, u64, u64, C.c_int, C.c_uint32, C.c_int]
         _lib = L
@@ -164,10 +165,12 @@ def bench_diff_apply(n, mode, ppm, seed, seconds, threads):
     return pages.value, dt.value, bool(ok.value)
 
 
-def bench_mmult(state, faults, nodes, twin, cur, rep, plan, rowvals):
+def bench_mmult(state, faults, nodes, twin, cur, rep, plan, rowvals, retwin=False):
     """bench.py's config-5 CPU baseline: the whole round loop in C on one thread
     (or_bench_mmult). plan = dict of flat arrays events / ev_off / ids / home / ids_off / row_dst
-    / row_src / row_off. Returns (seconds, totals[10])."""
+    / row_src / row_off. retwin: no twin step before a round's writes; the round's stream is
+    applied to the twin views after the diff instead (gdsm_release's re-twin, the dirty bytes
+    only); twin must equal cur at the start. Returns (seconds, totals[10])."""
     a = {k: np.ascontiguousarray(v) for k, v in plan.items()}
     rv = np.ascontiguousarray(rowvals, np.uint8)
     tot = np.zeros(10, np.uint64)
@@ -177,7 +180,7 @@ def bench_mmult(state, faults, nodes, twin, cur, rep, plan, rowvals):
                               _p(rep), rounds, _p(a["events"]), _p(a["ev_off"]), _p(a["ids"]),
                               _p(a["home"]), _p(a["ids_off"]), _p(a["row_dst"]),
                               _p(a["row_src"]), _p(a["row_off"]), _p(rv), rv.shape[1], _p(tot),
-                              C.byref(dt))
+                              C.byref(dt), 1 if retwin else 0)
     if rc:
         raise RuntimeError(f"or_bench_mmult: {rc}")
     return dt.value, tot

@@ -126,3 +126,9 @@ def test_mmult_cpu_baseline_c_loop_and_python_loop_agree(nodes):
     assert out["home_copy_equals_product"] is True
     assert out["python_driven"]["home_copy_equals_product"] is True
     assert out["timed_in"].startswith("C") and out["value"] > 0 and out["cores"] == 1
+    # the per-round twin work matches the GPU line's (gdsm_release re-twins after the diff), and
+    # the other workflow is timed beside it, also ending at the product
+    assert out["twin_workflow"] == "re-twin after the diff"
+    assert out["other_twin_workflow"]["twin_workflow"] == "twin before the writes"
+    assert out["other_twin_workflow"]["home_copy_equals_product"] is True
+    assert out["other_twin_workflow"]["value"] > 0

@@ -111,6 +111,13 @@ def test_bench_multi_rank_rehearsal_gloo(ranks, overlap):
     assert d["exchange"]["received_bytes_per_step"] > 0
     assert d["pipelined"] is (overlap == "on")
     assert d["scaling"] == "strong" and d["config"]["total_pages"] == ranks * ranks * 8192
+    # the same sweep's N = 1 reference (rank 0 alone, after the N-rank run) and the efficiency
+    # from it; the box ceilings beside the spec fraction
+    same = d["same_run_reference"]
+    assert same["pages"] == ranks * ranks * 8192 and same["ms_per_step"] > 0
+    assert d["efficiency_same_run"] > 0
+    roof = d["roofline"]
+    assert roof["box_read_gbs"] > 0 and roof["box_copy_gbs"] > 0 and roof["frac_of_box"] > 0
 
 
 def _bench_no_launcher(args, backend="gloo"):

@@ -106,3 +106,86 @@ def test_capture_end_on_joined_context_is_refused():
         # both contexts work eagerly again
         a.sync()
         b.sync()
+
+
+def _hip():
+    import ctypes as C
+    h = C.CDLL("libamdhip64.so")
+    vp = C.c_void_p
+    h.hipStreamBeginCapture.argtypes = [vp, C.c_int]
+    h.hipStreamEndCapture.argtypes = [vp, C.POINTER(vp)]
+    h.hipGraphInstantiate.argtypes = [C.POINTER(vp), vp, vp, vp, C.c_size_t]
+    h.hipGraphLaunch.argtypes = [vp, vp]
+    h.hipGraphExecDestroy.argtypes = [vp]
+    h.hipGraphDestroy.argtypes = [vp]
+    return h
+
+
+def test_direct_capture_of_the_context_stream_replays_twice():
+    """A caller that captures gdsm_stream() itself (hipStreamBeginCapture, not gdsm_capture_*):
+    the recorded short release and small coherence batch must replay correctly more than once
+    (round-5 advice: the chained one-launch forms carry a per-launch epoch that a replay would
+    repeat, so every call checks hipStreamIsCapturing and records the zeroing forms). CURRENT
+    and the event buffer change between the two replays; each replay's stream, REPLICA and page
+    table equal the oracle's."""
+    import ctypes as C
+    hip = _hip()
+    n = 48
+    twin, cur1 = _pages(n, 11)
+    _, cur2 = oracle.gen_pages(n, seed=12, mode=0, ppm=60000)
+    counts = np.random.default_rng(13).integers(0, 9, 300).astype(np.uint64)
+    ev1 = oracle.gen_events(counts, seed=14, n_nodes=8, write_pct=30)
+    ev2 = oracle.gen_events(counts, seed=15, n_nodes=8, write_pct=30)
+    m = len(ev1)
+    assert len(ev2) == m and not np.array_equal(ev1, ev2)
+    with ga.Context(n) as c, ga.Context(300, arenas=()) as pt:
+        c.upload("twin", twin)
+        c.upload("current", cur1)
+        c.upload("replica", twin)
+        pt.coh_init(8)
+        d_ev = pt.buffer(8 * m)
+        d_tot = pt.buffer(80)
+        d_ids = c.ids(np.arange(n, dtype=np.uint32))
+        runs = Runs(c, n, cap=n * 4200)
+        ga.gdsm.check(ga.gdsm.lib().gdsm_reserve(c.handle, n, 0), "reserve")
+        ga.gdsm.check(ga.gdsm.lib().gdsm_reserve(pt.handle, 0, m), "reserve")
+        c.sync()
+        pt.sync()
+        graphs = []
+        for ctx, record in ((c, lambda: c.diff(d_ids.ptr, n=n, out=runs, apply_to="replica")),
+                            (pt, None)):
+            s = C.c_void_p(ctx.stream)
+            assert hip.hipStreamBeginCapture(s, 2) == 0  # relaxed mode
+            if record:
+                record()
+            else:
+                ga.gdsm.check(ga.gdsm.lib().gdsm_coherence_batch_async(
+                    pt.handle, d_ev.ptr, m, d_tot.ptr), "coherence")
+            g, ge = C.c_void_p(), C.c_void_p()
+            assert hip.hipStreamEndCapture(s, C.byref(g)) == 0
+            assert hip.hipGraphInstantiate(C.byref(ge), g, None, None, 0) == 0
+            graphs.append((s, g, ge))
+        st, fl = oracle.coh_init(300, 8)
+        for cur, ev in ((cur1, ev1), (cur2, ev2)):
+            c.upload("current", cur)
+            c.upload("replica", twin)
+            d_ev.upload(ev)
+            for s, _, ge in graphs:
+                assert hip.hipGraphLaunch(ge, s) == 0
+            c.sync()
+            pt.sync()
+            h = runs.to_host()
+            ro, data = oracle.diff_pages(twin, cur)
+            assert np.array_equal(h.rec_off, ro)
+            assert np.array_equal(h.data[:int(ro[-1])], data)
+            assert np.array_equal(c.download("replica"), cur)
+            rc, otot = oracle.coherence(st, fl, ev)
+            assert rc == 0
+            tot = d_tot.download(np.uint64, 10)
+            assert tot.tolist() == [otot["invalidations"], otot["transfers"], *otot["node_faults"]]
+            gst, gfl = pt.coh_download()
+            assert np.array_equal(gst, st) and np.array_equal(gfl, fl)
+        for _, g, ge in graphs:
+            hip.hipGraphExecDestroy(ge)
+            hip.hipGraphDestroy(g)
+        runs.free()
