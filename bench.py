@@ -299,7 +299,8 @@ def box_ceilings(ctx, n: int, read=None, copy=None, reps: int = 5) -> dict:
         out[f"box_{key}_gbs_median"] = round(moved / (med.value * 1e-3) / 1e9, 1)
     out["box_probe"] = (f"gdsm_probe_ceiling over this run's own arenas ({n} pages), best of "
                         f"{reps} launches: read = two page arenas read once with 16-B "
-                        f"nontemporal loads (the diff's input), copy = a flat 16-B copy; "
+                        f"nontemporal loads (the diff's input), copy = the fastest of a flat "
+                        f"16-B copy and two page-shaped copies; "
                         f"frac_of_box = achieved / the ceiling matching the kernel")
     return out
 

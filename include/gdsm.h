@@ -148,7 +148,8 @@ int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches);
 /* Box ceilings (measurement support for bench.py, gdsm_probe.hip; no reference counterpart): how
  * fast this GPU streams given page arenas, `reps` launches timed by HIP events on ctx's stream
  * (best and median ms per launch). GDSM_PROBE_READ: arenas a and b (n_pages each) read once, the
- * diff's input pattern; GDSM_PROBE_COPY: dst := a over n_pages pages (dst is overwritten). */
+ * diff's input pattern; GDSM_PROBE_COPY: dst := a over n_pages pages (dst is overwritten), the
+ * fastest of three copy shapes (`reps` launches each). */
 #define GDSM_PROBE_READ 0
 #define GDSM_PROBE_COPY 1
 int gdsm_probe_ceiling(gdsm_ctx* ctx, int kind, const void* a, const void* b, void* dst,

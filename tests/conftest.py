@@ -16,4 +16,5 @@ def golden():
     import numpy as np
     g = ROOT / "tests" / "golden"
     return {k: np.load(g / f"{k}.npz") for k in ("nw_ref", "pages", "coherence", "c1_windows",
-                                                   "ref_windows", "ref_layout")}
+                                                   "ref_windows", "ref_layout",
+                                                   "raw_windows")}

@@ -21,6 +21,10 @@
                  BASELINE config 3's clustered workload, a dense set (40 % of the words
                  rewritten) and the SPEC edge pages of pages.npz; keys '<set>_<field>'. Windows
                  whose reference alignment has gaps keep only L and the crc32s.
+  raw_windows.npz BASELINE's own bytes with no remap: the north-star generator's pages (SPEC §6
+                 uniform 1 %, seed 2026; config 2's are its first 1M) in two ranges of 65 536
+                 pages (the first and the last of the 16M), every 1024-B window whose bytes hold
+                 neither NUL nor '-' (tests/helpers.py:RAW_RANGES), through the reference diff().
   ref_layout.npz zone offsets of test_mmult's objects (test/test_mmult.cpp:31-37, 152-154) as
                  the REFERENCE custom_malloc hands them out (libgallocy.cpp over
                  heaplayers/application.h:20-29, compiled in place into
@@ -40,7 +44,8 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 from oracle import oracle  # noqa: E402
-from tests.helpers import REF_WINDOW_SETS, c1_windows, window_pages  # noqa: E402
+from tests.helpers import (RAW_RANGES, REF_WINDOW_SETS, c1_windows, raw_range_pages,  # noqa: E402
+                           raw_windows, window_pages)
 
 OUT = Path(__file__).resolve().parent
 
@@ -141,12 +146,14 @@ def make_pages():
     print("pages.npz", twin.shape[0], "edge pages;", int(ro2[-1]), "B for config 1")
 
 
-def _ref_windows(t, c):
-    """The pages cut into 1024-B windows, each pair aligned by the REFERENCE diff(): alignment
-    length, crc32 of both strings, gap-free flag and (gap-free windows) the bit-packed positions
-    where out1[i] != out2[i]."""
+def _ref_windows(t, c, sel=None):
+    """The pages cut into 1024-B windows (those listed in `sel`, else all), each pair aligned by
+    the REFERENCE diff(): alignment length, crc32 of both strings, gap-free flag and (gap-free
+    windows) the bit-packed positions where out1[i] != out2[i]."""
     import zlib
     tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+    if sel is not None:
+        tw, cw = tw[sel], cw[sel]
     cases = [(tw[i].tobytes(), cw[i].tobytes()) for i in range(len(tw))]
     outs = oracle.ref_nw_batch(cases)
     L = np.array([len(o1) for o1, _ in outs], np.int64)
@@ -177,6 +184,24 @@ def make_ref_windows():
         out.update({f"{name}_{k}": v for k, v in d.items()})
         print(name, len(d["L"]), "windows,", int(d["gapfree"].sum()), "gap-free")
     np.savez_compressed(OUT / "ref_windows.npz", **out)
+
+
+def make_raw_windows():
+    """raw_windows.npz: BASELINE's own bytes, unremapped (tests/helpers.py:RAW_RANGES): every
+    window of the two north-star page ranges that holds no 0x00 / 0x2D byte, through the
+    reference diff(); keys 'r<i>_<field>' plus 'r<i>_win' (window index inside the range)."""
+    out = {}
+    for i, (first, n) in enumerate(RAW_RANGES):
+        t, c = raw_range_pages(first, n)
+        win = raw_windows(t, c)
+        d = _ref_windows(t, c, win)
+        out.update({f"r{i}_{k}": v for k, v in d.items()})
+        out[f"r{i}_win"] = win.astype(np.int64)
+        out[f"r{i}_range"] = np.array([first, n], np.int64)
+        dirty = d["mask"].any(axis=1)
+        print(f"range {first}+{n}:", len(win), "windows,", int(d["gapfree"].sum()), "gap-free,",
+              int((dirty & d["gapfree"]).sum()), "gap-free with changes")
+    np.savez_compressed(OUT / "raw_windows.npz", **out)
 
 
 LAYOUT_DRIVER = ROOT / "oracle" / "_ref" / "ref_layout_driver"
@@ -234,8 +259,10 @@ def make_coherence():
 if __name__ == "__main__":
     if not oracle.ref_available():
         raise SystemExit("oracle/_ref/ref_nw_driver missing: run `make -C oracle ref` here first")
-    which = sys.argv[1:] or ["nw", "pages", "coherence", "c1_windows", "ref_windows", "layout"]
+    which = sys.argv[1:] or ["nw", "pages", "coherence", "c1_windows", "ref_windows", "layout",
+                             "raw_windows"]
     for w in which:
         {"nw": make_nw, "pages": make_pages, "coherence": make_coherence,
          "c1_windows": make_c1_windows, "ref_windows": make_ref_windows,
+         "raw_windows": make_raw_windows,
          "layout": make_layout}[w]()

@@ -80,6 +80,27 @@ def window_pages(name: str, golden=None):
     return c1_remap(t), c1_remap(c)
 
 
+# Windows of BASELINE's own bytes, no remap (tests/golden/raw_windows.npz): the north-star /
+# config-2 generator (SPEC §6 UNIFORM, 10 000 ppm, bench seed 2026; config 2's 1M pages are the
+# north star's first 1M), two ranges of 65 536 pages (the first and the last of the 16M). Every
+# 1024-B window whose twin and current bytes hold neither 0x00 nor '-' (0x2D) is taken as it is:
+# the reference diff() returns NUL-terminated alignments with '-' gaps (diff.h:9-11), so those
+# two bytes are the only ones it cannot carry.
+RAW_RANGES = ((0, 65536), ((16 << 20) - 65536, 65536))
+
+
+def raw_range_pages(first: int, n: int):
+    """(twin, current) of north-star pages [first, first + n): BASELINE's bytes, unremapped."""
+    from oracle import oracle
+    return oracle.gen_pages(n, seed=2026, mode=0, ppm=10000, first_page=first)
+
+
+def raw_windows(t: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """Indices of the 1024-B windows of (t, c) that hold no 0x00 and no 0x2D byte on either side."""
+    tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+    return np.flatnonzero(~((tw == 0) | (tw == 0x2D) | (cw == 0) | (cw == 0x2D)).any(axis=1))
+
+
 def runs_positions(rec_off, data, n_pages: int) -> np.ndarray:
     """bool[n_pages * 4096]: True at every byte covered by a run of the stream (SPEC §3),
     record i describing page i."""

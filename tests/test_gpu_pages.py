@@ -10,7 +10,8 @@ from gallocy_amd import _lib
 from gallocy_amd._lib import GdsmRuns
 from gallocy_amd.gdsm import GdsmError, HostRuns, Runs
 from oracle import oracle
-from tests.helpers import REF_WINDOW_SETS, c1_windows, np_diff, runs_positions, window_pages
+from tests.helpers import (RAW_RANGES, REF_WINDOW_SETS, c1_windows, np_diff, raw_range_pages,
+                           runs_positions, window_pages)
 
 pytestmark = pytest.mark.gpu
 
@@ -628,6 +629,46 @@ def test_ref_windows_pinned_by_reference_diff(name, variant, golden):
     for w in np.flatnonzero(gapfree):
         assert zlib.crc32(rep[w].tobytes()) == int(crc[w][1]), w
     assert np.array_equal(rep.reshape(n, 4096), cur)
+
+
+@pytest.mark.parametrize("r", [0, 1])
+def test_raw_windows_pinned_by_reference_diff(r, golden):
+    """BASELINE's own bytes, no remap (tests/golden/raw_windows.npz, the reference diff() through
+    oracle/_ref): the north-star pages of range r generated ON THE GPU (gdsm_gen_pages, seed
+    2026, uniform 1 %, the bench's generator) and diffed whole by gdsm_diff in the bench's
+    geometry. For every reference window (no NUL / '-' byte, all gap-free): the twin and current
+    bytes are the reference's out1 / out2 (crc32), the runs cover exactly {i : out1[i] !=
+    out2[i]}, and gdsm_apply of the stream to REPLICA gives out2."""
+    import zlib
+    g = golden["raw_windows"]
+    pre = f"r{r}_"
+    first, n = (int(x) for x in g[pre + "range"])
+    assert (first, n) == RAW_RANGES[r]
+    win, crc, mask = (g[pre + k] for k in ("win", "crc", "mask"))
+    ref = np.unpackbits(mask, axis=1).astype(bool)
+    with ga.Context(n) as c:
+        c.gen_pages(seed=2026, mode=ga.GEN_UNIFORM, ppm=10000, first_global=first)
+        runs = c.diff(cap=n * 128)
+        c.apply(runs)
+        c.sync()
+        h = runs.to_host()
+        pages = np.unique(win // 4)
+        tw = np.concatenate([c.download("twin", int(p), 1) for p in pages]).reshape(-1, 1024)
+        cw = np.concatenate([c.download("current", int(p), 1) for p in pages]).reshape(-1, 1024)
+        rw = np.concatenate([c.download("replica", int(p), 1) for p in pages]).reshape(-1, 1024)
+    where = {int(p): i for i, p in enumerate(pages)}
+    for j, w in enumerate(win):
+        k = 4 * where[int(w) // 4] + int(w) % 4
+        assert [zlib.crc32(tw[k].tobytes()), zlib.crc32(cw[k].tobytes())] == crc[j].tolist(), w
+        assert zlib.crc32(rw[k].tobytes()) == int(crc[j][1]), w
+        p = int(w) // 4
+        a, b = int(h.rec_off[p]), int(h.rec_off[p + 1])
+        pos = runs_positions(np.array([0, b - a], np.uint64), h.data[a:b], 1).reshape(4, 1024)
+        assert np.array_equal(pos[int(w) % 4], ref[j]), w
+    # and the host generator agrees with the device one on these pages
+    t, cu = raw_range_pages(first, n)
+    assert np.array_equal(t[pages].reshape(-1, 1024), tw)
+    assert np.array_equal(cu[pages].reshape(-1, 1024), cw)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])

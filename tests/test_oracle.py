@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle
-from tests.helpers import (REF_WINDOW_SETS, c1_windows, hash3, np_diff, np_runs, py_coherence,
+from tests.helpers import (RAW_RANGES, REF_WINDOW_SETS, c1_windows, raw_range_pages, raw_windows, hash3, np_diff, np_runs, py_coherence,
                            runs_positions, window_pages, zipf_counts)
 
 
@@ -254,6 +254,40 @@ def test_ref_windows_pinned_by_reference_diff(name, golden):
     for i in np.flatnonzero(~gapfree):
         o1, o2 = oracle.nw_diff(tw[i].tobytes(), cw[i].tobytes())
         assert len(o1) == L[i] and [zlib.crc32(o1), zlib.crc32(o2)] == crc[i].tolist(), i
+
+
+@pytest.mark.parametrize("r", [0, 1])
+def test_raw_windows_pinned_by_reference_diff(r, golden):
+    """BASELINE's own bytes, no remap (tests/helpers.py:RAW_RANGES; fixture
+    tests/golden/raw_windows.npz from the reference diff(), gallocy/utils/diff.cpp:73-167, run
+    through oracle/_ref, test/test_diff.cpp:38-57 window shape): the north-star generator's pages
+    at seed 2026 in the first and the last 65 536 of the 16M. The windows are the ones holding
+    no NUL and no '-' byte, which the selection rule reproduces; every one is gap-free, so
+    {i : out1[i] != out2[i]} must equal the positions the oracle's runs cover, out1 / out2 the
+    window's twin / current bytes (crc32), and the oracle's apply must give out2."""
+    import zlib
+    g = golden["raw_windows"]
+    pre = f"r{r}_"
+    first, n = (int(x) for x in g[pre + "range"])
+    assert (first, n) == RAW_RANGES[r]
+    win, crc, gapfree, mask = (g[pre + k] for k in ("win", "crc", "gapfree", "mask"))
+    t, c = raw_range_pages(first, n)
+    assert np.array_equal(raw_windows(t, c), win)
+    assert gapfree.all() and len(win) >= 60
+    ref = np.unpackbits(mask, axis=1).astype(bool)
+    assert ref.any(axis=1).sum() >= 50  # most windows hold changed words
+    pages = np.unique(win // 4)
+    tp, cp = t[pages], c[pages]
+    ro, data = oracle.diff_pages(tp, cp)
+    pos = runs_positions(ro, data, len(pages)).reshape(len(pages), 4, 1024)
+    tw, cw = t.reshape(-1, 1024), c.reshape(-1, 1024)
+    where = {int(p): i for i, p in enumerate(pages)}
+    for j, w in enumerate(win):
+        assert [zlib.crc32(tw[w].tobytes()), zlib.crc32(cw[w].tobytes())] == crc[j].tolist(), w
+        assert np.array_equal(pos[where[int(w) // 4], int(w) % 4], ref[j]), w
+    rep = tp.copy()
+    assert oracle.apply(rep, ro, data) == 0
+    assert np.array_equal(rep, cp)
 
 
 def test_coherence_rejects_node_outside_the_table():
