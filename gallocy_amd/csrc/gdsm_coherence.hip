@@ -162,69 +162,6 @@ __device__ __forceinline__ uint32_t wave_rev_compose_dpp(uint32_t v) {
   return lane_bcast(v, 63);
 }
 
-// GDSM_FOLD_PS (default 1): every segment of the walk starts from PROBE and is corrected against
-// its incoming state afterwards (ps_close), so the walk never loads a page-table word and its
-// head steps are a few selects; 0: the round-5 walk (the lane's first and last heads seeded
-// with their gathered words, middle heads' words loaded inside the walk), kept for A/B.
-#ifndef GDSM_FOLD_PS
-#define GDSM_FOLD_PS 0
-#endif
-#ifndef GDSM_PS_EARLY
-#define GDSM_PS_EARLY 0
-#endif
-// A probe segment's summary in 32 bits: copyset (8) | kHE, kHW, kPRE (3) << 8 | last writer
-// (3) << 11 | misses (6) << 14 | the prefix's readers P8 (8) << 20 | first writer (3) << 28.
-__device__ __forceinline__ uint32_t ps_pack(uint32_t H, uint32_t O, uint32_t t, uint32_t Hc,
-                                            uint32_t Xc) {
-  return (H & 0xFFu) | (((H >> 16) & 7u) << 8) | (((O >> 1) & 7u) << 11) | (t << 14) |
-         ((Hc & 0xFFu) << 20) | (((Xc >> 1) & 7u) << 28);
-}
-// The summary the walk gives a one-event segment (event e alone from PROBE).
-__device__ __forceinline__ uint32_t ps_single(uint32_t e) {
-  const uint32_t n = (e >> 1) & 7u, m = 1u << n;
-  return (e & 1u) ? (m | (3u << 8) | (n << 11) | (1u << 14) | (n << 28))
-                  : (m | (4u << 8) | (7u << 11) | (1u << 14) | (m << 20) | (n << 28));
-}
-// A probe segment met with incoming state `cur` (a CONST: a head's page-table word, or the
-// lane's carry): its final state and fault count, and the corrections of the lane's totals (the
-// prefix reads that hit after all; the first write's fault, invalidations and transfer).
-struct PsOut {
-  uint32_t state, count, dinv, dxfer, cfe, cfo;
-};
-__device__ __forceinline__ PsOut ps_close(uint32_t cur, uint32_t rec) {
-  PsOut r;
-  const uint32_t fl = (rec >> 8) & 7u, on = (rec >> 11) & 7u, ts = (rec >> 14) & 63u;
-  const uint32_t P8 = (rec >> 20) & 0xFFu, w = (rec >> 28) & 7u;
-  const uint32_t h = (rec & 0xFFu) | ((fl & 1u) ? kHE : 0u) | ((fl & 2u) ? kHW : 0u);
-  const uint32_t hitP = P8 & cur & 0xFFu;  // prefix reads that hit after all
-  const uint32_t s1 = tcompose(cur, P8);   // the state after the prefix
-  uint32_t d = (uint32_t)__popc(hitP);
-  const uint32_t e = hitP & 0x55u, o = (hitP >> 1) & 0x55u;
-  r.cfe = (e & 1u) | ((e & 4u) << 6) | ((e & 16u) << 12) | ((e & 64u) << 18);
-  r.cfo = (o & 1u) | ((o & 4u) << 6) | ((o & 16u) << 12) | ((o & 64u) << 18);
-  r.dinv = 0;
-  r.dxfer = 0;
-  if (!(fl & 4u)) {  // the prefix ended at a write by w
-    const uint32_t wb = 1u << w, own = (s1 >> 8) & 0xFFu;
-    const bool f = !(((s1 >> 16) & 3u) == 2u && own == w);
-    r.dinv = (f ? (uint32_t)__popc(s1 & 0xFFu & ~wb) : 0u) - (uint32_t)__popc(P8 & ~wb);
-    r.dxfer = (f && own != w) ? 0u : ~0u;  // the probe counted one transfer
-    if (!f) {
-      d += 1;
-      const uint32_t one = 1u << (8u * (w >> 1));
-      if (w & 1u)
-        r.cfo += one;
-      else
-        r.cfe += one;
-    }
-    r.state = seg_final(h, 2u * on, 0u);
-  } else {
-    r.state = s1 & 0x7FFFFu;
-  }
-  r.count = ts - d;
-  return r;
-}
-
 // 2v + (this lane's bit of `mask`): one v_addc with the lane mask as carry-in.
 __device__ __forceinline__ uint32_t shl1_add(uint32_t v, uint64_t mask) {
   uint32_t r;
@@ -345,334 +282,6 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   if (lane == 0) xp = xprev_w;
   const bool batch_first = lo == 0 && lane == 0;
 
-#if GDSM_FOLD_PS
-  // ---- heads (a new page) and validity: pages must not decrease (every event is checked here,
-  // so the walk carries no check) and (kNodes) every node lies inside the group
-  uint32_t X[kFH];
-  uint32_t hm = 0;
-  uint32_t bad = hib ? 1u : 0u;
-  uint32_t dec = 0;    // bit 31: a page decreased somewhere (pages < 2^28)
-  uint32_t nodes = 0;  // kNodes: the largest node field
-#pragma unroll
-  for (uint32_t h = 0; h < kFK / kFH; ++h) {
-    fold_half(tr, lane, h, X);
-#pragma unroll
-    for (uint32_t j = 0; j < kFH; ++j) {
-      const uint32_t k = kFH * h + j;
-      if (kFull || k < nv) {
-        const uint32_t x = X[j], pv = j ? X[j ? j - 1 : 0] : xp;
-        const uint32_t pg = x >> 4, pp = pv >> 4;
-        const bool first = k == 0 && batch_first;
-        const bool head = first || pg != pp;
-        if (!first) dec |= pg - pp;
-        asm volatile("" : "+v"(dec));  // in order: else every page is kept to the end (+23 VGPRs)
-        if (kNodes) {
-          nodes = max(nodes, x & 14u);
-          asm volatile("" : "+v"(nodes));
-        }
-        if (kFull)
-          hm = shl1_add(hm, __ballot(head));  // bit 31 - k, one v_addc per event
-        else
-          hm |= (head ? 1u : 0u) << k;
-      }
-    }
-    xp = X[kFH - 1];
-  }
-  if (dec >> 31) bad = 1;
-  if (kNodes && (nodes >> 1) >= n_nodes) bad = 1;
-  if (kFull) hm = __brev(hm) >> (32u - kFK);
-  const uint32_t hc = (uint32_t)__popc(hm);
-  const uint32_t kl = hc ? 31u - (uint32_t)__builtin_clz(hm) : 0u;  // the lane's last head
-  uint32_t xf = 0, xl = 0;  // the lane's first and last head events
-  if (hc) {
-    xf = tr[fold_slot(kFK * lane + (uint32_t)__builtin_ctz(hm))];
-    xl = tr[fold_slot(kFK * lane + kl)];
-  }
-  asm volatile("" : "+v"(hm), "+v"(xf), "+v"(xl));
-  if (nv && (xlast >> 4) >= n_pages) bad = 1;
-  uint32_t nh0 = from_next_lane(hm & 1u);
-  if (lane == 63) nh0 = has_next ? (((xnext_w >> 4) != (xlast >> 4)) ? 1u : 0u) : 1u;
-  bool last_end = nh0 != 0;
-  if (!kFull && nv > 0 && g0 + nv == n) last_end = true;
-  // the lane's first segment continues one opened before the lane; it ends in the lane
-  const bool cont = nv && !(hm & 1u);
-  const bool hasD = cont && (hc != 0 || last_end);
-
-  // ---- page-table words of the lane's last, first and second heads: gathered now, used after
-  // the walk (which never waits for one)
-  uint64_t Wl = 0, Wf = 0, Ws = 0;
-  {
-    const uint32_t pl = xl >> 4, pf = xf >> 4;
-    if (hc && pl < n_pages) Wl = pt[pl];
-    if (hc > 1 && pf < n_pages) Wf = pt[pf];
-    if (GDSM_FOLD_PRE2 && hc > 2) {
-      const uint32_t h2 = hm & (hm - 1u);
-      const uint32_t p2 = tr[fold_slot(kFK * lane + (uint32_t)__builtin_ctz(h2))] >> 4;
-      if (p2 < n_pages) Ws = pt[p2];
-    }
-  }
-  if ((GDSM_FOLD_PRIO & 5) == 5) __builtin_amdgcn_s_setprio(0);
-  if (!GDSM_PS_EARLY && early) {
-    // Early publication (see above), once the gathered words have landed (the last head's is
-    // the only one another wave may store): successors need not wait for this walk.
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    if (lane == 0)
-      __hip_atomic_store(status + b, kFAgg | (__ballot(hc != 0) ? kFHead : 0ull) | eagg,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-
-  // ---- the walk. Every segment starts from PROBE at its head (an empty copyset, no write hits,
-  // kPRE: "still in the prefix"), so no page-table word is needed here: the reads before the
-  // segment's first write count one miss per node and the first write misses; Hc / Xc keep the
-  // prefix's copyset and the first write. A segment that closes inside the lane (at the next
-  // head) leaves a 4-B summary in the LDS slot of its last event (ps_pack: its events were read
-  // already, and that slot is never a head's or event 0's); a one-event segment leaves none (the
-  // segment pass recomputes it from its event). The lane's open segment stays in registers. All
-  // of them are corrected against their incoming states after the walk (ps_close).
-  static_assert(kFK == 32, "fold_slot(kFK lane + k) = rec_base ^ k needs 32 events per lane");
-  const uint32_t rec_base = fold_slot(kFK * lane);
-  uint32_t H = kPRE, O = 0x1FEu, c0 = 0, T = 0;
-  uint32_t inv = 0, xfer = 0, F[4] = {0, 0, 0, 0}, Hc = kPRE, Xc = 0, pm = ~0u;
-#pragma unroll
-  for (uint32_t h = 0; h < (kM == 1 ? 0u : kFK / kFH); ++h) {
-    fold_half(tr, lane, h, X);
-#pragma unroll
-    for (uint32_t j = 0; j < kFH; ++j) {
-      const uint32_t k = kFH * h + j;
-      if (kFull || k < nv) {
-        const uint32_t x = X[j];
-        uint32_t hmk = hm;  // opaque per step: the head tests are not hoisted out of the walk
-        asm volatile("" : "+v"(hmk));
-        const uint32_t isH = (hmk >> k) & 1u;
-        if (__ballot(isH != 0u)) {
-          // the segment closing here, when it holds two or more events (k - 1 is no head)
-          if (k >= 2 && ((hmk >> (k - 1)) & 3u) == 2u) {
-            // (fold_slot(kFK lane + k') = L ^ k' for k' < 32; L opaque, so the compiler does not
-            // keep 31 precomputed slot addresses live through the walk)
-            uint32_t L = rec_base;
-            asm volatile("" : "+v"(L));
-            tr[L ^ (k - 1)] = ps_pack(H, O, T - c0, Hc, Xc);
-          }
-          if (isH) {
-            H = kPRE;
-            O = 0x1FEu;
-            Hc = kPRE;
-            c0 = T;
-            pm = ~0u;
-          }
-        }
-        Xc = bfi(pm, x, Xc);  // the event, while still in the prefix
-        const uint32_t xn2 = x & 14u, nd = xn2 >> 1, rw = x & 1u;
-        const bool wr = rw != 0u;
-        const uint32_t bi = nd + (rw << 3);
-        const uint32_t hitv = __builtin_amdgcn_ubfe(H, bi, 1u);
-        const bool hit = hitv != 0;
-        const uint32_t miss = hitv ^ 1u;
-        const uint32_t m = 1u << nd;
-        const uint32_t sel = (wr && !hit) ? (H & kHRead & ~m) : 0u;
-        asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(inv) : "v"(sel), "v"(inv));
-        xfer += (wr && O != xn2) ? 1u : 0u;  // a write by a non-owner always faults
-        const uint32_t Hr = hit ? H : ((H | m) & kKr);
-        H = wr ? ((0x101u << nd) | (kHE | kHW)) : Hr;
-        O = wr ? xn2 : O;
-        asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(F[k / 8]) : "v"(miss), "v"(2u * xn2), "v"(F[k / 8]));
-        T += miss;
-        pm = (uint32_t)((int32_t)(H << 13) >> 31);  // still in the prefix after this event
-        asm volatile("" : "+v"(pm));
-        Hc = bfi(pm, H, Hc);
-        asm volatile("" : "+v"(inv), "+v"(xfer), "+v"(F[k / 8]), "+v"(Hc), "+v"(Xc));
-      }
-    }
-    if (GDSM_PS_EARLY && h == 0 && early) {
-      // (GDSM_PS_EARLY 1: the early publication after the walk's first half, by when the
-      // gathered words have landed without a wait; the walk itself issues no global load)
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      if (lane == 0)
-        __hip_atomic_store(status + b, kFAgg | (__ballot(hc != 0) ? kFHead : 0ull) | eagg,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  uint32_t cFe = 0, cFo = 0;  // probe corrections of the per-node fault bytes (nodes 2i / 2i+1)
-  const uint32_t rec_open = ps_pack(H, O, T - c0, Hc, Xc);  // the lane's open segment
-  // ---- the lane's last segment (opened at its last head): exact now that its word is here
-  const uint32_t Bl = (uint32_t)Wl & 0x7FFFFu, Bfl = (uint32_t)(Wl >> 32);
-  uint32_t a;         // the lane's transform (its aggregate)
-  uint32_t own_last = 0;
-  if (hc) {
-    const PsOut r = ps_close(kConst | Bl, rec_open);
-    inv += r.dinv;
-    xfer += r.dxfer;
-    cFe += r.cfe;
-    cFo += r.cfo;
-    a = kConst | r.state;
-    own_last = r.count;
-    if (last_end && (xlast >> 4) < n_pages)  // it also ends here: the whole segment is this lane's
-      pt[xlast >> 4] = (uint64_t)r.state | ((uint64_t)(Bfl + r.count) << 32);
-  } else {
-    // no head: the lane's events continue one segment; after its first write its state no
-    // longer depends on the incoming one, before it the lane is READ(its readers)
-    a = !(H & kPRE) ? (kConst | seg_final(H, O, 0u)) : hit_copyset(H);
-  }
-
-  // ---- lane aggregate, scan, publish, look back
-  COH_FSTAMP(2, __builtin_amdgcn_s_memtime());
-  const uint32_t inc = wave_incl_compose_dpp(a);
-  const uint32_t agg = lane_bcast(inc, 63);
-  const bool whead = __ballot(hc != 0) != 0;
-  if (early && agg != eagg) bad = 1;  // never expected
-  if (!early) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the gathered words have landed
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  }
-  if (lane == 0 && !early)
-    __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (whead ? kFHead : 0ull) | agg,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-  // ---- the segments that close inside the lane at a later head (pages no other lane or wave
-  // touches): corrected against their heads' words (the first two gathered before the walk, the
-  // others loaded here) and stored whole
-  {
-    uint32_t mm = hc > 1 ? hm & ~(1u << kl) : 0u;  // heads whose segment closes at the next head
-    uint32_t i = 0;
-    while (mm) {
-      const uint32_t p = (uint32_t)__builtin_ctz(mm);
-      mm &= mm - 1u;
-      const uint32_t pn = mm ? (uint32_t)__builtin_ctz(mm) : kl;  // the next head
-      const uint32_t e = tr[fold_slot(kFK * lane + p)];
-      const uint32_t pg = e >> 4;
-      const uint32_t rec = pn - p > 1u ? tr[fold_slot(kFK * lane + pn - 1u)] : ps_single(e);
-      uint64_t W;
-      if (i == 0)
-        W = Wf;
-      else if (GDSM_FOLD_PRE2 && i == 1)
-        W = Ws;
-      else
-        W = pt[pg < n_pages ? pg : 0u];  // (a page >= n_pages fails the batch)
-      const PsOut r = ps_close(kConst | ((uint32_t)W & 0x7FFFFu), rec);
-      inv += r.dinv;
-      xfer += r.dxfer;
-      cFe += r.cfe;
-      cFo += r.cfo;
-      if (pg < n_pages) pt[pg] = (uint64_t)r.state | ((uint64_t)((uint32_t)(W >> 32) + r.count) << 32);
-      ++i;
-    }
-  }
-
-  // Only a wave that stores the state of a segment opened before it (its first segment ends
-  // here) needs the head's wave to have loaded that page's word: it looks back to a block with a
-  // head. Every other wave stops at the nearest CONST aggregate or inclusive prefix (CONST
-  // absorbs everything before it), so the blocks of a hot page do not chain their look-backs.
-  const bool ordered = kM != 3 &&
-                       __ballot(hasD && (__ballot(hc != 0) & ((1ull << lane) - 1ull)) == 0) != 0;
-  uint32_t carry = 0;
-  if (GDSM_FOLD_PRIO & 2) __builtin_amdgcn_s_setprio(2);
-  if (b > 0 && kM != 2) {
-    int64_t pos = (int64_t)b - 1;
-    for (;;) {
-      const int64_t q = pos - (int64_t)lane;
-      uint64_t st = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : kFIncl;
-      uint32_t s, spins = 0;
-      for (;;) {
-        const uint64_t pub = __ballot((st >> 62) != 0);
-        const uint64_t stop =
-            __ballot(ordered ? (st & kFHead) != 0
-                             : ((st >> 62) == 2 || (st & kFHead) || (st & kConst)));
-        const uint32_t u = ~pub ? (uint32_t)__builtin_ctzll(~pub) : 64u;
-        s = (stop & pub) ? (uint32_t)__builtin_ctzll(stop & pub) : 64u;
-        if (s < u || u == 64) break;
-        if (++spins > (1u << 24)) {  // never expected: fail the batch rather than hang the GPU
-          bad = 1;
-          s = u;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        if ((st >> 62) == 0 && q >= 0)
-          st = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      uint32_t part;
-      if (s == 0)
-        part = (uint32_t)lane_bcast64(st, 0);
-      else
-        part = wave_rev_compose_dpp(lane <= s ? (uint32_t)st : 0u);
-      carry = tcompose(part, carry);
-      if (s < 64) break;
-      pos -= 64;
-    }
-    if (lane == 0)
-      __hip_atomic_store(status + b, kFIncl | (whead ? kFHead : 0ull) | tcompose(carry, agg),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  COH_FSTAMP(3, __builtin_amdgcn_s_memtime());
-  const uint32_t cur = tcompose(carry, from_prev_lane(inc));
-  if (cont && !(cur & kConst)) bad = 1;
-
-  // ---- the lane's first segment (opened before the lane): corrected against the incoming
-  // state `cur`; its summary is the record before the first head (or event 0 alone), or the open
-  // segment's registers when the lane holds no head
-  uint32_t Df = 0, Dc = 0;
-  if (cont) {
-    const uint32_t p0 = hc ? (uint32_t)__builtin_ctz(hm) : 0u;
-    const uint32_t rec = !hc ? rec_open
-                             : p0 > 1u ? tr[fold_slot(kFK * lane + p0 - 1u)]
-                                       : ps_single(tr[fold_slot(kFK * lane)]);
-    const PsOut r = ps_close(cur, rec);
-    inv += r.dinv;
-    xfer += r.dxfer;
-    cFe += r.cfe;
-    cFo += r.cfo;
-    Df = r.state;
-    Dc = r.count;
-  }
-  const uint32_t dP = tr[fold_slot(kFK * lane)] >> 4;  // the first segment's page
-
-  // ---- fault counts of segments that cross lanes (counts only: old counts are 32-bit)
-  const uint32_t own = hc ? own_last : Dc;
-  const uint32_t sin = wave_incl_segsum_dpp((hc ? kConst : 0u) | own);
-  const uint32_t cnt_in = from_prev_lane(sin) & ~kConst;
-  const uint64_t hb = __ballot(hc != 0);
-  const uint64_t below = hb & ((1ull << lane) - 1ull);
-  const uint32_t hl = below ? 63u - (uint32_t)__clzll(below) : 0u;
-  const uint32_t oldf = (uint32_t)__shfl((int)Bfl, (int)hl, 64);
-  uint32_t* pst = reinterpret_cast<uint32_t*>(pt);
-  if (hasD && dP < n_pages) {
-    const uint32_t c = cnt_in + Dc;
-    if (below) {
-      pt[dP] = (uint64_t)Df | ((uint64_t)(oldf + c) << 32);
-    } else {  // the wave's first segment: opened before it
-      pst[2 * (uint64_t)dP] = Df;
-      if (c) atomicAdd(&pst[2 * (uint64_t)dP + 1], c);
-    }
-  }
-  if (kFull && lane == 63 && !last_end) {  // the wave's last segment continues
-    const uint32_t p = xlast >> 4, c = sin & ~kConst;
-    if (c && p < n_pages) atomicAdd(&pst[2 * (uint64_t)p + 1], c);
-  }
-
-  // ---- totals: one partial row per wave (16-bit fields hold a wave's sums)
-  uint32_t Fe = 0, Fo = 0;  // bytes: nodes 0, 2, 4, 6 / 1, 3, 5, 7
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    Fe += F[q] & 0x0F0F0F0Fu;
-    Fo += (F[q] >> 4) & 0x0F0F0F0Fu;
-  }
-  Fe -= cFe;
-  Fo -= cFo;
-  const uint32_t v[5] = {inv | (xfer << 16), (Fe & 0xFFu) | ((Fo & 0xFFu) << 16),
-                         ((Fe >> 8) & 0xFFu) | (((Fo >> 8) & 0xFFu) << 16),
-                         ((Fe >> 16) & 0xFFu) | (((Fo >> 16) & 0xFFu) << 16),
-                         (Fe >> 24) | ((Fo >> 24) << 16)};
-  uint32_t mine = 0;
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const uint32_t s = wave_sum(v[q]);
-    if (lane == 2u * q) mine = s & 0xFFFFu;
-    if (lane == 2u * q + 1u) mine = s >> 16;
-  }
-  if (lane < 10) partial[b * 10 + lane] = mine;
-  if (kM == 0 && __ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
-  COH_FSTAMP(4, __builtin_amdgcn_s_memtime());
-#else
   // ---- heads (a new page), validity. (Sortedness inside a lane is checked where the walk meets
   // a head; the first / last head events are read back from LDS.)
   uint32_t X[kFH];
@@ -1036,26 +645,18 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   if (lane < 10) partial[b * 10 + lane] = mine;
   if (kM == 0 && __ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
   COH_FSTAMP(4, __builtin_amdgcn_s_memtime());
-#endif  // GDSM_FOLD_PS
 }
 
 // kFull: the batch's whole blocks, one ticket per workgroup (tickets are drawn in dispatch
 // order, so a wave only ever waits for running waves); otherwise the single trailing partial
 // block `nb - 1`, launched after them.
-// GDSM_FOLD_PERSIST (measurement, default 0): 1 = a grid of resident workgroups that draw
-// tickets until the blocks run out; 2 = the same with the workgroups' starts staggered by
-// their slot on the CU (slot = blockIdx / `cus`, slot x ~3.4 us), so that the waves sharing a
-// SIMD are not all loading, or all walking, at the same time.
-#ifndef GDSM_FOLD_PERSIST
-#define GDSM_FOLD_PERSIST 0
-#endif
 template <bool kVec, bool kFull, bool kNodes, int kM = 0>
 __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                        const uint64_t* __restrict__ ev, uint64_t n,
                                                        uint64_t nb, uint64_t* __restrict__ ws,
                                                        uint32_t* __restrict__ partial,
                                                        uint32_t* __restrict__ err,
-                                                       uint32_t n_nodes, uint32_t cus) {
+                                                       uint32_t n_nodes) {
   __shared__ __attribute__((aligned(16))) uint32_t tr_all[4][kFBlock];
   uint64_t b;
   if (kFull) {
@@ -1067,26 +668,13 @@ __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt
     // (the ticket passes through wave 0's event buffer: a separate LDS word would take the
     // workgroup past 32 KiB and cost a workgroup per CU)
     const uint32_t cls = blockIdx.x % kFoldCtrs;
-    if (GDSM_FOLD_PERSIST >= 2 && cus) {
-      for (uint32_t d = blockIdx.x / cus; d; --d) __builtin_amdgcn_s_sleep(127);
-    }
-    for (;;) {
-      if (threadIdx.x == 0) tr_all[0][0] = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
-      __syncthreads();
-      const uint32_t ticket = __builtin_amdgcn_readfirstlane(tr_all[0][0]);
-      __syncthreads();
-      const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
-      b = w * 4 + (threadIdx.x >> 6);
-      if (!GDSM_FOLD_PERSIST) {
-        if (b >= nb) return;
-        break;
-      }
-      if (w * 4 >= nb) return;  // workgroup-uniform
-      if (b < nb)
-        coh_fold_wave<kVec, kFull, kNodes, kM>(pt, n_pages, ev, n, b, ws + kFoldStatus, partial,
-                                               err, n_nodes, tr_all[threadIdx.x >> 6]);
-      __syncthreads();  // the event images are reused by the next block
-    }
+    if (threadIdx.x == 0) tr_all[0][0] = atomicAdd(reinterpret_cast<uint32_t*>(ws + cls * 32), 1u);
+    __syncthreads();
+    const uint32_t ticket = __builtin_amdgcn_readfirstlane(tr_all[0][0]);
+    __syncthreads();
+    const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
+    b = w * 4 + (threadIdx.x >> 6);
+    if (b >= nb) return;
   } else {
     if (threadIdx.x >= 64) return;
     b = nb - 1;
@@ -1741,27 +1329,13 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
         if (vec && !nodes && cv == 6) kern = coh_fold_kernel<true, true, false, 3>;
         if (vec && !nodes && cv == 7) kern = coh_fold_kernel<true, true, false, 4>;
 #endif
-        uint64_t grid = (full + 3) / 4;
-        uint32_t cus = 0;
-        if (GDSM_FOLD_PERSIST) {  // (measurement) the resident grid, a multiple of kFoldCtrs
-          int dev = 0, ncu = 0, occ = 0;
-          if (hipGetDevice(&dev) == hipSuccess &&
-              hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) ==
-                  hipSuccess &&
-              hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) == hipSuccess &&
-              ncu > 0 && occ > 0) {
-            const uint64_t res = (uint64_t)ncu * (uint64_t)occ / kFoldCtrs * kFoldCtrs;
-            if (res && res < grid) grid = res;
-            cus = (uint32_t)ncu;
-          }
-        }
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, s, pt, n_pages,
-                           events, n_events, full, fws, fpart, err, n_nodes, cus);
+        hipLaunchKernelGGL(kern, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
+                           events, n_events, full, fws, fpart, err, n_nodes);
       }
       if (nf > full) {
         auto kern = nodes ? coh_fold_kernel<false, false, true> : coh_fold_kernel<false, false, false>;
         hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, s, pt, n_pages, events, n_events, nf, fws,
-                           fpart, err, n_nodes, 0u);
+                           fpart, err, n_nodes);
       }
     }
     uint64_t g = (nf + 255) / 256;
