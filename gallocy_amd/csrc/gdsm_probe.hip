@@ -8,8 +8,8 @@
 //   measured in round 3 (scripts/dev/read_probe.hip "pages ppw4 inf1 nt", 6.63 TB/s at 16M pages).
 // copy: dst := src over whole pages (the twin step's traffic), the fastest of three shapes: a
 //   flat grid-stride 16-B copy (four loads per lane in flight before the four stores, 8
-//   workgroups per CU) and two page-shaped copies (a wave per page, one or two pages' loads in
-//   flight); written independently of the product's twin kernel.
+//   workgroups per CU) and two page-shaped grid-stride copies (a wave per page per step, its 4 x
+//   16 B per lane loaded before the stores; cached or nontemporal loads).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -68,32 +68,22 @@ __global__ __launch_bounds__(256) void probe_copy_kernel(u32x4p* __restrict__ ds
   for (; i < n16; i += stride) dst[i] = src[i];
 }
 
-// The twin step's shape, written independently: a wave per kPP pages in flight (each lane's
-// 4 x 16 B of every page loaded before any store), kPPW pages per wave.
-template <uint32_t kPP>
+// Page-shaped copies: a wave per page per step over a grid-stride loop (grid capped at 16384
+// workgroups), each lane's 4 x 16 B of the page loaded before any store; kNT: nontemporal loads.
+template <bool kNT>
 __global__ __launch_bounds__(256) void probe_copy_pages_kernel(u32x4p* __restrict__ dst,
                                                                const u32x4p* __restrict__ src,
                                                                uint64_t n) {
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wave) * kProbePPW;
-  for (uint32_t j = 0; j < kProbePPW; j += kPP) {
-    u32x4p v[kPP][4];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < n;
+       p += (uint64_t)gridDim.x * 4) {
+    u32x4p v[4];
 #pragma unroll
-    for (uint32_t q = 0; q < kPP; ++q) {
-      const uint64_t p = w0 + j + q;
-      if (p < n) {
+    for (int k = 0; k < 4; ++k)
+      v[k] = kNT ? __builtin_nontemporal_load(src + p * 256 + k * 64 + lane)
+                 : src[p * 256 + k * 64 + lane];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[q][k] = __builtin_nontemporal_load(src + p * 256 + k * 64 + lane);
-      }
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < kPP; ++q) {
-      const uint64_t p = w0 + j + q;
-      if (p < n) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dst[p * 256 + k * 64 + lane] = v[q][k];
-      }
-    }
+    for (int k = 0; k < 4; ++k) dst[p * 256 + k * 64 + lane] = v[k];
   }
 }
 
@@ -120,8 +110,8 @@ extern "C" int gdsm_probe_ceiling(gdsm_ctx* ctx, int kind, const void* a, const 
     (void)hipEventDestroy(e0);
     return -EIO;
   }
-  // the read takes one shape; the copy takes three (flat, page-shaped with one or two pages in
-  // flight per wave) and reports the fastest: the ceiling is the best copy this box does
+  // the read takes one shape; the copy takes three (flat; page-shaped with cached or nontemporal
+  // loads) and reports the fastest: the ceiling is the best copy this box does
   const int shapes = kind == GDSM_PROBE_READ ? 1 : 3;
   const uint64_t waves = (n_pages + gdsm::kProbePPW - 1) / gdsm::kProbePPW;
   const dim3 page_grid((unsigned)((waves + 3) / 4));
@@ -142,10 +132,12 @@ extern "C" int gdsm_probe_ceiling(gdsm_ctx* ctx, int kind, const void* a, const 
                              ctx->stream, static_cast<gdsm::u32x4p*>(dst),
                              static_cast<const gdsm::u32x4p*>(a), n_pages * 256);
         } else {
-          hipLaunchKernelGGL(sh == 1 ? gdsm::probe_copy_pages_kernel<1>
-                                     : gdsm::probe_copy_pages_kernel<2>,
-                             page_grid, dim3(256), 0, ctx->stream, static_cast<gdsm::u32x4p*>(dst),
-                             static_cast<const gdsm::u32x4p*>(a), n_pages);
+          const uint64_t g = std::min<uint64_t>((n_pages + 3) / 4, 16384);
+          hipLaunchKernelGGL(sh == 1 ? gdsm::probe_copy_pages_kernel<false>
+                                     : gdsm::probe_copy_pages_kernel<true>,
+                             dim3((unsigned)g), dim3(256), 0, ctx->stream,
+                             static_cast<gdsm::u32x4p*>(dst), static_cast<const gdsm::u32x4p*>(a),
+                             n_pages);
         }
         e = hipGetLastError();
       }
