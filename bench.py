@@ -84,10 +84,12 @@ def parse():
                          "per round); off = a twin launch before the round's writes (round 4)")
     ap.add_argument("--graph", action="store_true",
                     help="mmult: replay one HIP graph of every round instead of eager launches")
-    ap.add_argument("--driver", choices=["native", "native2", "python"], default="native",
+    ap.add_argument("--driver", choices=["native", "native2", "python", "device"],
+                    default="native",
                     help="mmult: rounds issued by the C++ loop over the C ABI "
                          "(gallocy_amd/native/replay.cpp; native2: two host threads, one per "
-                         "context) or from Python")
+                         "context), from Python, or on the device (gdsm_rounds: one persistent "
+                         "launch per context, barriers between the rounds' steps)")
     ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
     ap.add_argument("--coh-pages", type=int, default=16 << 20, help="coherence: pages")
     ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
@@ -848,6 +850,9 @@ def run_mmult(args):
                                          "eager, two streams, rounds issued by two C++ threads, one "
                                          "per context (gallocy_amd/native/replay.cpp)"
                                          if args.driver == "native2" else
+                                         "one persistent launch per stream for every round "
+                                         "(gdsm_rounds), device-wide barriers between a round's "
+                                         "steps" if args.driver == "device" else
                                          "eager, two streams, rounds issued from Python"),
            "python_rounds": other,
            "round": ("coherence batch | the round's row writes (one batched copy), the release "

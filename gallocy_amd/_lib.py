@@ -61,6 +61,8 @@ SIGNATURES = {
     "gdsm_graph_destroy": (C.c_int, [vp]),
     "gdsm_prof_enable": (C.c_int, [vp, C.c_int]),
     "gdsm_prof_read": (C.c_int, [vp, C.POINTER(C.c_double), u64p]),
+    "gdsm_rounds": (C.c_int, [vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "gdsm_rounds": (C.c_int, [vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "gdsm_probe_ceiling": (C.c_int, [vp, C.c_int, vp, vp, vp, C.c_uint64, C.c_int,
                                      C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "gdsm_gen_pages": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,

@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -118,6 +119,7 @@ int check_and_clear_err(gdsm_ctx* ctx) {
   // a fixed-budget exchange stream over its budget, and nothing else: the release can be redone
   // with exact sizes (gdsm.h GDSM_XCHG_FIXED)
   if (h == kErrOverBudget) return -EOVERFLOW;
+  if (h & gdsm::kErrRoundsBarrier) return -ETIMEDOUT;  // gdsm_rounds: a grid barrier gave up
   return h ? -EINVAL : 0;
 }
 
@@ -259,6 +261,7 @@ int gdsm_fini(gdsm_ctx* ctx) {
   if (ctx->chain.ws) (void)hipFree(ctx->chain.ws);
   if (ctx->coh_chain.ws) (void)hipFree(ctx->coh_chain.ws);
   if (ctx->coh_ws) (void)hipFree(ctx->coh_ws);
+  if (ctx->rounds_ws) (void)hipFree(ctx->rounds_ws);
   if (ctx->coh_pt) (void)hipFree(ctx->coh_pt);
   if (ctx->coh_totals) (void)hipFree(ctx->coh_totals);
   if (ctx->track_dev) (void)hipFree(ctx->track_dev);
@@ -835,6 +838,96 @@ int gdsm_coherence_batch_async(gdsm_ctx* ctx, const uint64_t* events, uint64_t n
   GDSM_TRY(gdsm::launch_coherence(ctx->coh_pt, ctx->n_pages, ctx->n_nodes, events, n_events,
                                   totals_dev, ctx->coh_ws, ctx->coh_ws_bytes, ctx->err,
                                   ctx->stream, ctx->P(), chain));
+  return 0;
+}
+
+// ---- DSM rounds on the device ----------------------------------------------------------------
+namespace {
+// offsets (host, n + 1) checked: non-decreasing from 0; the largest step
+bool check_offsets(const int64_t* off, uint32_t n, uint64_t* max_step) {
+  if (!off || off[0] != 0) return false;
+  uint64_t m = 0;
+  for (uint32_t r = 0; r < n; ++r) {
+    if (off[r + 1] < off[r]) return false;
+    m = std::max<uint64_t>(m, (uint64_t)(off[r + 1] - off[r]));
+  }
+  *max_step = m;
+  return true;
+}
+
+// The largest grid of 256-thread workgroups of `kern` that is resident at once (0 on failure).
+uint64_t resident_grid(const void* kern) {
+  int dev = 0, ncu = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess)
+    return 0;
+  return (uint64_t)std::max(ncu, 0) * (uint64_t)std::max(occ, 0);
+}
+}  // namespace
+
+int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t* events,
+                const int64_t* ev_off, uint64_t* totals, const uint32_t* ids,
+                const uint32_t* home, const int64_t* id_off, const uint64_t* desc,
+                const int64_t* desc_off, gdsm_runs* runs) {
+  if (!data || !pt || data == pt || data->device != pt->device || !runs || !runs->rec_off ||
+      (!runs->data && runs->cap))
+    return -EINVAL;
+  if (!data->arena[GDSM_TWIN] || !data->arena[GDSM_CURRENT] || !data->arena[GDSM_REPLICA] ||
+      !pt->coh_pt || !data->chain.ws || !pt->coh_chain.ws)
+    return -EINVAL;
+  uint64_t max_ev = 0, max_ids = 0, max_desc = 0;
+  if (!check_offsets(ev_off, n_rounds, &max_ev) || !check_offsets(id_off, n_rounds, &max_ids) ||
+      !check_offsets(desc_off, n_rounds, &max_desc))
+    return -EINVAL;
+  if ((ev_off[n_rounds] && !events) || (id_off[n_rounds] && (!ids || !home)) ||
+      (desc_off[n_rounds] && !desc) || (n_rounds && !totals))
+    return -EINVAL;
+  // a round's pages: one look-back granule each; its events: the streaming fold's spans
+  if (max_ids > gdsm::kDiffChainUnits || max_ev > (1u << 20)) return -EINVAL;
+  if (runs->n_cap ? max_ids > runs->n_cap : (runs->owned && max_ids > runs->n)) return -EINVAL;
+  if (n_rounds == 0) return 0;
+  if (recording(data) || recording(pt)) return -EBUSY;  // (epochs per launch: not replayable)
+  CtxGuard gd(data);
+  if (gd.rc) return gd.rc;
+  CtxGuard gp(pt);
+  if (gp.rc) return gp.rc;
+  // the offsets on the device (behind them the grid-barrier word, 256-B aligned)
+  const uint64_t ob = 8ull * (n_rounds + 1);
+  const uint64_t bar_at = (2 * ob + 255) & ~255ull;
+  int rc = ensure(data, &data->rounds_ws, &data->rounds_ws_bytes, bar_at + 256);
+  if (!rc) rc = ensure(pt, &pt->rounds_ws, &pt->rounds_ws_bytes, bar_at + 256);
+  if (rc) return rc;
+  GDSM_TRY(hipMemcpyAsync(data->rounds_ws, id_off, ob, hipMemcpyHostToDevice, data->stream));
+  GDSM_TRY(hipMemcpyAsync(data->rounds_ws + ob, desc_off, ob, hipMemcpyHostToDevice, data->stream));
+  GDSM_TRY(hipMemcpyAsync(pt->rounds_ws, ev_off, ob, hipMemcpyHostToDevice, pt->stream));
+  // grids: a workgroup per page or copy of the largest round (data), a wave per 256-event span of
+  // the largest round (page table); both far below what is resident at once, which the barriers
+  // need (checked)
+  const uint64_t gd_n = std::min<uint64_t>(std::max<uint64_t>({max_ids, max_desc, 1}), 256);
+  const uint64_t gp_n = std::min<uint64_t>(std::max<uint64_t>((max_ev + 1023) / 1024, 1), 256);
+  if (gd_n > resident_grid(gdsm::rounds_data_kernel_ptr()) ||
+      gp_n > resident_grid(gdsm::rounds_fold_kernel_ptr()))
+    return -EINVAL;
+  gdsm::DiffChain& ch = data->chain;
+  if (ch.epoch == 0 || ch.epoch + n_rounds >= (1u << 30)) {
+    GDSM_TRY(hipMemsetAsync(ch.ws, 0, gdsm::diff_chain_bytes(), data->stream));
+    ch.epoch = 1;
+  }
+  const uint32_t epoch0 = ch.epoch;
+  ch.epoch = 0;  // the next chained release zeroes the workspace again (its ticket sets restart)
+  GDSM_TRY(gdsm::launch_rounds_fold(
+      pt->coh_pt, pt->n_pages, pt->n_nodes, events,
+      reinterpret_cast<const int64_t*>(pt->rounds_ws), n_rounds, (uint32_t)gp_n, totals, pt->err,
+      &pt->coh_chain, reinterpret_cast<uint32_t*>(pt->rounds_ws + bar_at), pt->stream, pt->P()));
+  runs->n = (uint64_t)(id_off[n_rounds] - id_off[n_rounds - 1]);
+  GDSM_TRY(gdsm::launch_rounds_data(
+      data->arena[GDSM_TWIN], data->arena[GDSM_CURRENT], ids, home,
+      reinterpret_cast<const int64_t*>(data->rounds_ws), desc,
+      reinterpret_cast<const int64_t*>(data->rounds_ws + ob), n_rounds, (uint32_t)gd_n,
+      runs->rec_off, runs->data, runs->cap, ch.ws, data->arena[GDSM_REPLICA], data->n_pages,
+      data->err, epoch0, reinterpret_cast<uint32_t*>(data->rounds_ws + bar_at), data->stream,
+      data->P()));
   return 0;
 }
 

@@ -758,7 +758,10 @@ struct CohChain {
   uint32_t epoch;    // 1 .. 2^29 - 1
   uint32_t* flag;    // == epoch once the caller's totals are zeroed
 };
-template <uint32_t kSC, bool kFull, bool kChain = false>
+// kWT (gdsm_rounds' persistent grid): page-table words stored write-through and gathered past
+// L1 (st_wt / ld_wt), since the next round's waves on other XCDs read them after a fence-free
+// barrier.
+template <uint32_t kSC, bool kFull, bool kChain = false, bool kWT = false>
 __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                 const uint64_t* __restrict__ ev, uint64_t n,
                                                 uint64_t b, uint64_t* __restrict__ status,
@@ -808,7 +811,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
                    ((xl_ >> 1) & 7u) >= n_nodes)) ? 1u : 0u;                         \
     Hg[gslot_] = __ballot(h_);                                                       \
     uint64_t w_ = 0;                                                                 \
-    if (h_ && p_ < n_pages) w_ = pt[p_];                                             \
+    if (h_ && p_ < n_pages) w_ = kWT ? ld_wt(pt + p_) : pt[p_];                      \
     Wg[gslot_] = w_;                                                                 \
     pprev = (uint32_t)__builtin_amdgcn_readlane((int)p_, 63);                        \
   } while (0)
@@ -846,7 +849,8 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       if (c > 0 && (Hd & 1ull)) {
         if (open_local) {
           if (lane == 0 && open_page < n_pages)
-            pt[open_page] = (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32);
+            st_<kWT>(pt + open_page,
+                     (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32));
         } else {
           has_d = true;
           d_state = carry;
@@ -903,8 +907,8 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
         const uint32_t f0 = (uint32_t)__shfl((int)(uint32_t)(W >> 32), (int)h, 64);
         const uint32_t pg = xl >> 4;
         if (end && pg < n_pages && (inchunk || open_local))
-          pt[pg] = (uint64_t)s_state(incl) |
-                   ((uint64_t)(inchunk ? f0 + cnt : open_f0 + open_cnt + cnt) << 32);
+          st_<kWT>(pt + pg, (uint64_t)s_state(incl) |
+                                ((uint64_t)(inchunk ? f0 + cnt : open_f0 + open_cnt + cnt) << 32));
         if (!open_local) {
           const uint64_t dm = __ballot(end && !inchunk);
           if (dm) {  // the span's first segment ends here (lowest end lane)
@@ -942,7 +946,8 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   if (next_head) {
     if (open_local) {
       if (lane == 0 && last_page < n_pages)
-        pt[last_page] = (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32);
+        st_<kWT>(pt + last_page,
+                 (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32));
     } else {
       has_d = true;
       d_state = carry;
@@ -1025,7 +1030,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       const uint32_t word = (d_state & kSF) ? s_state(d_state) : (tcompose(cur, (d_state >> 20) & 0xFFu) & 0x7FFFFu);
       if (lane == 0 && d_page < n_pages) {
         uint32_t* pst = reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)d_page;
-        pst[0] = word;
+        st_<kWT>(pst, word);
         const uint32_t c = d_cnt + dfc;
         if (c) atomicAdd(pst + 1, c);
       }
@@ -1038,7 +1043,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
     // no prefix (the span starts a page): the first segment was counted exactly
     if (has_d && lane == 0 && d_page < n_pages) {
       uint32_t* pst = reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)d_page;
-      pst[0] = s_state(d_state);
+      st_<kWT>(pst, s_state(d_state));
       if (d_cnt) atomicAdd(pst + 1, d_cnt);
     }
   }
@@ -1060,7 +1065,12 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   if (kChain) {  // the caller's totals are zeroed for this launch once the flag holds its epoch
     while (__hip_atomic_load(ch.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ch.epoch)
       __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // (kWT: the zeroes were stored write-through and drained before the flag, and the adds below
+    // are atomics: no acquire)
+    if (kWT)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    else
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   if (totals) {
     if (lane < 10 && mine) atomicAdd(totals + lane, (unsigned long long)mine);
@@ -1116,6 +1126,79 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
   else
     coh_stream_wave<kSC, false, kChain>(pt, n_pages, ev, n, b, status, partial, err, n_nodes,
                                         totals, ch);
+}
+
+// ---- DSM rounds on the device (gdsm_rounds, page-table side): one persistent launch folds
+// every round's events in turn, a grid barrier between rounds (round r + 1 reads the words round
+// r stored). Round r = events [eoff[r], eoff[r+1]), spans of 256 (coh_stream_wave, chained form:
+// granules and the totals flag tagged with epoch epoch0 + r in CohChainState's ws), span s on
+// wave s mod (4 x gridDim.x), each wave's spans in ascending order, so a look-back only waits
+// for running waves. Totals: row r of `totals` (10 u64), zeroed by span 0's wave. The page-table
+// words one round hands the next are stored write-through and gathered past L1 (kWT), so the
+// barrier between rounds needs no fence.
+__global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__ pt,
+                                                          uint64_t n_pages,
+                                                          const uint64_t* __restrict__ ev,
+                                                          const int64_t* __restrict__ eoff,
+                                                          uint32_t n_rounds,
+                                                          uint64_t* __restrict__ ws,
+                                                          uint32_t* __restrict__ err,
+                                                          uint32_t n_nodes,
+                                                          unsigned long long* __restrict__ totals,
+                                                          uint32_t epoch0,
+                                                          uint32_t* __restrict__ bar) {
+  constexpr uint64_t kSpan = 64ull * kSCSmall;
+  const uint64_t nw = (uint64_t)gridDim.x * 4, wv = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t* const status = ws + kCohChainStatus;
+  uint32_t* const flag = reinterpret_cast<uint32_t*>(ws + kCohChainFlag);
+  for (uint32_t r = 0; r < n_rounds; ++r) {
+    const uint64_t e0 = (uint64_t)eoff[r], n = (uint64_t)eoff[r + 1] - e0;
+    const uint64_t nb = (n + kSpan - 1) / kSpan, nfull = n / kSpan;
+    const CohChain ch{epoch0 + r, flag};
+    unsigned long long* const tot = totals + 10ull * r;
+    for (uint64_t b = wv; b < nb; b += nw) {
+      if (b == 0) {  // span 0's wave: the round's totals zeroed (drained), then the flag raised
+        if (lane < 10) st_wt(tot + lane, 0ull);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(flag, ch.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (b < nfull)
+        coh_stream_wave<kSCSmall, true, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
+                                                    err, n_nodes, tot, ch);
+      else
+        coh_stream_wave<kSCSmall, false, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
+                                                     err, n_nodes, tot, ch);
+    }
+    if (n == 0 && wv == 0 && lane < 10) st_wt(tot + lane, 0ull);
+    grid_barrier_wt(bar, (r + 1) * gridDim.x, err, kErrRoundsBarrier);
+  }
+}
+
+const void* rounds_fold_kernel_ptr() { return reinterpret_cast<const void*>(rounds_fold_kernel); }
+
+hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
+                              const uint64_t* events, const int64_t* eoff, uint32_t n_rounds,
+                              uint32_t grid, uint64_t* totals, uint32_t* err, CohChainState* chain,
+                              uint32_t* bar, hipStream_t s, Prof* prof) {
+  if (n_rounds == 0) return hipSuccess;
+  if (!chain || !chain->ws) return hipErrorInvalidValue;
+  // the rounds take epochs [epoch0, epoch0 + n_rounds); the chain is zeroed again afterwards by
+  // its next launch (its ticket sets are not kept in step here)
+  if (chain->epoch == 0 || chain->epoch + n_rounds >= (1u << 29)) {
+    const hipError_t e = hipMemsetAsync(chain->ws, 0, coh_chain_bytes(), s);
+    if (e != hipSuccess) return e;
+    chain->epoch = 1;
+  }
+  const uint32_t epoch0 = chain->epoch;
+  chain->epoch = 0;
+  hipError_t e = hipMemsetAsync(bar, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
+  hipLaunchKernelGGL(rounds_fold_kernel, dim3(grid), dim3(256), 0, s, pt, n_pages, events, eoff,
+                     n_rounds, chain->ws, err, n_nodes,
+                     reinterpret_cast<unsigned long long*>(totals), epoch0, bar);
+  return hipGetLastError();
 }
 
 // The small-batch path's zeroing (batch totals and the tickets + status granules) in one launch.

@@ -18,6 +18,39 @@ __device__ __forceinline__ uint4 ld_nt16(const void* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// ---- write-through access for hand-offs inside one launch (gdsm_rounds' persistent grids):
+// stores `sc1` (written through to memory, so another XCD's reader needs no release fence from
+// the writer) and loads `sc1` (past this CU's L1, so the reader needs no acquire), both as
+// agent-scope relaxed atomics, which gfx950 lowers to plain global_store / global_load with sc1
+// (MI355X_MICROARCH.md, inter-workgroup visibility: valid forms). 16 B = two 8-B accesses.
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt16(void* p, const uint4& v) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+  st_wt(q, (uint64_t)v.x | ((uint64_t)v.y << 32));
+  st_wt(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32));
+}
+__device__ __forceinline__ uint4 ld_wt16(const void* p) {
+  uint64_t* q = const_cast<uint64_t*>(reinterpret_cast<const uint64_t*>(p));
+  const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+template <typename T>
+__device__ __forceinline__ T ld_wt(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a store, write-through when kWT
+template <bool kWT, typename T>
+__device__ __forceinline__ void st_(T* p, T v) {
+  if (kWT)
+    st_wt(p, v);
+  else
+    *p = v;
+}
+
 // ---- wave64 cross-lane primitives on DPP (VALU, no LDS traffic) -------------------------
 // gfx9-family DPP controls: row_shr:n = 0x110+n, row_bcast:15 = 0x142, row_bcast:31 = 0x143,
 // wave_shl:1 = 0x130, wave_shr:1 = 0x138. Lanes whose source is out of range (or whose row is
@@ -124,6 +157,59 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A barrier of a persistent grid (every workgroup resident): `bar` counts arrivals across the
+// whole launch (zeroed before it), the k-th barrier (1-based) waits for k x gridDim.x of them.
+// Agent-scope release before the arrival and acquire after the wait, so what one workgroup
+// stored before the barrier is what another reads after it. A wait that never ends (a
+// workgroup not resident: never expected, the launcher sizes the grid below the occupancy) sets
+// `err_bit` in *err and lets the workgroup go on, so the grid always drains.
+__device__ __forceinline__ void grid_barrier(uint32_t* __restrict__ bar, uint32_t target,
+                                             uint32_t* __restrict__ err, uint32_t err_bit) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      // (a barrier that already gave up anywhere: no more waiting, the grid drains)
+      if ((++spins & 1023u) == 0 &&
+          (spins > (1u << 22) ||
+           (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & err_bit))) {
+        atomicOr(err, err_bit);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// The same barrier for grids whose hand-offs are all write-through (st_wt / ld_wt above): no
+// release or acquire fence (their L2 write-back and L1 invalidate cost ~1.7 us each); every wave
+// drains its stores (vmcnt(0)) before the workgroup's arrival, and the arrival counter is an
+// agent atomic polled by sc1 loads.
+__device__ __forceinline__ void grid_barrier_wt(uint32_t* __restrict__ bar, uint32_t target,
+                                                uint32_t* __restrict__ err, uint32_t err_bit) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 1023u) == 0 &&
+          (spins > (1u << 22) ||
+           (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & err_bit))) {
+        atomicOr(err, err_bit);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps loads below)
+  __syncthreads();
 }
 
 // SPEC §6 mixers (must match oracle/gdsm_oracle.c bit for bit).

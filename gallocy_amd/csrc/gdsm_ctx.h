@@ -30,6 +30,9 @@ struct gdsm_ctx {
   uint64_t* coh_totals = nullptr;  // device 10 x u64
   gdsm::CohChainState coh_chain;   // small batches without a zeroing launch (allocated by gdsm_init)
   uint32_t n_nodes = 0;
+  // gdsm_rounds: the rounds' offset arrays on the device and the grid-barrier word
+  uint8_t* rounds_ws = nullptr;
+  uint64_t rounds_ws_bytes = 0;
   uint32_t diff_bpp = 0;         // stream bytes per page the host last learned (diff geometry)
   std::set<void*> allocs;        // gdsm_dev_alloc / gdsm_runs_alloc blocks
   // gdsm_apply_async: applies run on `aux`, ordered after everything enqueued on `stream` before
@@ -81,6 +84,7 @@ constexpr uint32_t kErrNw = 4;           // GPU NW input out of range
 constexpr uint32_t kErrIds = 8;          // page id / index out of range
 constexpr uint32_t kErrStream = 16;      // exchanged stream with malformed offsets
 constexpr uint32_t kErrOverBudget = 32;  // fixed-budget exchanged stream over its budget
+static_assert(gdsm::kErrRoundsBarrier == 64, "gdsm_rounds: a barrier that never completed");
 
 int map_err(hipError_t e);
 // ctx->stream is being recorded into a graph (gdsm_capture_* or a caller's own capture of it).

@@ -256,6 +256,7 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, uint32_t b) {
 // start is the last run start at or before its end: inside this chunk, or `ps` - 1 where `ps` is
 // the exclusive prefix maximum of (last start + 1) over the earlier chunks. (Called once per k
 // with scalars, so no per-thread array is ever indexed at run time.)
+template <bool kWT = false>
 __device__ __forceinline__ void emit_chunk(uint32_t ch, uint32_t s, uint32_t e, uint32_t m,
                                            uint32_t ps, uint32_t excl, const uint4 c,
                                            uint32_t* __restrict__ hdr, uint8_t* __restrict__ pay) {
@@ -266,13 +267,13 @@ __device__ __forceinline__ void emit_chunk(uint32_t ch, uint32_t s, uint32_t e, 
     e &= e - 1;
     const uint32_t upto = s & ((2u << b) - 1u);
     const uint32_t start = upto ? pos + 31u - (uint32_t)__builtin_clz(upto) : ps - 1u;
-    hdr[r++] = start | ((pos + b - start + 1u) << 16);
+    st_<kWT>(hdr + r++, start | ((pos + b - start + 1u) << 16));
   }
   uint32_t q = excl >> 16;
   while (m) {
     const uint32_t b = (uint32_t)__builtin_ctz(m);
     m &= m - 1;
-    pay[q++] = (uint8_t)byte_of(c, b);
+    st_<kWT>(pay + q++, (uint8_t)byte_of(c, b));
   }
 }
 
@@ -432,10 +433,14 @@ __device__ __forceinline__ uint32_t record_size_masks(const uint32_t (&m)[4], ui
 
 // The bytes of a 16-B chunk selected by `m` (bit j = byte j), stored from registers: one 16-B
 // store for a whole chunk, 8-B stores for whole halves, dword stores for whole dwords, else bytes.
+template <bool kWT = false>
 __device__ __forceinline__ void store_masked16(uint8_t* __restrict__ dst, uint32_t m,
                                                const uint4& c) {
   if (m == 0xFFFFu) {
-    *reinterpret_cast<uint4*>(dst) = c;
+    if (kWT)
+      st_wt16(dst, c);
+    else
+      *reinterpret_cast<uint4*>(dst) = c;
     return;
   }
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -443,7 +448,10 @@ __device__ __forceinline__ void store_masked16(uint8_t* __restrict__ dst, uint32
   for (int h = 0; h < 2; ++h) {
     const uint32_t lo = h ? c.z : c.x, hi = h ? c.w : c.y;
     if (((m >> (8 * h)) & 0xFFu) == 0xFFu) {
-      *reinterpret_cast<u32x2*>(dst + 8 * h) = (u32x2){lo, hi};
+      if (kWT)
+        st_wt(reinterpret_cast<uint64_t*>(dst + 8 * h), (uint64_t)lo | ((uint64_t)hi << 32));
+      else
+        *reinterpret_cast<u32x2*>(dst + 8 * h) = (u32x2){lo, hi};
       continue;
     }
 #pragma unroll
@@ -451,11 +459,11 @@ __device__ __forceinline__ void store_masked16(uint8_t* __restrict__ dst, uint32
       const uint32_t wv = d ? hi : lo, nib = (m >> (8 * h + 4 * d)) & 0xFu;
       uint8_t* q = dst + 8 * h + 4 * d;
       if (nib == 0xFu) {
-        *reinterpret_cast<uint32_t*>(q) = wv;
+        st_<kWT>(reinterpret_cast<uint32_t*>(q), wv);
       } else if (nib) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if ((nib >> k) & 1u) q[k] = (uint8_t)(wv >> (8 * k));
+          if ((nib >> k) & 1u) st_<kWT>(q + k, (uint8_t)(wv >> (8 * k)));
       }
     }
   }
@@ -841,41 +849,42 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
 // next launch's counter zeroed). Records are written straight from the registers (run headers
 // and payload bytes, emit_chunk), the home copy's changed bytes with store_masked16, the twin's
 // dirty chunks whole (kRetwin). Same stream, apply and re-twin as every other diff form.
-template <bool kApply, bool kRetwin>
-__global__ __launch_bounds__(256) void release_page_kernel(
-    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
-    const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
-    uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard g) {
+// One page (list entry u of n) by the calling four-wave workgroup; the kernel below draws u as a
+// ticket, rounds_data_kernel assigns it (every workgroup resident, pages in ascending order per
+// workgroup, so the look-back only ever waits for running workgroups).
+// kWT: every store write-through and the page loads past L1 (st_wt / ld_wt16): the persistent
+// rounds grid hands CURRENT, TWIN, REPLICA and the stream from one workgroup to another with no
+// fences.
+template <bool kApply, bool kRetwin, bool kWT = false>
+__device__ __forceinline__ void release_page_wg(
+    const uint64_t u, const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, const DiffSplit& sp, uint64_t* __restrict__ ws,
+    uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard& g) {
   uint8_t* const twin_w = const_cast<uint8_t*>(twin);  // (kRetwin: see diff_single_kernel)
   __shared__ uint32_t edge_first[4], edge_last[4], tot[4], lastst[4];
-  __shared__ uint32_t ticket;
   __shared__ uint64_t rec_at;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t E = sp.epoch;
   const uint64_t tag = (uint64_t)E << 32;
-  uint32_t* const ctr = reinterpret_cast<uint32_t*>(ws);
-  if (threadIdx.x == 0) {
-    ticket = atomicAdd(ctr + (E & 1u), 1u);
-    if (blockIdx.x == 0)
-      __hip_atomic_store(ctr + ((E + 1u) & 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const uint64_t u = ticket;  // one page per workgroup (one stream: first[0] = 0)
   const uint64_t n = sp.first[1] - sp.first[0];
-  if (u >= n) return;  // workgroup-uniform
   uint32_t bad = 0;
   const uint64_t i = sp.first[0] + u;
   const uint64_t pj = ids ? (g.ids ? guarded_id(ids, i, g.n_pages, bad) : ids[i]) : i;
   const uint64_t cap = sp.cap[0];
   const bool ample = kRetwin && cap >= n * GDSM_MAX_RECORD;
   const uint32_t ch = w * 64 + lane;  // this lane's chunk of the page
-  const uint4 t = ld_nt16(twin + pj * kPage + ch * 16u);
-  const uint4 c = ld_nt16(cur + pj * kPage + ch * 16u);
+  const uint4 t = kWT ? ld_wt16(twin + pj * kPage + ch * 16u) : ld_nt16(twin + pj * kPage + ch * 16u);
+  const uint4 c = kWT ? ld_wt16(cur + pj * kPage + ch * 16u) : ld_nt16(cur + pj * kPage + ch * 16u);
   const uint32_t m = diffmask16(t, c);
   const uint64_t pt = kApply ? (tids ? (g.tids ? guarded_id(tids, i, g.n_pages, bad) : tids[i]) : pj)
                              : 0;  // page at target
-  if (kApply && m) store_masked16(target + pt * kPage + ch * 16u, m, c);
-  if (ample && m && twin_ok(g, pj)) *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
+  if (kApply && m) store_masked16<kWT>(target + pt * kPage + ch * 16u, m, c);
+  if (ample && m && twin_ok(g, pj)) {
+    if (kWT)
+      st_wt16(twin_w + pj * kPage + ch * 16u, c);
+    else
+      *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
+  }
   if (lane == 0) edge_first[w] = m;
   if (lane == 63) edge_last[w] = m;
   __syncthreads();
@@ -939,8 +948,8 @@ __global__ __launch_bounds__(256) void release_page_kernel(
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) {
-      sp.rec_off[0][u + 1] = excl + size;
-      if (u == 0) sp.rec_off[0][0] = 0;
+      st_<kWT>(sp.rec_off[0] + u + 1, (uint64_t)(excl + size));
+      if (u == 0) st_<kWT>(sp.rec_off[0], (uint64_t)0);
       rec_at = excl;
     }
   }
@@ -950,14 +959,37 @@ __global__ __launch_bounds__(256) void release_page_kernel(
   if (size) {
     uint8_t* rec = sp.data[0] + at;
     if (threadIdx.x == 0) {
-      *reinterpret_cast<uint32_t*>(rec) = NR;
-      for (uint32_t q = NP; q & 3u; ++q) rec[4 + 4 * NR + q] = 0;
+      st_<kWT>(reinterpret_cast<uint32_t*>(rec), NR);
+      for (uint32_t q = NP; q & 3u; ++q) st_<kWT>(rec + 4 + 4 * NR + q, (uint8_t)0);
     }
-    emit_chunk(ch, st, en, m, max(cmax, from_prev_lane(mx)), carry + inc - v, c,
+    emit_chunk<kWT>(ch, st, en, m, max(cmax, from_prev_lane(mx)), carry + inc - v, c,
                reinterpret_cast<uint32_t*>(rec + 4), rec + 4 + 4 * NR);
   }
-  if (kRetwin && !ample && m && twin_ok(g, pj))
-    *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
+  if (kRetwin && !ample && m && twin_ok(g, pj)) {
+    if (kWT)
+      st_wt16(twin_w + pj * kPage + ch * 16u, c);
+    else
+      *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
+  }
+}
+
+template <bool kApply, bool kRetwin>
+__global__ __launch_bounds__(256) void release_page_kernel(
+    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, const DiffSplit sp, uint64_t* __restrict__ ws,
+    uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard g) {
+  __shared__ uint32_t ticket;
+  const uint32_t E = sp.epoch;
+  uint32_t* const ctr = reinterpret_cast<uint32_t*>(ws);
+  if (threadIdx.x == 0) {
+    ticket = atomicAdd(ctr + (E & 1u), 1u);
+    if (blockIdx.x == 0)
+      __hip_atomic_store(ctr + ((E + 1u) & 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint64_t u = ticket;  // one page per workgroup (one stream: first[0] = 0)
+  if (u >= sp.first[1] - sp.first[0]) return;  // workgroup-uniform
+  release_page_wg<kApply, kRetwin>(u, twin, cur, ids, sp, ws, target, tids, g);
 }
 
 // ------------------------------------------------------------------------- apply (SPEC §4)
@@ -1740,50 +1772,128 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
 
 // A workgroup copies n words of T, four per lane in flight before their stores (a load-store
 // pair per step would wait out one memory latency per step).
-template <typename T>
+template <bool kWT, typename T>
+__device__ __forceinline__ void st_word(T* p, const T& v) {
+  if constexpr (sizeof(T) == 16) {
+    if (kWT)
+      st_wt16(p, v);
+    else
+      *p = v;
+  } else {
+    st_<kWT>(p, v);
+  }
+}
+template <typename T, bool kWT = false>
 __device__ __forceinline__ void copy_words(T* __restrict__ d, const T* __restrict__ s,
                                            uint64_t n) {
   const uint64_t st = blockDim.x;
   uint64_t i = threadIdx.x;
   for (; i + 3 * st < n; i += 4 * st) {
     const T a = s[i], b = s[i + st], c = s[i + 2 * st], e = s[i + 3 * st];
-    d[i] = a;
-    d[i + st] = b;
-    d[i + 2 * st] = c;
-    d[i + 3 * st] = e;
+    st_word<kWT>(d + i, a);
+    st_word<kWT>(d + i + st, b);
+    st_word<kWT>(d + i + 2 * st, c);
+    st_word<kWT>(d + i + 3 * st, e);
   }
-  for (; i < n; i += st) d[i] = s[i];
+  for (; i < n; i += st) st_word<kWT>(d + i, s[i]);
 }
 
-// n device-to-device copies in one launch (gdsm_memcpy_batch): copy i = desc[3i .. 3i+2] =
-// (dst, src, bytes), one workgroup per copy, in the widest words (16, 8, 4 or 1 B) that dst and
-// src are both aligned to, the remainder bytes after them. (Config 5's rows are 8-B aligned:
-// copied byte by byte they took 13-16 us of a ~45 us round.)
-__global__ __launch_bounds__(256) void copy_batch_kernel(const uint64_t* __restrict__ desc,
-                                                         uint64_t n) {
-  for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
-    uint8_t* dst = reinterpret_cast<uint8_t*>(desc[3 * i]);
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(desc[3 * i + 1]);
-    const uint64_t bytes = desc[3 * i + 2];
+// One (dst, src, bytes) copy by the calling workgroup, in the widest words (16, 8, 4 or 1 B)
+// that dst and src are both aligned to, the remainder bytes after them. (Config 5's rows are 8-B
+// aligned: copied byte by byte they took 13-16 us of a ~45 us round.)
+// kWT: write-through stores (the persistent rounds grid: the release of another workgroup reads
+// the bytes after a fence-free barrier). The sources are never written in the launch.
+template <bool kWT = false>
+__device__ __forceinline__ void copy_desc_wg(const uint64_t* __restrict__ d) {
+  {
+    uint8_t* dst = reinterpret_cast<uint8_t*>(d[0]);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(d[1]);
+    const uint64_t bytes = d[2];
     const uintptr_t al = (uintptr_t)dst | (uintptr_t)src;
     uint64_t done;
     if (!(al & 15u)) {
-      copy_words(reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), bytes / 16);
+      copy_words<uint4, kWT>(reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src),
+                             bytes / 16);
       done = bytes & ~15ull;
     } else if (!(al & 7u)) {
-      copy_words(reinterpret_cast<uint64_t*>(dst), reinterpret_cast<const uint64_t*>(src),
-                 bytes / 8);
+      copy_words<uint64_t, kWT>(reinterpret_cast<uint64_t*>(dst),
+                                reinterpret_cast<const uint64_t*>(src), bytes / 8);
       done = bytes & ~7ull;
     } else if (!(al & 3u)) {
-      copy_words(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src),
-                 bytes / 4);
+      copy_words<uint32_t, kWT>(reinterpret_cast<uint32_t*>(dst),
+                                reinterpret_cast<const uint32_t*>(src), bytes / 4);
       done = bytes & ~3ull;
     } else {
-      copy_words(dst, src, bytes);
+      copy_words<uint8_t, kWT>(dst, src, bytes);
       done = bytes;
     }
-    for (uint64_t b = done + threadIdx.x; b < bytes; b += blockDim.x) dst[b] = src[b];
+    for (uint64_t b = done + threadIdx.x; b < bytes; b += blockDim.x) st_<kWT>(dst + b, src[b]);
   }
+}
+
+// n device-to-device copies in one launch (gdsm_memcpy_batch): copy i = desc[3i .. 3i+2] =
+// (dst, src, bytes), one workgroup per copy.
+__global__ __launch_bounds__(256) void copy_batch_kernel(const uint64_t* __restrict__ desc,
+                                                         uint64_t n) {
+  for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) copy_desc_wg(desc + 3 * i);
+}
+
+// ---- DSM rounds on the device (gdsm_rounds, page-data side): one persistent launch runs every
+// round's row writes (the application's stores, as copy descriptors) and its release (diff of the
+// written pages + home apply + re-twin, release_page_wg), with grid barriers where separate
+// launches had their boundaries: copies | barrier | release | barrier. Round r's pages are list
+// entries [off[r], off[r+1]) of ids / tids (r's records land in the one stream sp describes, as
+// a release of those pages would write them), its copies descriptors [doff[r], doff[r+1]).
+// Look-back granules carry epoch epoch0 + r (DiffChain's ws and layout; the launcher leaves the
+// chain to be zeroed again by its next chained launch). Every byte one workgroup hands another
+// (CURRENT rows, TWIN, REPLICA, the stream) is stored write-through and the pages are loaded past
+// L1 (kWT), so the barriers need no L2 write-back or L1 invalidate.
+__global__ __launch_bounds__(256) void rounds_data_kernel(
+    const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
+    const uint32_t* __restrict__ ids, const uint32_t* __restrict__ tids,
+    const int64_t* __restrict__ off, const uint64_t* __restrict__ desc,
+    const int64_t* __restrict__ doff, uint32_t n_rounds, DiffSplit sp, uint64_t* __restrict__ ws,
+    uint8_t* __restrict__ target, IdGuard g, uint32_t epoch0, uint32_t* __restrict__ bar) {
+  uint32_t phase = 0;
+  for (uint32_t r = 0; r < n_rounds; ++r) {
+    const uint64_t d0 = (uint64_t)doff[r], d1 = (uint64_t)doff[r + 1];
+    for (uint64_t i = d0 + blockIdx.x; i < d1; i += gridDim.x) copy_desc_wg<true>(desc + 3 * i);
+    grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
+    const uint64_t a = (uint64_t)off[r], n = (uint64_t)off[r + 1] - a;
+    DiffSplit rs = sp;
+    rs.first[0] = 0;
+    rs.first[1] = n;
+    rs.epoch = epoch0 + r;
+    for (uint64_t u = blockIdx.x; u < n; u += gridDim.x) {
+      release_page_wg<true, true, true>(u, twin, cur, ids + a, rs, ws, target, tids + a, g);
+      __syncthreads();  // (the page's LDS exchange is reused by the workgroup's next page)
+    }
+    if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) st_wt(rs.rec_off[0], (uint64_t)0);
+    grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
+  }
+}
+
+const void* rounds_data_kernel_ptr() { return reinterpret_cast<const void*>(rounds_data_kernel); }
+
+hipError_t launch_rounds_data(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
+                              const uint32_t* tids, const int64_t* off, const uint64_t* desc,
+                              const int64_t* doff, uint32_t n_rounds, uint32_t grid,
+                              uint64_t* rec_off, uint8_t* data, uint64_t cap, uint64_t* chain_ws,
+                              uint8_t* target, uint64_t n_pages, uint32_t* err, uint32_t epoch0,
+                              uint32_t* bar, hipStream_t s, Prof* prof) {
+  if (n_rounds == 0) return hipSuccess;
+  DiffSplit sp{};
+  sp.G = 1;
+  sp.rec_off[0] = rec_off;
+  sp.data[0] = data;
+  sp.cap[0] = cap;
+  const IdGuard g{ids, tids, nullptr, nullptr, n_pages, err};
+  hipError_t e = hipMemsetAsync(bar, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  ProfScope ps(prof, GDSM_PROF_DIFF, s);
+  hipLaunchKernelGGL(rounds_data_kernel, dim3(grid), dim3(256), 0, s, twin, cur, ids, tids, off,
+                     desc, doff, n_rounds, sp, chain_ws, target, g, epoch0, bar);
+  return hipGetLastError();
 }
 
 hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s) {

@@ -68,8 +68,10 @@ def native_driver():
 class MmultReplay:
     def __init__(self, ndim: int = 1000, nodes: int = 4, seed: int = 0, device: int = 0,
                  fused: bool = True, retwin: bool = True, driver: str = "native"):
-        if driver not in ("native", "native2", "python"):
+        if driver not in ("native", "native2", "python", "device"):
             raise ValueError(driver)
+        if driver == "device" and not (fused and retwin):
+            raise ValueError("driver='device' runs the re-twinning release (gdsm_rounds)")
         self.driver = driver
         self.fused = fused
         # retwin: every release refreshes its pages' twins (gdsm_release, GDSM_RELEASE_RETWIN), so
@@ -181,6 +183,20 @@ class MmultReplay:
             self.data.sync()
             dt = time.perf_counter() - t0
             g.destroy()
+        elif self.driver == "device":
+            # every round in one persistent launch per context (gdsm_rounds)
+            ev_off = np.ascontiguousarray(self.ev_off, np.int64)
+            id_off = np.ascontiguousarray(self.id_off, np.int64)
+            desc_off = np.ascontiguousarray(self.desc_off, np.int64)
+            t0 = time.perf_counter()
+            gdsm.check(gdsm.lib().gdsm_rounds(
+                self.data.handle, self.pt.handle, self.T.rounds, self.d_events.ptr,
+                ev_off.ctypes.data, self.d_tot.ptr, self.d_ids.ptr, self.d_home.ptr,
+                id_off.ctypes.data, self.d_desc.ptr, desc_off.ctypes.data,
+                C.byref(self._runs.s)), "gdsm_rounds")
+            self.data.sync()
+            self.pt.sync()
+            dt = time.perf_counter() - t0
         elif self.driver in ("native", "native2") and self.fused:
             d = native_driver()
             drv_fn = d.gdsm_replay_mmult_threads if self.driver == "native2" else d.gdsm_replay_mmult

@@ -155,6 +155,48 @@ int gdsm_prof_read(gdsm_ctx* ctx, double* ms, uint64_t* launches);
 int gdsm_probe_ceiling(gdsm_ctx* ctx, int kind, const void* a, const void* b, void* dst,
                        uint64_t n_pages, int reps, float* best_ms, float* median_ms);
 
+/* ---- DSM rounds on the device ------------------------------------------------------------
+ * n_rounds release rounds of one DSM run, each: a coherence batch of fault events on `pt`'s page
+ * table (as gdsm_coherence_batch_async, totals row r = totals + 10 r), the application's writes
+ * of the round on `data` (copy descriptors as gdsm_memcpy_batch) and the release of the pages
+ * written (as gdsm_release with GDSM_RELEASE_RETWIN: diff of list entries ids, applied to
+ * REPLICA at home, TWIN := CURRENT), round after round. Instead of three calls per round, ONE
+ * persistent launch per context: the page-table rounds on pt's stream, the page-data rounds on
+ * data's stream, with device-wide barriers where the per-round launches had their boundaries.
+ * Round r = events [ev_off[r], ev_off[r+1]), list entries [id_off[r], id_off[r+1]) of ids / home,
+ * descriptors [desc_off[r], desc_off[r+1]) of desc (3 u64 each). The offset arrays are HOST
+ * arrays of n_rounds + 1 entries from 0 (copied to the device by the call); events, totals, ids,
+ * home, desc are device pointers. Limits: <= 2048 pages and <= 2^20 events per round, runs sized
+ * for the largest round; data and pt distinct contexts of one device. runs ends holding the last
+ * round's stream. Asynchronous on both streams; gdsm_sync on each reports failures (-ETIMEDOUT:
+ * a device barrier gave up, never expected). Replaces gallocy_amd/native/replay.cpp's per-round
+ * calls for config 5 (test/test_mmult.cpp:51-64's rounds). */
+int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t* events,
+                const int64_t* ev_off, uint64_t* totals, const uint32_t* ids,
+                const uint32_t* home, const int64_t* id_off, const uint64_t* desc,
+                const int64_t* desc_off, gdsm_runs* runs);
+
+/* ---- DSM rounds on the device ------------------------------------------------------------
+ * n_rounds release rounds of one DSM run, each: a coherence batch of fault events on `pt`'s page
+ * table (as gdsm_coherence_batch_async, totals row r = totals + 10 r), the application's writes
+ * of the round on `data` (copy descriptors as gdsm_memcpy_batch) and the release of the pages
+ * written (as gdsm_release with GDSM_RELEASE_RETWIN: diff of list entries ids, applied to
+ * REPLICA at home, TWIN := CURRENT), round after round. Instead of three calls per round, ONE
+ * persistent launch per context: the page-table rounds on pt's stream, the page-data rounds on
+ * data's stream, with device-wide barriers where the per-round launches had their boundaries.
+ * Round r = events [ev_off[r], ev_off[r+1]), list entries [id_off[r], id_off[r+1]) of ids / home,
+ * descriptors [desc_off[r], desc_off[r+1]) of desc (3 u64 each). The offset arrays are HOST
+ * arrays of n_rounds + 1 entries from 0 (copied to the device by the call); events, totals, ids,
+ * home, desc are device pointers. Limits: <= 2048 pages and <= 2^20 events per round, runs sized
+ * for the largest round; data and pt distinct contexts of one device. runs ends holding the last
+ * round's stream. Asynchronous on both streams; gdsm_sync on each reports failures (-ETIMEDOUT:
+ * a device barrier gave up, never expected). Replaces gallocy_amd/native/replay.cpp's per-round
+ * calls for config 5 (test/test_mmult.cpp:51-64's rounds). */
+int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t* events,
+                const int64_t* ev_off, uint64_t* totals, const uint32_t* ids,
+                const uint32_t* home, const int64_t* id_off, const uint64_t* desc,
+                const int64_t* desc_off, gdsm_runs* runs);
+
 /* ---- synthetic inputs (SPEC §6) ------------------------------------------------------- */
 /* Fills the arenas named in `arenas` (bit 1<<GDSM_TWIN | 1<<GDSM_CURRENT | 1<<GDSM_REPLICA,
  * 0 = all) for every page; arena page i has global id first_global + i * stride (stride 0 = 1).

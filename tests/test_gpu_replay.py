@@ -26,13 +26,41 @@ def test_mmult_replay_end_to_end(ndim, nodes, graph, fused):
 
 @pytest.mark.parametrize("ndim,nodes,retwin,driver", [
     (1000, 4, True, "python"), (257, 3, False, "python"), (64, 8, True, "python"),
-    (1000, 4, True, "native2"), (257, 3, False, "native2")])
+    (1000, 4, True, "native2"), (257, 3, False, "native2"),
+    (64, 1, True, "device"), (257, 3, True, "device"), (1000, 1, True, "device"),
+    (1000, 2, True, "device"), (1000, 4, True, "device"), (1000, 8, True, "device")])
 def test_mmult_replay_other_drivers(ndim, nodes, retwin, driver):
-    """The same replay with every round issued from Python (MmultReplay.round, driver="python") or
-    by two C++ threads, one per context (driver="native2"), with and without the re-twinning
-    release: the same home copies, totals and page table."""
+    """The same replay with every round issued from Python (MmultReplay.round, driver="python"),
+    by two C++ threads, one per context (driver="native2"), or on the device (driver="device":
+    gdsm_rounds, one persistent launch per context with device-wide barriers between a round's
+    steps), with and without the re-twinning release: the same home copies, totals and page
+    table."""
     _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, retwin=retwin, driver=driver),
                   nodes, False)
+
+
+@pytest.mark.parametrize("ndim,nodes", [(1000, 1), (257, 3), (1000, 8)])
+def test_device_rounds_stream_equals_the_issued_rounds(ndim, nodes):
+    """gdsm_rounds (every round in one persistent launch per context, write-through hand-offs
+    between its workgroups) leaves the same last-round stream, the same TWIN and CURRENT views
+    and the same home copy as the C++-issued rounds (one chained release launch per round): the
+    stream checks the record bytes and offsets that no home-copy comparison sees."""
+    Rs = [MmultReplay(ndim=ndim, nodes=nodes, seed=11, driver=d) for d in ("native", "device")]
+    try:
+        out = []
+        for R in Rs:
+            R.run()
+            h = R._runs.to_host()
+            n = int(R.id_off[-1] - R.id_off[-2])
+            out.append((h.rec_off[:n + 1].copy(), h.data[:int(h.rec_off[n])].copy(),
+                        R.data.download("twin"), R.data.download("current"), R.home_copy(),
+                        R.totals.copy()))
+        for a, b in zip(*out):
+            assert np.array_equal(a, b)
+        assert out[0][0][-1] > 0  # the last round ships records
+    finally:
+        for R in Rs:
+            R.close()
 
 
 def _check_replay(R, nodes, graph):
