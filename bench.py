@@ -802,6 +802,17 @@ def run_mmult(args):
                  "note": "the same warm replay with each round's calls issued from Python "
                          "(MmultReplay.round, ~1 us of interpreter per call)",
                  "home_copy_equals_product": ok3}
+    # the other C++/device issue mode on the same box, same warm state: the per-round calls of the
+    # C++ loop against gdsm_rounds (every round in one persistent launch per context)
+    alt = None
+    if not args.graph and args.driver in ("native", "device") and args.retwin == "on":
+        other_driver = "device" if args.driver == "native" else "native"
+        R4 = replay(other_driver)
+        dt4 = R4.run()
+        ok4 = bool(np.array_equal(R4.home_copy(), R4.final_image()))
+        R4.close()
+        alt = {"driver": other_driver, "value": round(R.T.rounds / dt4, 1), "unit": "rounds/s",
+               "home_copy_equals_product": ok4}
     ok = bool(np.array_equal(R.home_copy(), R.final_image()))
     # latency breakdown: the same replay again on a fresh state with per-launch HIP events (a
     # separate run, so the events do not weigh on `value`)
@@ -855,6 +866,8 @@ def run_mmult(args):
                                          "steps" if args.driver == "device" else
                                          "eager, two streams, rounds issued from Python"),
            "python_rounds": other,
+           "driver": args.driver,
+           "other_driver_rounds": alt,
            "round": ("coherence batch | the round's row writes (one batched copy), the release "
                      "applying its runs to the home copies and re-twinning its pages "
                      "(gdsm_release)") if args.retwin == "on" else

@@ -1153,6 +1153,7 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
   uint64_t* const status = ws + kCohChainStatus;
   uint32_t* const flag = reinterpret_cast<uint32_t*>(ws + kCohChainFlag);
   for (uint32_t r = 0; r < n_rounds; ++r) {
+    GDSM_RSTAMP(1, r, 0);
     const uint64_t e0 = (uint64_t)eoff[r], n = (uint64_t)eoff[r + 1] - e0;
     const uint64_t nb = (n + kSpan - 1) / kSpan, nfull = n / kSpan;
     const CohChain ch{epoch0 + r, flag};
@@ -1171,6 +1172,7 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
                                                      err, n_nodes, tot, ch);
     }
     if (n == 0 && wv == 0 && lane < 10) st_wt(tot + lane, 0ull);
+    GDSM_RSTAMP(1, r, 1);
     grid_barrier_wt(bar, (r + 1) * gridDim.x, err, kErrRoundsBarrier);
   }
 }
@@ -1444,6 +1446,14 @@ hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t
 
 }  // namespace gdsm
 
+#ifdef GDSM_ROUNDS_STAMPS
+extern "C" int gdsm_debug_round_stamps_pt(void* out, size_t bytes) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gdsm::g_round_stamps), bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -5;
+}
+#endif
 #ifdef GDSM_COH_STAMPS
 extern "C" int gdsm_debug_coh_stamps(void* out, size_t bytes) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(gdsm::g_coh_stamps), bytes, 0, hipMemcpyDeviceToHost) ==

@@ -212,6 +212,22 @@ __device__ __forceinline__ void grid_barrier_wt(uint32_t* __restrict__ bar, uint
   __syncthreads();
 }
 
+// Measurement builds only (-DGDSM_ROUNDS_STAMPS): s_memtime stamps of gdsm_rounds' grids,
+// workgroup 0, [kernel: 0 data, 1 page table][round][point], read by gdsm_debug_round_stamps
+// (gdsm_pages.hip's copy: the data side) and gdsm_debug_round_stamps_pt (the page-table side).
+#ifdef GDSM_ROUNDS_STAMPS
+static __device__ unsigned long long g_round_stamps[2][4096][4];  // (one copy per file)
+#define GDSM_RSTAMP(k_, r_, i_)                                                          \
+  do {                                                                                  \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (r_) < 4096)                             \
+      g_round_stamps[k_][r_][i_] = __builtin_amdgcn_s_memtime();                        \
+  } while (0)
+#else
+#define GDSM_RSTAMP(k_, r_, i_) \
+  do {                          \
+  } while (0)
+#endif
+
 // SPEC §6 mixers (must match oracle/gdsm_oracle.c bit for bit).
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z ^= z >> 30;

@@ -1856,9 +1856,12 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
     uint8_t* __restrict__ target, IdGuard g, uint32_t epoch0, uint32_t* __restrict__ bar) {
   uint32_t phase = 0;
   for (uint32_t r = 0; r < n_rounds; ++r) {
+    GDSM_RSTAMP(0, r, 0);
     const uint64_t d0 = (uint64_t)doff[r], d1 = (uint64_t)doff[r + 1];
     for (uint64_t i = d0 + blockIdx.x; i < d1; i += gridDim.x) copy_desc_wg<true>(desc + 3 * i);
+    GDSM_RSTAMP(0, r, 1);
     grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
+    GDSM_RSTAMP(0, r, 2);
     const uint64_t a = (uint64_t)off[r], n = (uint64_t)off[r + 1] - a;
     DiffSplit rs = sp;
     rs.first[0] = 0;
@@ -1869,6 +1872,7 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
       __syncthreads();  // (the page's LDS exchange is reused by the workgroup's next page)
     }
     if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) st_wt(rs.rec_off[0], (uint64_t)0);
+    GDSM_RSTAMP(0, r, 3);
     grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
   }
 }
@@ -2145,3 +2149,12 @@ hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
 }
 
 }  // namespace gdsm
+
+#ifdef GDSM_ROUNDS_STAMPS
+extern "C" int gdsm_debug_round_stamps(void* out, size_t bytes) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gdsm::g_round_stamps), bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -5;
+}
+#endif
