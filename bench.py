@@ -84,12 +84,13 @@ def parse():
                          "per round); off = a twin launch before the round's writes (round 4)")
     ap.add_argument("--graph", action="store_true",
                     help="mmult: replay one HIP graph of every round instead of eager launches")
-    ap.add_argument("--driver", choices=["native", "native2", "python", "device"],
-                    default="native",
-                    help="mmult: rounds issued by the C++ loop over the C ABI "
+    ap.add_argument("--driver", choices=["device", "native", "native2", "python"],
+                    default="device",
+                    help="mmult: every round on the device (gdsm_rounds: one persistent launch "
+                         "per context, a barrier between rounds; the default, faster at 1-8 "
+                         "nodes: DESIGN §4), or rounds issued by the C++ loop over the C ABI "
                          "(gallocy_amd/native/replay.cpp; native2: two host threads, one per "
-                         "context), from Python, or on the device (gdsm_rounds: one persistent "
-                         "launch per context, barriers between the rounds' steps)")
+                         "context), or from Python")
     ap.add_argument("--events", type=int, default=1 << 30, help="coherence: events per batch")
     ap.add_argument("--coh-pages", type=int, default=16 << 20, help="coherence: pages")
     ap.add_argument("--dist", choices=["zipf", "uniform"], default="zipf")
@@ -776,6 +777,8 @@ def run_mmult(args):
     if world > 1:
         return run_mmult_ranks(args, int(os.environ.get("RANK", "0")), world)
     torch.cuda.set_device(0)
+    if args.driver == "device" and (args.graph or args.retwin == "off"):
+        args.driver = "native"  # (gdsm_rounds runs the re-twinning release, eagerly)
     # warmup: with --warmup W > 0, one untimed replay of the whole trace on a fresh state first
     # (the kernels' code objects loaded and the host paths warm: a cold first replay in a fresh
     # process takes ~1.5x as long per round); the timed replay starts from a fresh state again
@@ -831,20 +834,26 @@ def run_mmult(args):
     kern_ms = sum(v[0] for v in pd.values()) + sum(v[0] for v in pp.values())
     launches = sum(v[1] for v in pd.values()) + sum(v[1] for v in pp.values())
     copies = sum(len(R.rows[r]) for r in range(rounds))  # rows written per round
+    device = args.driver == "device"
     latency = {"bound": "latency",
-               "kernel_launches_per_round": round(launches / rounds, 2),
-               "copy_launches_per_round": 1,
+               "kernel_launches_per_round": round(launches / rounds, 4),
+               "copy_launches_per_round": 0 if device else 1,
                "rows_written_per_round": round(copies / rounds, 2),
                "host_syncs_per_round": 0,
                "kernel_ms_per_round": round(kern_ms / rounds, 5),
                "wall_ms_per_round_profiled": round(dt2 / rounds * 1e3, 5),
                "stages": stages,
-               "note": "a round is ~10 dense pages (~500 runs each) and ~8000 fault events: "
-                       "every operation is a few microseconds of dependent latency, so the round "
-                       "is the longer of two streams (page data: the row writes' batched copy, "
-                       "then one release launch that diffs, applies to the home copies and "
-                       "re-twins; page table: one coherence fold launch) or the host's issue "
-                       "time for the three calls. No HBM or MFMA roofline applies."}
+               "note": ("a round is ~10 dense pages (~500 runs each) and ~8000 fault events: "
+                        "every operation is a few microseconds of dependent latency. "
+                        + ("gdsm_rounds: two launches for the whole trace (stages: ms per launch "
+                           "= all rounds), a round is the longer of the page-data loop (the "
+                           "release with the round's writes laid on, then a device barrier) and "
+                           "the page-table loop (the fold, then a device barrier)" if device else
+                           "The round is the longer of two streams (page data: the row writes' "
+                           "batched copy, then one release launch that diffs, applies to the "
+                           "home copies and re-twins; page table: one coherence fold launch) or "
+                           "the host's issue time for the three calls")
+                        + ". No HBM or MFMA roofline applies.")}
     res = {"metric": "mmult trace replay rounds/sec", "value": round(R.T.rounds / dt, 1),
            "unit": "rounds/s", "n_gpus": 1, "steps": R.T.rounds, "warmup": warm_rounds,
            "ms_per_step": round(dt / R.T.rounds * 1e3, 4), "higher_is_better": True,
@@ -862,8 +871,8 @@ def run_mmult(args):
                                          "per context (gallocy_amd/native/replay.cpp)"
                                          if args.driver == "native2" else
                                          "one persistent launch per stream for every round "
-                                         "(gdsm_rounds), device-wide barriers between a round's "
-                                         "steps" if args.driver == "device" else
+                                         "(gdsm_rounds), a device-wide barrier between rounds"
+                                         if args.driver == "device" else
                                          "eager, two streams, rounds issued from Python"),
            "python_rounds": other,
            "driver": args.driver,

@@ -901,10 +901,10 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   GDSM_TRY(hipMemcpyAsync(data->rounds_ws, id_off, ob, hipMemcpyHostToDevice, data->stream));
   GDSM_TRY(hipMemcpyAsync(data->rounds_ws + ob, desc_off, ob, hipMemcpyHostToDevice, data->stream));
   GDSM_TRY(hipMemcpyAsync(pt->rounds_ws, ev_off, ob, hipMemcpyHostToDevice, pt->stream));
-  // grids: a workgroup per page or copy of the largest round (data), a wave per 256-event span of
+  // grids: a workgroup per page of the largest round (data), a wave per 256-event span of
   // the largest round (page table); both far below what is resident at once, which the barriers
   // need (checked)
-  const uint64_t gd_n = std::min<uint64_t>(std::max<uint64_t>({max_ids, max_desc, 1}), 256);
+  const uint64_t gd_n = std::min<uint64_t>(std::max<uint64_t>(max_ids, 1), 256);
   const uint64_t gp_n = std::min<uint64_t>(std::max<uint64_t>((max_ev + 1023) / 1024, 1), 256);
   if (gd_n > resident_grid(gdsm::rounds_data_kernel_ptr()) ||
       gp_n > resident_grid(gdsm::rounds_fold_kernel_ptr()))

@@ -758,9 +758,16 @@ struct CohChain {
   uint32_t epoch;    // 1 .. 2^29 - 1
   uint32_t* flag;    // == epoch once the caller's totals are zeroed
 };
+// A span's events loaded ahead (gdsm_rounds: the next round's, while the barrier is waited out):
+// its first chunks' events and the events before and after it.
+struct SpanPre {
+  uint64_t X[kSCSmall];
+  uint32_t xprev, xnext;
+};
+
 // kWT (gdsm_rounds' persistent grid): page-table words stored write-through and gathered past
 // L1 (st_wt / ld_wt), since the next round's waves on other XCDs read them after a fence-free
-// barrier.
+// barrier. pre: the span's events already loaded (kSC <= kSCSmall), else loaded here.
 template <uint32_t kSC, bool kFull, bool kChain = false, bool kWT = false>
 __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                 const uint64_t* __restrict__ ev, uint64_t n,
@@ -768,7 +775,9 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
                                                 uint32_t* __restrict__ partial,
                                                 uint32_t* __restrict__ err, uint32_t n_nodes,
                                                 unsigned long long* __restrict__ totals,
-                                                const CohChain ch = CohChain{}) {
+                                                const CohChain ch = CohChain{},
+                                                const bool use_pre = false,
+                                                const SpanPre pre = SpanPre{}) {
   const uint64_t tag = kChain ? (uint64_t)ch.epoch << 32 : 0ull;
   // a status granule as this launch sees it (kChain: an earlier launch's reads as unpublished)
   auto ld_status = [&](int64_t q) {
@@ -783,9 +792,9 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   const uint32_t nch = kFull ? kSC : (nev + 63u) / 64u;
   const uint64_t lem = le_mask(lane);
   // the event before the span and the one after it (uniform scalar loads)
-  const uint32_t xprev = lo > 0 ? (uint32_t)ev[lo - 1] : 0u;
   const bool has_next = hi < n;
-  const uint32_t xnext = has_next ? (uint32_t)ev[hi] : 0u;
+  const uint32_t xprev = use_pre ? pre.xprev : (lo > 0 ? (uint32_t)ev[lo - 1] : 0u);
+  const uint32_t xnext = use_pre ? pre.xnext : (has_next ? (uint32_t)ev[hi] : 0u);
 
   uint64_t X[kSD];       // events of chunks c .. c + kSD - 1 (ring)
   uint64_t Wg[kSG];      // page-table words of the heads of chunks c .. c + kSG - 1 (ring)
@@ -817,7 +826,12 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   } while (0)
 
 #pragma unroll
-  for (uint32_t j = 0; j < kSD; ++j) GDSM_SLOAD(j, j);
+  for (uint32_t j = 0; j < kSD; ++j) {
+    if (kSC <= kSCSmall && use_pre)
+      X[j] = j < kSC ? pre.X[j < kSC ? j : 0] : ~0ull;
+    else
+      GDSM_SLOAD(j, j);
+  }
 #pragma unroll
   for (uint32_t j = 0; j < kSG; ++j) GDSM_SGATHER(j, j, j);
 
@@ -835,6 +849,20 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   bool has_d = false;                         // the span's first segment ended inside it
   uint32_t d_state = 0, d_cnt = 0, d_page = 0;
   bool any_head = false;
+  // kDefer (the write-through rounds path, short spans): the segment ends found in the chunks are
+  // held in registers and stored after the span's aggregate is published, so the publication's
+  // wait for the loads does not also wait for write-through store acknowledgements
+  constexpr bool kDefer = kWT && kSC <= kSD;
+  constexpr uint32_t kDN = kDefer ? kSC : 1;
+  uint64_t dval[kDN], oval[kDN];  // chunk j: this lane's segment end / lane 0's open segment
+  uint32_t dpg[kDN], opg[kDN];    // their pages (~0u: none)
+#pragma unroll
+  for (uint32_t j = 0; j < kDN; ++j) {
+    dpg[j] = opg[j] = ~0u;
+    dval[j] = oval[j] = 0;
+  }
+  uint32_t lpg = ~0u, apg = ~0u, acnt = 0;  // the span-end store / count add
+  uint64_t lval = 0;
 
   for (uint32_t c0 = 0; c0 < nch; c0 += kSD) {
 #pragma unroll
@@ -848,9 +876,15 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       // the open segment closes at the previous chunk's end when this chunk starts a page
       if (c > 0 && (Hd & 1ull)) {
         if (open_local) {
-          if (lane == 0 && open_page < n_pages)
-            st_<kWT>(pt + open_page,
-                     (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32));
+          const uint64_t wv = (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32);
+          if (kDefer) {  // (c == j: one pass of the outer loop when kSC <= kSD)
+            if (lane == 0 && open_page < n_pages) {
+              opg[j < kDN ? j : 0] = open_page;
+              oval[j < kDN ? j : 0] = wv;
+            }
+          } else if (lane == 0 && open_page < n_pages) {
+            st_<kWT>(pt + open_page, wv);
+          }
         } else {
           has_d = true;
           d_state = carry;
@@ -906,9 +940,16 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
         const uint32_t cnt = popc64(M & lem & ~((1ull << h) - 1ull));
         const uint32_t f0 = (uint32_t)__shfl((int)(uint32_t)(W >> 32), (int)h, 64);
         const uint32_t pg = xl >> 4;
-        if (end && pg < n_pages && (inchunk || open_local))
-          st_<kWT>(pt + pg, (uint64_t)s_state(incl) |
-                                ((uint64_t)(inchunk ? f0 + cnt : open_f0 + open_cnt + cnt) << 32));
+        if (end && pg < n_pages && (inchunk || open_local)) {
+          const uint64_t wv = (uint64_t)s_state(incl) |
+                              ((uint64_t)(inchunk ? f0 + cnt : open_f0 + open_cnt + cnt) << 32);
+          if (kDefer) {
+            dpg[j < kDN ? j : 0] = pg;
+            dval[j < kDN ? j : 0] = wv;
+          } else {
+            st_<kWT>(pt + pg, wv);
+          }
+        }
         if (!open_local) {
           const uint64_t dm = __ballot(end && !inchunk);
           if (dm) {  // the span's first segment ends here (lowest end lane)
@@ -945,9 +986,15 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   bool cont_first = false;   // the span's first segment runs past it
   if (next_head) {
     if (open_local) {
-      if (lane == 0 && last_page < n_pages)
-        st_<kWT>(pt + last_page,
-                 (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32));
+      const uint64_t wv = (uint64_t)s_state(carry) | ((uint64_t)(open_f0 + open_cnt) << 32);
+      if (lane == 0 && last_page < n_pages) {
+        if (kDefer) {
+          lpg = last_page;
+          lval = wv;
+        } else {
+          st_<kWT>(pt + last_page, wv);
+        }
+      }
     } else {
       has_d = true;
       d_state = carry;
@@ -955,8 +1002,14 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       d_page = last_page;
     }
   } else if (open_local) {
-    if (lane == 0 && open_cnt && last_page < n_pages)
-      atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, open_cnt);
+    if (lane == 0 && open_cnt && last_page < n_pages) {
+      if (kDefer) {
+        apg = last_page;
+        acnt = open_cnt;
+      } else {
+        atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, open_cnt);
+      }
+    }
   } else {
     cont_first = true;
   }
@@ -968,6 +1021,15 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   if (lane == 0)
     __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (any_head ? kFHead : 0ull) | tag | agg,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (kDefer) {  // the held segment ends (pages inside this span: no other wave touches them)
+#pragma unroll
+    for (uint32_t j = 0; j < kDN; ++j) {
+      if (opg[j] != ~0u) st_<kWT>(pt + opg[j], oval[j]);
+      if (dpg[j] != ~0u) st_<kWT>(pt + dpg[j], dval[j]);
+    }
+    if (lpg != ~0u) st_<kWT>(pt + lpg, lval);
+    if (apg != ~0u) atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)apg + 1, acnt);
+  }
   const bool ordered = has_d;
   uint32_t cur = 0;
   if (b > 0) {
@@ -1152,6 +1214,23 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
   const uint32_t lane = threadIdx.x & 63;
   uint64_t* const status = ws + kCohChainStatus;
   uint32_t* const flag = reinterpret_cast<uint32_t*>(ws + kCohChainFlag);
+  // the events of this wave's first span of round r, loaded before round r - 1's barrier
+  // (events are never written in the launch: no hand-off)
+  SpanPre pre;
+  auto prefetch = [&](uint32_t r) {
+    const uint64_t e0 = (uint64_t)eoff[r], n = (uint64_t)eoff[r + 1] - e0;
+    const uint64_t lo = wv * kSpan;
+    if (lo >= n) return false;
+#pragma unroll
+    for (uint32_t j = 0; j < kSCSmall; ++j) {
+      const uint64_t g = lo + 64ull * j + lane;
+      pre.X[j] = g < n ? __builtin_nontemporal_load(ev + e0 + g) : ~0ull;
+    }
+    pre.xprev = lo > 0 ? (uint32_t)ev[e0 + lo - 1] : 0u;
+    pre.xnext = lo + kSpan < n ? (uint32_t)ev[e0 + lo + kSpan] : 0u;
+    return true;
+  };
+  bool have_pre = n_rounds > 0 && prefetch(0);
   for (uint32_t r = 0; r < n_rounds; ++r) {
     GDSM_RSTAMP(1, r, 0);
     const uint64_t e0 = (uint64_t)eoff[r], n = (uint64_t)eoff[r + 1] - e0;
@@ -1164,13 +1243,15 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(flag, ch.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      const bool up = b == wv && have_pre;
       if (b < nfull)
         coh_stream_wave<kSCSmall, true, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
-                                                    err, n_nodes, tot, ch);
+                                                    err, n_nodes, tot, ch, up, pre);
       else
         coh_stream_wave<kSCSmall, false, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
-                                                     err, n_nodes, tot, ch);
+                                                     err, n_nodes, tot, ch, up, pre);
     }
+    have_pre = r + 1 < n_rounds && prefetch(r + 1);
     if (n == 0 && wv == 0 && lane < 10) st_wt(tot + lane, 0ull);
     GDSM_RSTAMP(1, r, 1);
     grid_barrier_wt(bar, (r + 1) * gridDim.x, err, kErrRoundsBarrier);

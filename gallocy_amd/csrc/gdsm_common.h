@@ -159,38 +159,13 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// A barrier of a persistent grid (every workgroup resident): `bar` counts arrivals across the
-// whole launch (zeroed before it), the k-th barrier (1-based) waits for k x gridDim.x of them.
-// Agent-scope release before the arrival and acquire after the wait, so what one workgroup
-// stored before the barrier is what another reads after it. A wait that never ends (a
-// workgroup not resident: never expected, the launcher sizes the grid below the occupancy) sets
-// `err_bit` in *err and lets the workgroup go on, so the grid always drains.
-__device__ __forceinline__ void grid_barrier(uint32_t* __restrict__ bar, uint32_t target,
-                                             uint32_t* __restrict__ err, uint32_t err_bit) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      // (a barrier that already gave up anywhere: no more waiting, the grid drains)
-      if ((++spins & 1023u) == 0 &&
-          (spins > (1u << 22) ||
-           (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & err_bit))) {
-        atomicOr(err, err_bit);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-// The same barrier for grids whose hand-offs are all write-through (st_wt / ld_wt above): no
-// release or acquire fence (their L2 write-back and L1 invalidate cost ~1.7 us each); every wave
-// drains its stores (vmcnt(0)) before the workgroup's arrival, and the arrival counter is an
-// agent atomic polled by sc1 loads.
+// A barrier of a persistent grid (every workgroup resident) whose hand-offs are all write-through
+// (st_wt / ld_wt above): no release or acquire fence (their L2 write-back and L1 invalidate cost
+// ~1.7 us each); every wave drains its stores (vmcnt(0)) before the workgroup's arrival, and the
+// arrival counter `bar` (zeroed before the launch; the k-th barrier waits for k x gridDim.x
+// arrivals) is an agent atomic polled by sc1 loads. A wait that never ends (a workgroup not
+// resident: never expected, the launcher sizes the grid below the occupancy) sets `err_bit` in
+// *err and lets the workgroup go on, so the grid always drains.
 __device__ __forceinline__ void grid_barrier_wt(uint32_t* __restrict__ bar, uint32_t target,
                                                 uint32_t* __restrict__ err, uint32_t err_bit) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

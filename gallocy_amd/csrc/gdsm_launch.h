@@ -30,6 +30,8 @@ hipError_t launch_twin(uint8_t* twin, const uint8_t* cur, const uint32_t* ids, u
 // tids, err |= 8 when any id was out of range. A null list is not checked.
 // Device error bit of a persistent grid's barrier that never completed (gdsm_rounds).
 constexpr uint32_t kErrRoundsBarrier = 64;
+// ... and of a round's writes that were not 8-B aligned or fell outside its released pages.
+constexpr uint32_t kErrRoundsWrites = 128;
 struct IdGuard {
   const uint32_t* ids;
   const uint32_t* tids;

@@ -852,14 +852,26 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
 // One page (list entry u of n) by the calling four-wave workgroup; the kernel below draws u as a
 // ticket, rounds_data_kernel assigns it (every workgroup resident, pages in ascending order per
 // workgroup, so the look-back only ever waits for running workgroups).
+// A round's writes for release_page_wg<..., kFuse>: copy descriptors [d0, d1) of desc, each
+// (dst, src, bytes) 8-B aligned; `covered` counts the 8-B words laid onto released pages.
+struct RoundWrites {
+  const uint64_t* desc;
+  uint64_t d0, d1;
+  unsigned long long* covered;
+};
+
 // kWT: every store write-through and the page loads past L1 (st_wt / ld_wt16): the persistent
 // rounds grid hands CURRENT, TWIN, REPLICA and the stream from one workgroup to another with no
-// fences.
-template <bool kApply, bool kRetwin, bool kWT = false>
+// fences. kFuse: the round's writes (rw) that fall on this page are laid onto its CURRENT chunk
+// in registers and stored to CURRENT here, so the release needs no copy step and no barrier
+// before it (a word outside every released page is never written: `covered` falls short and the
+// launch flags it).
+template <bool kApply, bool kRetwin, bool kWT = false, bool kFuse = false>
 __device__ __forceinline__ void release_page_wg(
     const uint64_t u, const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit& sp, uint64_t* __restrict__ ws,
-    uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard& g) {
+    uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard& g,
+    const RoundWrites& rw = RoundWrites{}) {
   uint8_t* const twin_w = const_cast<uint8_t*>(twin);  // (kRetwin: see diff_single_kernel)
   __shared__ uint32_t edge_first[4], edge_last[4], tot[4], lastst[4];
   __shared__ uint64_t rec_at;
@@ -874,7 +886,34 @@ __device__ __forceinline__ void release_page_wg(
   const bool ample = kRetwin && cap >= n * GDSM_MAX_RECORD;
   const uint32_t ch = w * 64 + lane;  // this lane's chunk of the page
   const uint4 t = kWT ? ld_wt16(twin + pj * kPage + ch * 16u) : ld_nt16(twin + pj * kPage + ch * 16u);
-  const uint4 c = kWT ? ld_wt16(cur + pj * kPage + ch * 16u) : ld_nt16(cur + pj * kPage + ch * 16u);
+  uint4 c = kWT ? ld_wt16(cur + pj * kPage + ch * 16u) : ld_nt16(cur + pj * kPage + ch * 16u);
+  if (kFuse) {
+    const uint64_t a = reinterpret_cast<uint64_t>(cur + pj * kPage + ch * 16u);
+    uint32_t wm = 0;  // bit h: 8-B half h of the chunk written this round
+    uint64_t hv[2] = {(uint64_t)c.x | ((uint64_t)c.y << 32), (uint64_t)c.z | ((uint64_t)c.w << 32)};
+    for (uint64_t d = rw.d0; d < rw.d1; ++d) {
+      const uint64_t dst = rw.desc[3 * d], src = rw.desc[3 * d + 1], bytes = rw.desc[3 * d + 2];
+      if (a + 16 <= dst || a >= dst + bytes) continue;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint64_t ha = a + 8 * h;
+        if (ha >= dst && ha + 8 <= dst + bytes) {
+          hv[h] = *reinterpret_cast<const uint64_t*>(src + (ha - dst));
+          wm |= 1u << h;
+        }
+      }
+    }
+    if (wm) {
+      c = make_uint4((uint32_t)hv[0], (uint32_t)(hv[0] >> 32), (uint32_t)hv[1],
+                     (uint32_t)(hv[1] >> 32));
+      uint8_t* const cw = const_cast<uint8_t*>(cur) + pj * kPage + ch * 16u;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h)
+        if ((wm >> h) & 1u) st_<kWT>(reinterpret_cast<uint64_t*>(cw + 8 * h), hv[h]);
+    }
+    const uint32_t words = wave_sum((uint32_t)__popc(wm));
+    if (words && lane == 0) atomicAdd(rw.covered, (unsigned long long)words);
+  }
   const uint32_t m = diffmask16(t, c);
   const uint64_t pt = kApply ? (tids ? (g.tids ? guarded_id(tids, i, g.n_pages, bad) : tids[i]) : pj)
                              : 0;  // page at target
@@ -1840,10 +1879,12 @@ __global__ __launch_bounds__(256) void copy_batch_kernel(const uint64_t* __restr
 
 // ---- DSM rounds on the device (gdsm_rounds, page-data side): one persistent launch runs every
 // round's row writes (the application's stores, as copy descriptors) and its release (diff of the
-// written pages + home apply + re-twin, release_page_wg), with grid barriers where separate
-// launches had their boundaries: copies | barrier | release | barrier. Round r's pages are list
-// entries [off[r], off[r+1]) of ids / tids (r's records land in the one stream sp describes, as
-// a release of those pages would write them), its copies descriptors [doff[r], doff[r+1]).
+// written pages + home apply + re-twin, release_page_wg), a grid barrier between rounds. The
+// writes are laid onto the released pages inside the release (kFuse: the workgroup releasing a
+// page first applies the round's descriptors that fall on it, in order), so a round is one step:
+// separate launches needed a copy, a boundary and the release. Round r's pages are list entries
+// [off[r], off[r+1]) of ids / tids (r's records land in the one stream sp describes, as a release
+// of those pages would write them), its writes descriptors [doff[r], doff[r+1]).
 // Look-back granules carry epoch epoch0 + r (DiffChain's ws and layout; the launcher leaves the
 // chain to be zeroed again by its next chained launch). Every byte one workgroup hands another
 // (CURRENT rows, TWIN, REPLICA, the stream) is stored write-through and the pages are loaded past
@@ -1854,27 +1895,43 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
     const int64_t* __restrict__ off, const uint64_t* __restrict__ desc,
     const int64_t* __restrict__ doff, uint32_t n_rounds, DiffSplit sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, IdGuard g, uint32_t epoch0, uint32_t* __restrict__ bar) {
+  // bar[0]: barrier arrivals; bar[2..3]: the words laid onto released pages minus the words
+  // the descriptors hold (0 at the end, else a write fell outside the released pages)
+  unsigned long long* const covered = reinterpret_cast<unsigned long long*>(bar + 2);
   uint32_t phase = 0;
   for (uint32_t r = 0; r < n_rounds; ++r) {
     GDSM_RSTAMP(0, r, 0);
     const uint64_t d0 = (uint64_t)doff[r], d1 = (uint64_t)doff[r + 1];
-    for (uint64_t i = d0 + blockIdx.x; i < d1; i += gridDim.x) copy_desc_wg<true>(desc + 3 * i);
-    GDSM_RSTAMP(0, r, 1);
-    grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
-    GDSM_RSTAMP(0, r, 2);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      unsigned long long words = 0;
+      uint32_t misaligned = 0;
+      for (uint64_t d = d0; d < d1; ++d) {
+        words += desc[3 * d + 2] / 8;
+        misaligned |= (uint32_t)((desc[3 * d] | desc[3 * d + 1] | desc[3 * d + 2]) & 7u);
+      }
+      if (words) atomicAdd(covered, 0ull - words);
+      if (misaligned && g.err) atomicOr(g.err, kErrRoundsWrites);
+    }
     const uint64_t a = (uint64_t)off[r], n = (uint64_t)off[r + 1] - a;
     DiffSplit rs = sp;
     rs.first[0] = 0;
     rs.first[1] = n;
     rs.epoch = epoch0 + r;
+    const RoundWrites rw{desc, d0, d1, covered};
+    GDSM_RSTAMP(0, r, 1);
+    GDSM_RSTAMP(0, r, 2);
     for (uint64_t u = blockIdx.x; u < n; u += gridDim.x) {
-      release_page_wg<true, true, true>(u, twin, cur, ids + a, rs, ws, target, tids + a, g);
+      release_page_wg<true, true, true, true>(u, twin, cur, ids + a, rs, ws, target, tids + a, g,
+                                              rw);
       __syncthreads();  // (the page's LDS exchange is reused by the workgroup's next page)
     }
     if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) st_wt(rs.rec_off[0], (uint64_t)0);
     GDSM_RSTAMP(0, r, 3);
     grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && g.err &&
+      __hip_atomic_load(covered, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+    atomicOr(g.err, kErrRoundsWrites);
 }
 
 const void* rounds_data_kernel_ptr() { return reinterpret_cast<const void*>(rounds_data_kernel); }
@@ -1892,7 +1949,7 @@ hipError_t launch_rounds_data(const uint8_t* twin, const uint8_t* cur, const uin
   sp.data[0] = data;
   sp.cap[0] = cap;
   const IdGuard g{ids, tids, nullptr, nullptr, n_pages, err};
-  hipError_t e = hipMemsetAsync(bar, 0, sizeof(uint32_t), s);
+  hipError_t e = hipMemsetAsync(bar, 0, 16, s);  // arrivals + the coverage count
   if (e != hipSuccess) return e;
   ProfScope ps(prof, GDSM_PROF_DIFF, s);
   hipLaunchKernelGGL(rounds_data_kernel, dim3(grid), dim3(256), 0, s, twin, cur, ids, tids, off,

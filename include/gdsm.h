@@ -162,14 +162,17 @@ int gdsm_probe_ceiling(gdsm_ctx* ctx, int kind, const void* a, const void* b, vo
  * written (as gdsm_release with GDSM_RELEASE_RETWIN: diff of list entries ids, applied to
  * REPLICA at home, TWIN := CURRENT), round after round. Instead of three calls per round, ONE
  * persistent launch per context: the page-table rounds on pt's stream, the page-data rounds on
- * data's stream, with device-wide barriers where the per-round launches had their boundaries.
+ * data's stream, a device-wide barrier between rounds where the launches had their boundaries.
  * Round r = events [ev_off[r], ev_off[r+1]), list entries [id_off[r], id_off[r+1]) of ids / home,
  * descriptors [desc_off[r], desc_off[r+1]) of desc (3 u64 each). The offset arrays are HOST
  * arrays of n_rounds + 1 entries from 0 (copied to the device by the call); events, totals, ids,
- * home, desc are device pointers. Limits: <= 2048 pages and <= 2^20 events per round, runs sized
- * for the largest round; data and pt distinct contexts of one device. runs ends holding the last
- * round's stream. Asynchronous on both streams; gdsm_sync on each reports failures (-ETIMEDOUT:
- * a device barrier gave up, never expected). Replaces gallocy_amd/native/replay.cpp's per-round
+ * home, desc are device pointers. A round's writes are laid onto its released pages by the
+ * release itself (no separate copy step), so they must be 8-B aligned (dst, src and bytes) and lie
+ * inside the pages that round releases, each page listed once per round; otherwise gdsm_sync on
+ * data reports -EINVAL. Limits: <= 2048 pages and <= 2^20 events per round, runs sized for the
+ * largest round; data and pt distinct contexts of one device. runs ends holding the last round's
+ * stream. Asynchronous on both streams; gdsm_sync on each reports failures (-ETIMEDOUT: a device
+ * barrier gave up, never expected). Replaces gallocy_amd/native/replay.cpp's per-round
  * calls for config 5 (test/test_mmult.cpp:51-64's rounds). */
 int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t* events,
                 const int64_t* ev_off, uint64_t* totals, const uint32_t* ids,
@@ -183,14 +186,17 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
  * written (as gdsm_release with GDSM_RELEASE_RETWIN: diff of list entries ids, applied to
  * REPLICA at home, TWIN := CURRENT), round after round. Instead of three calls per round, ONE
  * persistent launch per context: the page-table rounds on pt's stream, the page-data rounds on
- * data's stream, with device-wide barriers where the per-round launches had their boundaries.
+ * data's stream, a device-wide barrier between rounds where the launches had their boundaries.
  * Round r = events [ev_off[r], ev_off[r+1]), list entries [id_off[r], id_off[r+1]) of ids / home,
  * descriptors [desc_off[r], desc_off[r+1]) of desc (3 u64 each). The offset arrays are HOST
  * arrays of n_rounds + 1 entries from 0 (copied to the device by the call); events, totals, ids,
- * home, desc are device pointers. Limits: <= 2048 pages and <= 2^20 events per round, runs sized
- * for the largest round; data and pt distinct contexts of one device. runs ends holding the last
- * round's stream. Asynchronous on both streams; gdsm_sync on each reports failures (-ETIMEDOUT:
- * a device barrier gave up, never expected). Replaces gallocy_amd/native/replay.cpp's per-round
+ * home, desc are device pointers. A round's writes are laid onto its released pages by the
+ * release itself (no separate copy step), so they must be 8-B aligned (dst, src and bytes) and lie
+ * inside the pages that round releases, each page listed once per round; otherwise gdsm_sync on
+ * data reports -EINVAL. Limits: <= 2048 pages and <= 2^20 events per round, runs sized for the
+ * largest round; data and pt distinct contexts of one device. runs ends holding the last round's
+ * stream. Asynchronous on both streams; gdsm_sync on each reports failures (-ETIMEDOUT: a device
+ * barrier gave up, never expected). Replaces gallocy_amd/native/replay.cpp's per-round
  * calls for config 5 (test/test_mmult.cpp:51-64's rounds). */
 int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t* events,
                 const int64_t* ev_off, uint64_t* totals, const uint32_t* ids,

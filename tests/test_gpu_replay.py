@@ -148,3 +148,48 @@ def test_rank_replay_multi_rank_loopback(ranks, ndim):
     finally:
         for R in Rs:
             R.close()
+
+
+@pytest.mark.parametrize("case", ["outside", "misaligned", "ok"])
+def test_rounds_refuse_writes_outside_released_pages(case):
+    """gdsm_rounds lays a round's writes onto the pages the round releases (no copy step), so a
+    write into a page the round does not release, or one that is not 8-B aligned, is reported by
+    gdsm_sync (-EINVAL) instead of being lost silently; a write inside the released page lands in
+    CURRENT, REPLICA (home apply) and TWIN (re-twin)."""
+    import ctypes as C
+    import errno
+    import gallocy_amd as ga
+    from gallocy_amd import gdsm
+    L = gdsm.lib()
+    with ga.Context(8) as d, ga.Context(8, arenas=()) as pt:
+        z = np.zeros((8, 4096), np.uint8)
+        for a in ("twin", "current", "replica"):
+            d.upload(a, z)
+        pt.coh_init(2)
+        src = d.buffer(4096).upload(np.arange(4096, dtype=np.uint64).view(np.uint8)[:4096])
+        base = d.arena_ptr("current")
+        dst_page = 2 if case == "outside" else 1
+        off = 8 if case != "misaligned" else 12
+        desc = np.array([base + dst_page * 4096 + off, src.ptr, 256], np.uint64)
+        dd = d.buffer(24).upload(desc)
+        ids = d.ids([1])
+        home = d.ids([1])
+        ev = pt.buffer(8).upload(np.array([(1 << 4) | 1], np.uint64))
+        tot = pt.buffer(80)
+        runs = gdsm.Runs(d, 1, cap=10244)
+        z2 = np.array([0, 1], np.int64)
+        rc = L.gdsm_rounds(d.handle, pt.handle, 1, ev.ptr, z2.ctypes.data, tot.ptr, ids.ptr,
+                           home.ptr, z2.ctypes.data, dd.ptr, z2.ctypes.data, C.byref(runs.s))
+        assert rc == 0
+        rc_d = L.gdsm_sync(d.handle)
+        assert L.gdsm_sync(pt.handle) == 0
+        if case == "ok":
+            assert rc_d == 0
+            want = np.frombuffer(src.download(np.uint8, 256).tobytes(), np.uint8)
+            for a in ("current", "replica", "twin"):
+                got = d.download(a, 1, 1).reshape(-1)
+                assert np.array_equal(got[8:264], want), a
+                assert not got[:8].any() and not got[264:].any(), a
+        else:
+            assert rc_d == -errno.EINVAL
+        runs.free()
