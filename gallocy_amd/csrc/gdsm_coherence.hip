@@ -757,6 +757,7 @@ __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popc
 struct CohChain {
   uint32_t epoch;    // 1 .. 2^29 - 1
   uint32_t* flag;    // == epoch once the caller's totals are zeroed
+  uint32_t round;    // (gdsm_rounds, measurement stamps only)
 };
 // A span's events loaded ahead (gdsm_rounds: the next round's, while the barrier is waited out):
 // its first chunks' events and the events before and after it.
@@ -796,9 +797,13 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   const uint32_t xprev = use_pre ? pre.xprev : (lo > 0 ? (uint32_t)ev[lo - 1] : 0u);
   const uint32_t xnext = use_pre ? pre.xnext : (has_next ? (uint32_t)ev[hi] : 0u);
 
+  // gather depth: the write-through rounds path gathers every chunk's head words at once (its
+  // spans fit one ring pass, kSC <= kSD), so the span waits out one gather round trip, not two
+  constexpr uint32_t kSGw = (kWT && kSC <= kSD) ? kSC : kSG;
+  static_assert(kSGw == kSG || kSC <= kSD, "ring geometry");
   uint64_t X[kSD];       // events of chunks c .. c + kSD - 1 (ring)
-  uint64_t Wg[kSG];      // page-table words of the heads of chunks c .. c + kSG - 1 (ring)
-  uint64_t Hg[kSG];      // their head masks
+  uint64_t Wg[kSGw];     // page-table words of the heads of chunks c .. c + kSGw - 1 (ring)
+  uint64_t Hg[kSGw];     // their head masks
 #define GDSM_SLOAD(c_, slot_)                                                        \
   do {                                                                               \
     const uint64_t g_ = lo + 64ull * (c_) + lane;                                    \
@@ -833,7 +838,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       GDSM_SLOAD(j, j);
   }
 #pragma unroll
-  for (uint32_t j = 0; j < kSG; ++j) GDSM_SGATHER(j, j, j);
+  for (uint32_t j = 0; j < kSGw; ++j) GDSM_SGATHER(j, j, j);
 
   // the span's first event continues the page before it: its first segment starts from PROBE
   const uint32_t x0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)X[0]);
@@ -870,8 +875,8 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       const uint32_t c = c0 + j;
       if (c >= nch) break;
       const uint64_t x = X[j];
-      const uint64_t W = Wg[j % kSG];
-      const uint64_t Hd = Hg[j % kSG];
+      const uint64_t W = Wg[j % kSGw];
+      const uint64_t Hd = Hg[j % kSGw];
       any_head |= Hd != 0;
       // the open segment closes at the previous chunk's end when this chunk starts a page
       if (c > 0 && (Hd & 1ull)) {
@@ -974,7 +979,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       carry = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       // refill the rings: events kSD chunks ahead, head words kSG chunks ahead
       GDSM_SLOAD(c + kSD, j);
-      GDSM_SGATHER(c + kSG, (j + kSG) % kSD, j % kSG);
+      GDSM_SGATHER(c + kSGw, (j + kSGw) % kSD, j % kSGw);
     }
   }
 #undef GDSM_SLOAD
@@ -1017,6 +1022,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   // ---- publish the span's aggregate once its loads landed, then look back
   const uint32_t agg = (carry & kSF) ? (kConst | s_state(carry)) : ((carry >> 20) & 0xFFu);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  if (kWT) GDSM_RSTAMP(1, ch.round, 2);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (lane == 0)
     __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (any_head ? kFHead : 0ull) | tag | agg,
@@ -1068,6 +1074,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
+  if (kWT) GDSM_RSTAMP(1, ch.round, 3);
   // ---- the span's first segment, now that its incoming state `cur` is known
   uint32_t dfc = 0;                 // correction of the first segment's fault count
   uint32_t Fcorr_node_minus = 0;    // nodes whose probe read fault did not happen
@@ -1124,7 +1131,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   uint32_t mine = 0;
 #pragma unroll
   for (uint32_t q = 0; q < 10; ++q) mine = lane == q ? tot[q] : mine;
-  if (kChain) {  // the caller's totals are zeroed for this launch once the flag holds its epoch
+  if (kChain && ch.flag) {  // the caller's totals are zeroed once the flag holds the epoch
     while (__hip_atomic_load(ch.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ch.epoch)
       __builtin_amdgcn_s_sleep(1);
     // (kWT: the zeroes were stored write-through and drained before the flag, and the adds below
@@ -1195,7 +1202,7 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
 // r stored). Round r = events [eoff[r], eoff[r+1]), spans of 256 (coh_stream_wave, chained form:
 // granules and the totals flag tagged with epoch epoch0 + r in CohChainState's ws), span s on
 // wave s mod (4 x gridDim.x), each wave's spans in ascending order, so a look-back only waits
-// for running waves. Totals: row r of `totals` (10 u64), zeroed by span 0's wave. The page-table
+// for running waves. Totals: row r of `totals` (10 u64, zeroed by the launcher). The page-table
 // words one round hands the next are stored write-through and gathered past L1 (kWT), so the
 // barrier between rounds needs no fence.
 __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__ pt,
@@ -1213,7 +1220,6 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
   const uint64_t nw = (uint64_t)gridDim.x * 4, wv = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   uint64_t* const status = ws + kCohChainStatus;
-  uint32_t* const flag = reinterpret_cast<uint32_t*>(ws + kCohChainFlag);
   // the events of this wave's first span of round r, loaded before round r - 1's barrier
   // (events are never written in the launch: no hand-off)
   SpanPre pre;
@@ -1235,14 +1241,10 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
     GDSM_RSTAMP(1, r, 0);
     const uint64_t e0 = (uint64_t)eoff[r], n = (uint64_t)eoff[r + 1] - e0;
     const uint64_t nb = (n + kSpan - 1) / kSpan, nfull = n / kSpan;
-    const CohChain ch{epoch0 + r, flag};
+    // (the launcher zeroed every round's totals: no flag to wait for before adding to them)
+    const CohChain ch{epoch0 + r, nullptr, r};
     unsigned long long* const tot = totals + 10ull * r;
     for (uint64_t b = wv; b < nb; b += nw) {
-      if (b == 0) {  // span 0's wave: the round's totals zeroed (drained), then the flag raised
-        if (lane < 10) st_wt(tot + lane, 0ull);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(flag, ch.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
       const bool up = b == wv && have_pre;
       if (b < nfull)
         coh_stream_wave<kSCSmall, true, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
@@ -1252,7 +1254,6 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
                                                      err, n_nodes, tot, ch, up, pre);
     }
     have_pre = r + 1 < n_rounds && prefetch(r + 1);
-    if (n == 0 && wv == 0 && lane < 10) st_wt(tot + lane, 0ull);
     GDSM_RSTAMP(1, r, 1);
     grid_barrier_wt(bar, (r + 1) * gridDim.x, err, kErrRoundsBarrier);
   }
@@ -1276,6 +1277,7 @@ hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   const uint32_t epoch0 = chain->epoch;
   chain->epoch = 0;
   hipError_t e = hipMemsetAsync(bar, 0, sizeof(uint32_t), s);
+  if (e == hipSuccess) e = hipMemsetAsync(totals, 0, 80ull * n_rounds, s);  // every round's row
   if (e != hipSuccess) return e;
   ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
   hipLaunchKernelGGL(rounds_fold_kernel, dim3(grid), dim3(256), 0, s, pt, n_pages, events, eoff,

@@ -517,6 +517,11 @@ __device__ __forceinline__ bool twin_ok(const IdGuard& g, uint64_t pj) {
   return g.n_pages == 0 || pj < g.n_pages;
 }
 
+__device__ __forceinline__ uint64_t guarded_value(uint32_t p, uint64_t n_pages, uint32_t& bad) {
+  bad |= p >= n_pages ? 1u : 0u;
+  return p < n_pages ? p : n_pages;
+}
+
 __device__ __forceinline__ uint64_t guarded_id(const uint32_t* __restrict__ ids, uint64_t i,
                                                uint64_t n_pages, uint32_t& bad) {
   const uint32_t p = ids[i];
@@ -854,11 +859,28 @@ __global__ __launch_bounds__(kSolo ? 64 * kSoloUnits : kChainW ? 64 * kChainW : 
 // workgroup, so the look-back only ever waits for running workgroups).
 // A round's writes for release_page_wg<..., kFuse>: copy descriptors [d0, d1) of desc, each
 // (dst, src, bytes) 8-B aligned; `covered` counts the 8-B words laid onto released pages.
+// (Holding a round's first 8 descriptors in registers, loaded a round ahead, measured ~0.6 us
+// per round SLOWER in the release than these scalar-cached loads: profiles/r06_rounds_ab.txt.)
 struct RoundWrites {
   const uint64_t* desc;
   uint64_t d0, d1;
   unsigned long long* covered;
 };
+
+// Lays descriptor (dst, src, bytes) onto the 16-B CURRENT chunk at address a: the 8-B halves
+// it covers (bit h of wm) take their bytes from src.
+__device__ __forceinline__ void lay_desc(uint64_t a, uint64_t dst, uint64_t src, uint64_t bytes,
+                                         uint64_t (&hv)[2], uint32_t& wm) {
+  if (a + 16 <= dst || a >= dst + bytes) return;
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint64_t ha = a + 8 * h;
+    if (ha >= dst && ha + 8 <= dst + bytes) {
+      hv[h] = *reinterpret_cast<const uint64_t*>(src + (ha - dst));
+      wm |= 1u << h;
+    }
+  }
+}
 
 // kWT: every store write-through and the page loads past L1 (st_wt / ld_wt16): the persistent
 // rounds grid hands CURRENT, TWIN, REPLICA and the stream from one workgroup to another with no
@@ -871,7 +893,7 @@ __device__ __forceinline__ void release_page_wg(
     const uint64_t u, const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit& sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard& g,
-    const RoundWrites& rw = RoundWrites{}) {
+    const RoundWrites& rw = RoundWrites{}, const int64_t pre_id = -1) {
   uint8_t* const twin_w = const_cast<uint8_t*>(twin);  // (kRetwin: see diff_single_kernel)
   __shared__ uint32_t edge_first[4], edge_last[4], tot[4], lastst[4];
   __shared__ uint64_t rec_at;
@@ -881,7 +903,11 @@ __device__ __forceinline__ void release_page_wg(
   const uint64_t n = sp.first[1] - sp.first[0];
   uint32_t bad = 0;
   const uint64_t i = sp.first[0] + u;
-  const uint64_t pj = ids ? (g.ids ? guarded_id(ids, i, g.n_pages, bad) : ids[i]) : i;
+  // (pre_id >= 0: the list entry, loaded ahead by the caller)
+  const uint64_t pj =
+      pre_id >= 0 ? (g.ids ? guarded_value((uint32_t)pre_id, g.n_pages, bad) : (uint64_t)pre_id)
+      : ids       ? (g.ids ? guarded_id(ids, i, g.n_pages, bad) : ids[i])
+                  : i;
   const uint64_t cap = sp.cap[0];
   const bool ample = kRetwin && cap >= n * GDSM_MAX_RECORD;
   const uint32_t ch = w * 64 + lane;  // this lane's chunk of the page
@@ -891,18 +917,8 @@ __device__ __forceinline__ void release_page_wg(
     const uint64_t a = reinterpret_cast<uint64_t>(cur + pj * kPage + ch * 16u);
     uint32_t wm = 0;  // bit h: 8-B half h of the chunk written this round
     uint64_t hv[2] = {(uint64_t)c.x | ((uint64_t)c.y << 32), (uint64_t)c.z | ((uint64_t)c.w << 32)};
-    for (uint64_t d = rw.d0; d < rw.d1; ++d) {
-      const uint64_t dst = rw.desc[3 * d], src = rw.desc[3 * d + 1], bytes = rw.desc[3 * d + 2];
-      if (a + 16 <= dst || a >= dst + bytes) continue;
-#pragma unroll
-      for (uint32_t h = 0; h < 2; ++h) {
-        const uint64_t ha = a + 8 * h;
-        if (ha >= dst && ha + 8 <= dst + bytes) {
-          hv[h] = *reinterpret_cast<const uint64_t*>(src + (ha - dst));
-          wm |= 1u << h;
-        }
-      }
-    }
+    for (uint64_t d = rw.d0; d < rw.d1; ++d)
+      lay_desc(a, rw.desc[3 * d], rw.desc[3 * d + 1], rw.desc[3 * d + 2], hv, wm);
     if (wm) {
       c = make_uint4((uint32_t)hv[0], (uint32_t)(hv[0] >> 32), (uint32_t)hv[1],
                      (uint32_t)(hv[1] >> 32));
@@ -1898,35 +1914,55 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
   // bar[0]: barrier arrivals; bar[2..3]: the words laid onto released pages minus the words
   // the descriptors hold (0 at the end, else a write fell outside the released pages)
   unsigned long long* const covered = reinterpret_cast<unsigned long long*>(bar + 2);
+  // workgroup 0's first wave accounts for each round's descriptors (their 8-B words, their
+  // alignment), lane-parallel, loaded one round ahead so the loads wait out a barrier
+  const bool acct = blockIdx.x == 0 && threadIdx.x < 64;
+  uint32_t acct_words = 0, acct_mis = 0;
+  auto acct_load = [&](uint32_t r) {
+    acct_words = acct_mis = 0;
+    for (uint64_t d = (uint64_t)doff[r] + threadIdx.x; d < (uint64_t)doff[r + 1]; d += 64) {
+      const uint64_t dst = desc[3 * d], src = desc[3 * d + 1], bytes = desc[3 * d + 2];
+      acct_words += (uint32_t)(bytes / 8);
+      acct_mis |= (uint32_t)((dst | src | bytes) & 7u);
+    }
+  };
+  if (acct && n_rounds) acct_load(0);
+  // this workgroup's first list entry of round r, loaded a round ahead (a uniform scalar load:
+  // the lists are never written in the launch), so the release's first loads go out at once
+  RoundWrites rw{desc, 0, 0, covered};
+  int64_t next_id = -1;
+  auto load_ahead = [&](uint32_t r) {
+    const uint64_t a = (uint64_t)off[r];
+    next_id = blockIdx.x < (uint64_t)off[r + 1] - a ? (int64_t)ids[a + blockIdx.x] : -1;
+  };
+  if (n_rounds) load_ahead(0);
   uint32_t phase = 0;
   for (uint32_t r = 0; r < n_rounds; ++r) {
     GDSM_RSTAMP(0, r, 0);
     const uint64_t d0 = (uint64_t)doff[r], d1 = (uint64_t)doff[r + 1];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      unsigned long long words = 0;
-      uint32_t misaligned = 0;
-      for (uint64_t d = d0; d < d1; ++d) {
-        words += desc[3 * d + 2] / 8;
-        misaligned |= (uint32_t)((desc[3 * d] | desc[3 * d + 1] | desc[3 * d + 2]) & 7u);
-      }
-      if (words) atomicAdd(covered, 0ull - words);
-      if (misaligned && g.err) atomicOr(g.err, kErrRoundsWrites);
+    if (acct) {
+      const uint32_t words = wave_sum(acct_words);
+      if (threadIdx.x == 0 && words) atomicAdd(covered, 0ull - (unsigned long long)words);
+      if (__ballot(acct_mis != 0) && threadIdx.x == 0 && g.err) atomicOr(g.err, kErrRoundsWrites);
     }
     const uint64_t a = (uint64_t)off[r], n = (uint64_t)off[r + 1] - a;
     DiffSplit rs = sp;
     rs.first[0] = 0;
     rs.first[1] = n;
     rs.epoch = epoch0 + r;
-    const RoundWrites rw{desc, d0, d1, covered};
+    rw.d0 = d0;
+    rw.d1 = d1;
     GDSM_RSTAMP(0, r, 1);
     GDSM_RSTAMP(0, r, 2);
     for (uint64_t u = blockIdx.x; u < n; u += gridDim.x) {
       release_page_wg<true, true, true, true>(u, twin, cur, ids + a, rs, ws, target, tids + a, g,
-                                              rw);
+                                              rw, u == blockIdx.x ? next_id : -1);
       __syncthreads();  // (the page's LDS exchange is reused by the workgroup's next page)
     }
     if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) st_wt(rs.rec_off[0], (uint64_t)0);
     GDSM_RSTAMP(0, r, 3);
+    if (acct && r + 1 < n_rounds) acct_load(r + 1);
+    if (r + 1 < n_rounds) load_ahead(r + 1);  // (landed by the barrier's end)
     grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && g.err &&

@@ -1,7 +1,7 @@
 """Where a gdsm_rounds round's time goes (measurement only; needs the -DGDSM_ROUNDS_STAMPS build:
 scripts/dev/build_variant.sh lib_st -DGDSM_ROUNDS_STAMPS, run with GDSM_LIB=gallocy_amd/lib_st/
 libgdsm.so). Workgroup 0's s_memtime stamps per round (shader clock; us at 2.4 GHz): page data
-[round start, copies done, barrier 1 done, release done] and page table [round start, fold done],
+[round start, copies done, barrier 1 done, release done] and page table [round start, fold done, span 0 published, span 0 looked back],
 medians over the rounds.  Usage: rounds_stamps.py NODES"""
 import ctypes as C
 import sys
@@ -35,3 +35,5 @@ print("page data: copies", us(d[:, 1] - d[:, 0]), "barrier 1", us(d[:, 2] - d[:,
       "round", us(d[1:, 0] - d[:-1, 0]))
 print("page table: fold", us(f[:, 1] - f[:, 0]), "barrier", us(f[1:, 0] - f[:-1, 1]),
       "round", us(f[1:, 0] - f[:-1, 0]))
+print("  span 0 of the fold: loads + gathers + scan", us(f[:, 2] - f[:, 0]),
+      "look-back", us(f[:, 3] - f[:, 2]), "tail (corrections, totals)", us(f[:, 1] - f[:, 3]))
