@@ -778,7 +778,8 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
                                                 unsigned long long* __restrict__ totals,
                                                 const CohChain ch = CohChain{},
                                                 const bool use_pre = false,
-                                                const SpanPre pre = SpanPre{}) {
+                                                const SpanPre pre = SpanPre{},
+                                                uint32_t* const tot_acc = nullptr) {
   const uint64_t tag = kChain ? (uint64_t)ch.epoch << 32 : 0ull;
   // a status granule as this launch sees it (kChain: an earlier launch's reads as unpublished)
   auto ld_status = [&](int64_t q) {
@@ -1141,7 +1142,9 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
     else
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
-  if (totals) {
+  if (tot_acc) {  // (the caller adds them once its round's hand-offs are drained)
+    *tot_acc += mine;
+  } else if (totals) {
     if (lane < 10 && mine) atomicAdd(totals + lane, (unsigned long long)mine);
   } else if (lane < 10) {
     partial[b * 10 + lane] = mine;
@@ -1200,11 +1203,13 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
 // ---- DSM rounds on the device (gdsm_rounds, page-table side): one persistent launch folds
 // every round's events in turn, a grid barrier between rounds (round r + 1 reads the words round
 // r stored). Round r = events [eoff[r], eoff[r+1]), spans of 256 (coh_stream_wave, chained form:
-// granules and the totals flag tagged with epoch epoch0 + r in CohChainState's ws), span s on
-// wave s mod (4 x gridDim.x), each wave's spans in ascending order, so a look-back only waits
-// for running waves. Totals: row r of `totals` (10 u64, zeroed by the launcher). The page-table
-// words one round hands the next are stored write-through and gathered past L1 (kWT), so the
-// barrier between rounds needs no fence.
+// granules tagged with epoch epoch0 + r in CohChainState's ws), span s on wave s mod
+// (4 x gridDim.x), each wave's spans in ascending order, so a look-back only waits for running
+// waves. Totals: row r of `totals` (10 u64, zeroed by the launcher), a wave's spans summed in
+// registers and added after the workgroup's arrival at the barrier (the next round never reads
+// them, so the barrier's drain does not wait for those atomics). The page-table words one round
+// hands the next are stored write-through and gathered past L1 (kWT), so the barrier between
+// rounds needs no fence.
 __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__ pt,
                                                           uint64_t n_pages,
                                                           const uint64_t* __restrict__ ev,
@@ -1223,8 +1228,11 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
   // the events of this wave's first span of round r, loaded before round r - 1's barrier
   // (events are never written in the launch: no hand-off)
   SpanPre pre;
+  uint64_t ne0 = 0, nn = 0;  // round r's event bounds, loaded with its events
   auto prefetch = [&](uint32_t r) {
     const uint64_t e0 = (uint64_t)eoff[r], n = (uint64_t)eoff[r + 1] - e0;
+    ne0 = e0;
+    nn = n;
     const uint64_t lo = wv * kSpan;
     if (lo >= n) return false;
 #pragma unroll
@@ -1239,23 +1247,30 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
   bool have_pre = n_rounds > 0 && prefetch(0);
   for (uint32_t r = 0; r < n_rounds; ++r) {
     GDSM_RSTAMP(1, r, 0);
-    const uint64_t e0 = (uint64_t)eoff[r], n = (uint64_t)eoff[r + 1] - e0;
+    if (!have_pre) {
+      ne0 = (uint64_t)eoff[r];
+      nn = (uint64_t)eoff[r + 1] - ne0;
+    }
+    const uint64_t e0 = ne0, n = nn;
     const uint64_t nb = (n + kSpan - 1) / kSpan, nfull = n / kSpan;
     // (the launcher zeroed every round's totals: no flag to wait for before adding to them)
     const CohChain ch{epoch0 + r, nullptr, r};
     unsigned long long* const tot = totals + 10ull * r;
+    uint32_t acc = 0;  // lane q < 10: this wave's spans' total q
     for (uint64_t b = wv; b < nb; b += nw) {
       const bool up = b == wv && have_pre;
       if (b < nfull)
         coh_stream_wave<kSCSmall, true, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
-                                                    err, n_nodes, tot, ch, up, pre);
+                                                    err, n_nodes, tot, ch, up, pre, &acc);
       else
         coh_stream_wave<kSCSmall, false, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
-                                                     err, n_nodes, tot, ch, up, pre);
+                                                     err, n_nodes, tot, ch, up, pre, &acc);
     }
-    have_pre = r + 1 < n_rounds && prefetch(r + 1);
     GDSM_RSTAMP(1, r, 1);
-    grid_barrier_wt(bar, (r + 1) * gridDim.x, err, kErrRoundsBarrier);
+    grid_arrive_wt(bar);
+    have_pre = r + 1 < n_rounds && prefetch(r + 1);
+    if (lane < 10 && acc) atomicAdd(tot + lane, (unsigned long long)acc);
+    grid_wait_wt(bar, (r + 1) * gridDim.x, err, kErrRoundsBarrier);
   }
 }
 

@@ -166,12 +166,17 @@ __device__ __forceinline__ void wave_lds_sync() {
 // arrivals) is an agent atomic polled by sc1 loads. A wait that never ends (a workgroup not
 // resident: never expected, the launcher sizes the grid below the occupancy) sets `err_bit` in
 // *err and lets the workgroup go on, so the grid always drains.
-__device__ __forceinline__ void grid_barrier_wt(uint32_t* __restrict__ bar, uint32_t target,
-                                                uint32_t* __restrict__ err, uint32_t err_bit) {
+// Split form: grid_arrive_wt drains the workgroup's stores and counts it in; loads issued between
+// it and grid_wait_wt (the next round's inputs) overlap the wait instead of delaying the arrival
+// (gfx9's vmcnt counts loads and stores alike, so a load issued before the drain is waited for).
+__device__ __forceinline__ void grid_arrive_wt(uint32_t* __restrict__ bar) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void grid_wait_wt(uint32_t* __restrict__ bar, uint32_t target,
+                                             uint32_t* __restrict__ err, uint32_t err_bit) {
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t spins = 0;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
@@ -185,6 +190,11 @@ __device__ __forceinline__ void grid_barrier_wt(uint32_t* __restrict__ bar, uint
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps loads below)
   __syncthreads();
+}
+__device__ __forceinline__ void grid_barrier_wt(uint32_t* __restrict__ bar, uint32_t target,
+                                                uint32_t* __restrict__ err, uint32_t err_bit) {
+  grid_arrive_wt(bar);
+  grid_wait_wt(bar, target, err, err_bit);
 }
 
 // Measurement builds only (-DGDSM_ROUNDS_STAMPS): s_memtime stamps of gdsm_rounds' grids,

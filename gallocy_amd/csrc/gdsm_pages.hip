@@ -1927,31 +1927,35 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
     }
   };
   if (acct && n_rounds) acct_load(0);
-  // this workgroup's first list entry of round r, loaded a round ahead (a uniform scalar load:
-  // the lists are never written in the launch), so the release's first loads go out at once
+  // round r's list and descriptor bounds and this workgroup's first list entry, loaded a round
+  // ahead (uniform scalar loads: the lists are never written in the launch), so the release's
+  // first loads go out as soon as the barrier ends
   RoundWrites rw{desc, 0, 0, covered};
   int64_t next_id = -1;
+  uint64_t na = 0, nn = 0, nd0 = 0, nd1 = 0;
   auto load_ahead = [&](uint32_t r) {
-    const uint64_t a = (uint64_t)off[r];
-    next_id = blockIdx.x < (uint64_t)off[r + 1] - a ? (int64_t)ids[a + blockIdx.x] : -1;
+    na = (uint64_t)off[r];
+    nn = (uint64_t)off[r + 1] - na;
+    nd0 = (uint64_t)doff[r];
+    nd1 = (uint64_t)doff[r + 1];
+    next_id = blockIdx.x < nn ? (int64_t)ids[na + blockIdx.x] : -1;
   };
   if (n_rounds) load_ahead(0);
   uint32_t phase = 0;
   for (uint32_t r = 0; r < n_rounds; ++r) {
     GDSM_RSTAMP(0, r, 0);
-    const uint64_t d0 = (uint64_t)doff[r], d1 = (uint64_t)doff[r + 1];
+    const uint64_t a = na, n = nn;
+    rw.d0 = nd0;
+    rw.d1 = nd1;
     if (acct) {
       const uint32_t words = wave_sum(acct_words);
       if (threadIdx.x == 0 && words) atomicAdd(covered, 0ull - (unsigned long long)words);
       if (__ballot(acct_mis != 0) && threadIdx.x == 0 && g.err) atomicOr(g.err, kErrRoundsWrites);
     }
-    const uint64_t a = (uint64_t)off[r], n = (uint64_t)off[r + 1] - a;
     DiffSplit rs = sp;
     rs.first[0] = 0;
     rs.first[1] = n;
     rs.epoch = epoch0 + r;
-    rw.d0 = d0;
-    rw.d1 = d1;
     GDSM_RSTAMP(0, r, 1);
     GDSM_RSTAMP(0, r, 2);
     for (uint64_t u = blockIdx.x; u < n; u += gridDim.x) {
@@ -1961,9 +1965,10 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
     }
     if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) st_wt(rs.rec_off[0], (uint64_t)0);
     GDSM_RSTAMP(0, r, 3);
+    grid_arrive_wt(bar);
     if (acct && r + 1 < n_rounds) acct_load(r + 1);
     if (r + 1 < n_rounds) load_ahead(r + 1);  // (landed by the barrier's end)
-    grid_barrier_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
+    grid_wait_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && g.err &&
       __hip_atomic_load(covered, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
