@@ -895,8 +895,8 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   // the offsets on the device (behind them the grid-barrier word, 256-B aligned)
   const uint64_t ob = 8ull * (n_rounds + 1);
   const uint64_t bar_at = (2 * ob + 255) & ~255ull;
-  int rc = ensure(data, &data->rounds_ws, &data->rounds_ws_bytes, bar_at + 256);
-  if (!rc) rc = ensure(pt, &pt->rounds_ws, &pt->rounds_ws_bytes, bar_at + 256);
+  int rc = ensure(data, &data->rounds_ws, &data->rounds_ws_bytes, bar_at + gdsm::kRoundsBarBytes);
+  if (!rc) rc = ensure(pt, &pt->rounds_ws, &pt->rounds_ws_bytes, bar_at + gdsm::kRoundsBarBytes);
   if (rc) return rc;
   GDSM_TRY(hipMemcpyAsync(data->rounds_ws, id_off, ob, hipMemcpyHostToDevice, data->stream));
   GDSM_TRY(hipMemcpyAsync(data->rounds_ws + ob, desc_off, ob, hipMemcpyHostToDevice, data->stream));
@@ -906,8 +906,15 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   // need (checked)
   const uint64_t gd_n = std::min<uint64_t>(std::max<uint64_t>(max_ids, 1), 256);
   const uint64_t gp_n = std::min<uint64_t>(std::max<uint64_t>((max_ev + 1023) / 1024, 1), 256);
-  if (gd_n > resident_grid(gdsm::rounds_data_kernel_ptr()) ||
-      gp_n > resident_grid(gdsm::rounds_fold_kernel_ptr()))
+  // small rounds (every round's workgroups fit one XCD, one per CU) run on one-XCD teams: a grid of
+  // 8x the workgroups, the members being those on the first one's XCD (about 1 in 8), their
+  // hand-offs meeting in that XCD's L2. GDSM_ROUNDS_XCD=0 / 1 forces the choice (A/B runs).
+  const char* xe = getenv("GDSM_ROUNDS_XCD");  // (read per call: tests switch it)
+  const int xcd_env = xe && *xe ? (xe[0] == '1' ? 1 : 0) : -1;
+  const bool xcd = xcd_env == 1 || (xcd_env < 0 && gd_n <= 32 && gp_n <= 32);
+  const uint64_t gd_grid = xcd ? 8 * gd_n : gd_n, gp_grid = xcd ? 8 * gp_n : gp_n;
+  if (gd_grid > resident_grid(gdsm::rounds_data_kernel_ptr(xcd)) ||
+      gp_grid > resident_grid(gdsm::rounds_fold_kernel_ptr(xcd)))
     return -EINVAL;
   gdsm::DiffChain& ch = data->chain;
   if (ch.epoch == 0 || ch.epoch + n_rounds >= (1u << 30)) {
@@ -918,16 +925,17 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   ch.epoch = 0;  // the next chained release zeroes the workspace again (its ticket sets restart)
   GDSM_TRY(gdsm::launch_rounds_fold(
       pt->coh_pt, pt->n_pages, pt->n_nodes, events,
-      reinterpret_cast<const int64_t*>(pt->rounds_ws), n_rounds, (uint32_t)gp_n, totals, pt->err,
-      &pt->coh_chain, reinterpret_cast<uint32_t*>(pt->rounds_ws + bar_at), pt->stream, pt->P()));
+      reinterpret_cast<const int64_t*>(pt->rounds_ws), n_rounds, (uint32_t)gp_grid, totals,
+      pt->err, &pt->coh_chain, reinterpret_cast<uint32_t*>(pt->rounds_ws + bar_at), xcd,
+      pt->stream, pt->P()));
   runs->n = (uint64_t)(id_off[n_rounds] - id_off[n_rounds - 1]);
   GDSM_TRY(gdsm::launch_rounds_data(
       data->arena[GDSM_TWIN], data->arena[GDSM_CURRENT], ids, home,
       reinterpret_cast<const int64_t*>(data->rounds_ws), desc,
-      reinterpret_cast<const int64_t*>(data->rounds_ws + ob), n_rounds, (uint32_t)gd_n,
+      reinterpret_cast<const int64_t*>(data->rounds_ws + ob), n_rounds, (uint32_t)gd_grid,
       runs->rec_off, runs->data, runs->cap, ch.ws, data->arena[GDSM_REPLICA], data->n_pages,
-      data->err, epoch0, reinterpret_cast<uint32_t*>(data->rounds_ws + bar_at), data->stream,
-      data->P()));
+      data->err, epoch0, reinterpret_cast<uint32_t*>(data->rounds_ws + bar_at), xcd,
+      data->stream, data->P()));
   return 0;
 }
 

@@ -28,6 +28,21 @@
 namespace gdsm {
 
 constexpr uint32_t kConst = 1u << 31;
+// Measurement builds only (-DGDSM_ROUNDS_STAMPS): per span of each gdsm_rounds round (spans < 32,
+// rounds < 1024), lane 0's s_memtime at [0] entry, [1] aggregate published, [2] look-back done,
+// [3] exit; read by gdsm_debug_fold_spans.
+#ifdef GDSM_ROUNDS_STAMPS
+__device__ unsigned long long g_fold_spans[1024][32][4];
+#define GDSM_SSTAMP(r_, b_, i_)                                                   \
+  do {                                                                           \
+    if (lane == 0 && (r_) < 1024 && (b_) < 32)                                   \
+      g_fold_spans[r_][b_][i_] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#else
+#define GDSM_SSTAMP(r_, b_, i_) \
+  do {                          \
+  } while (0)
+#endif
 #ifdef GDSM_COH_STAMPS
 __device__ unsigned long long g_coh_stamps[8192 * 4 * 8];
 // Fold kernel: every 16th block b (by ticket), lane 0: [0] entry, [1] events in LDS, [2] walk
@@ -768,8 +783,10 @@ struct SpanPre {
 
 // kWT (gdsm_rounds' persistent grid): page-table words stored write-through and gathered past
 // L1 (st_wt / ld_wt), since the next round's waves on other XCDs read them after a fence-free
-// barrier. pre: the span's events already loaded (kSC <= kSCSmall), else loaded here.
-template <uint32_t kSC, bool kFull, bool kChain = false, bool kWT = false>
+// barrier; kL2 (with kWT, a one-XCD team): stored plain and counted by L2 atomics instead, the
+// team's gathers finding them in its L2. pre: the span's events already loaded (kSC <= kSCSmall),
+// else loaded here.
+template <uint32_t kSC, bool kFull, bool kChain = false, bool kWT = false, bool kL2 = false>
 __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint64_t n_pages,
                                                 const uint64_t* __restrict__ ev, uint64_t n,
                                                 uint64_t b, uint64_t* __restrict__ status,
@@ -787,7 +804,9 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
     return (kChain && ((x >> 32) & 0x1FFFFFFFull) != ch.epoch) ? 0ull : x;
   };
   constexpr uint32_t kSpan = 64 * kSC;
+  constexpr bool kWTs = kWT && !kL2;  // write-through stores
   const uint32_t lane = lane_id();
+  if (kWT) GDSM_SSTAMP(ch.round, b, 0);
   const uint64_t lo = b * kSpan;
   const uint64_t hi = lo + kSpan;
   const uint32_t nev = kFull ? kSpan : (uint32_t)min((uint64_t)kSpan, n - lo);
@@ -889,7 +908,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
               oval[j < kDN ? j : 0] = wv;
             }
           } else if (lane == 0 && open_page < n_pages) {
-            st_<kWT>(pt + open_page, wv);
+            st_<kWTs>(pt + open_page, wv);
           }
         } else {
           has_d = true;
@@ -953,7 +972,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
             dpg[j < kDN ? j : 0] = pg;
             dval[j < kDN ? j : 0] = wv;
           } else {
-            st_<kWT>(pt + pg, wv);
+            st_<kWTs>(pt + pg, wv);
           }
         }
         if (!open_local) {
@@ -998,7 +1017,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
           lpg = last_page;
           lval = wv;
         } else {
-          st_<kWT>(pt + last_page, wv);
+          st_<kWTs>(pt + last_page, wv);
         }
       }
     } else {
@@ -1013,7 +1032,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
         apg = last_page;
         acnt = open_cnt;
       } else {
-        atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, open_cnt);
+        add_u32<kL2>(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, open_cnt);
       }
     }
   } else {
@@ -1024,6 +1043,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   const uint32_t agg = (carry & kSF) ? (kConst | s_state(carry)) : ((carry >> 20) & 0xFFu);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   if (kWT) GDSM_RSTAMP(1, ch.round, 2);
+  if (kWT) GDSM_SSTAMP(ch.round, b, 1);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (lane == 0)
     __hip_atomic_store(status + b, (b == 0 ? kFIncl : kFAgg) | (any_head ? kFHead : 0ull) | tag | agg,
@@ -1031,11 +1051,11 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   if (kDefer) {  // the held segment ends (pages inside this span: no other wave touches them)
 #pragma unroll
     for (uint32_t j = 0; j < kDN; ++j) {
-      if (opg[j] != ~0u) st_<kWT>(pt + opg[j], oval[j]);
-      if (dpg[j] != ~0u) st_<kWT>(pt + dpg[j], dval[j]);
+      if (opg[j] != ~0u) st_<kWTs>(pt + opg[j], oval[j]);
+      if (dpg[j] != ~0u) st_<kWTs>(pt + dpg[j], dval[j]);
     }
-    if (lpg != ~0u) st_<kWT>(pt + lpg, lval);
-    if (apg != ~0u) atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)apg + 1, acnt);
+    if (lpg != ~0u) st_<kWTs>(pt + lpg, lval);
+    if (apg != ~0u) add_u32<kL2>(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)apg + 1, acnt);
   }
   const bool ordered = has_d;
   uint32_t cur = 0;
@@ -1076,6 +1096,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
   }
 
   if (kWT) GDSM_RSTAMP(1, ch.round, 3);
+  if (kWT) GDSM_SSTAMP(ch.round, b, 2);
   // ---- the span's first segment, now that its incoming state `cur` is known
   uint32_t dfc = 0;                 // correction of the first segment's fault count
   uint32_t Fcorr_node_minus = 0;    // nodes whose probe read fault did not happen
@@ -1100,21 +1121,21 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
       const uint32_t word = (d_state & kSF) ? s_state(d_state) : (tcompose(cur, (d_state >> 20) & 0xFFu) & 0x7FFFFu);
       if (lane == 0 && d_page < n_pages) {
         uint32_t* pst = reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)d_page;
-        st_<kWT>(pst, word);
+        st_<kWTs>(pst, word);
         const uint32_t c = d_cnt + dfc;
-        if (c) atomicAdd(pst + 1, c);
+        if (c) add_u32<kL2>(pst + 1, c);
       }
     } else if (cont_first) {
       const uint32_t c = open_cnt + dfc;
       if (lane == 0 && c && last_page < n_pages)
-        atomicAdd(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, c);
+        add_u32<kL2>(reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)last_page + 1, c);
     }
   } else if (has_d || cont_first) {
     // no prefix (the span starts a page): the first segment was counted exactly
     if (has_d && lane == 0 && d_page < n_pages) {
       uint32_t* pst = reinterpret_cast<uint32_t*>(pt) + 2 * (uint64_t)d_page;
-      st_<kWT>(pst, s_state(d_state));
-      if (d_cnt) atomicAdd(pst + 1, d_cnt);
+      st_<kWTs>(pst, s_state(d_state));
+      if (d_cnt) add_u32<kL2>(pst + 1, d_cnt);
     }
   }
 
@@ -1150,6 +1171,7 @@ __device__ __forceinline__ void coh_stream_wave(uint64_t* __restrict__ pt, uint6
     partial[b * 10 + lane] = mine;
   }
   if (__ballot(bad != 0) && lane == 0) atomicOr(err, 2u);
+  if (kWT) GDSM_SSTAMP(ch.round, b, 3);
 }
 
 // Spans [0, nfull) are whole; a partial last span (nb > nfull) is walked by the wave that draws
@@ -1209,7 +1231,9 @@ __global__ __launch_bounds__(256) void coh_stream_kernel(uint64_t* __restrict__ 
 // registers and added after the workgroup's arrival at the barrier (the next round never reads
 // them, so the barrier's drain does not wait for those atomics). The page-table words one round
 // hands the next are stored write-through and gathered past L1 (kWT), so the barrier between
-// rounds needs no fence.
+// rounds needs no fence. kXcd: the rounds run on a one-XCD team (xcd_team, control words at
+// bar + 32), the page-table words stored plain and counted in that XCD's L2.
+template <bool kXcd>
 __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__ pt,
                                                           uint64_t n_pages,
                                                           const uint64_t* __restrict__ ev,
@@ -1222,7 +1246,11 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
                                                           uint32_t epoch0,
                                                           uint32_t* __restrict__ bar) {
   constexpr uint64_t kSpan = 64ull * kSCSmall;
-  const uint64_t nw = (uint64_t)gridDim.x * 4, wv = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const XcdTeam team = kXcd ? xcd_team(bar + 32, err, kErrRoundsBarrier)
+                            : XcdTeam{blockIdx.x, gridDim.x};
+  if (team.idx == ~0u) return;  // (workgroup-uniform: not on the team's XCD)
+  GDSM_RSTAMP_WG(team.idx == 0);
+  const uint64_t nw = (uint64_t)team.n * 4, wv = (uint64_t)team.idx * 4 + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
   uint64_t* const status = ws + kCohChainStatus;
   // the events of this wave's first span of round r, loaded before round r - 1's barrier
@@ -1260,26 +1288,31 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
     for (uint64_t b = wv; b < nb; b += nw) {
       const bool up = b == wv && have_pre;
       if (b < nfull)
-        coh_stream_wave<kSCSmall, true, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
-                                                    err, n_nodes, tot, ch, up, pre, &acc);
+        coh_stream_wave<kSCSmall, true, true, true, kXcd>(pt, n_pages, ev + e0, n, b, status,
+                                                          nullptr, err, n_nodes, tot, ch, up, pre,
+                                                          &acc);
       else
-        coh_stream_wave<kSCSmall, false, true, true>(pt, n_pages, ev + e0, n, b, status, nullptr,
-                                                     err, n_nodes, tot, ch, up, pre, &acc);
+        coh_stream_wave<kSCSmall, false, true, true, kXcd>(pt, n_pages, ev + e0, n, b, status,
+                                                           nullptr, err, n_nodes, tot, ch, up, pre,
+                                                           &acc);
     }
     GDSM_RSTAMP(1, r, 1);
-    grid_arrive_wt(bar);
+    grid_arrive_wt<kXcd>(bar);
     have_pre = r + 1 < n_rounds && prefetch(r + 1);
     if (lane < 10 && acc) atomicAdd(tot + lane, (unsigned long long)acc);
-    grid_wait_wt(bar, (r + 1) * gridDim.x, err, kErrRoundsBarrier);
+    grid_wait_wt(bar, (r + 1) * team.n, err, kErrRoundsBarrier);
   }
 }
 
-const void* rounds_fold_kernel_ptr() { return reinterpret_cast<const void*>(rounds_fold_kernel); }
+const void* rounds_fold_kernel_ptr(bool xcd) {
+  return xcd ? reinterpret_cast<const void*>(rounds_fold_kernel<true>)
+             : reinterpret_cast<const void*>(rounds_fold_kernel<false>);
+}
 
 hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                               const uint64_t* events, const int64_t* eoff, uint32_t n_rounds,
                               uint32_t grid, uint64_t* totals, uint32_t* err, CohChainState* chain,
-                              uint32_t* bar, hipStream_t s, Prof* prof) {
+                              uint32_t* bar, bool xcd, hipStream_t s, Prof* prof) {
   if (n_rounds == 0) return hipSuccess;
   if (!chain || !chain->ws) return hipErrorInvalidValue;
   // the rounds take epochs [epoch0, epoch0 + n_rounds); the chain is zeroed again afterwards by
@@ -1291,11 +1324,12 @@ hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
   }
   const uint32_t epoch0 = chain->epoch;
   chain->epoch = 0;
-  hipError_t e = hipMemsetAsync(bar, 0, sizeof(uint32_t), s);
+  hipError_t e = hipMemsetAsync(bar, 0, kRoundsBarBytes, s);  // arrivals + team words
   if (e == hipSuccess) e = hipMemsetAsync(totals, 0, 80ull * n_rounds, s);  // every round's row
   if (e != hipSuccess) return e;
   ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
-  hipLaunchKernelGGL(rounds_fold_kernel, dim3(grid), dim3(256), 0, s, pt, n_pages, events, eoff,
+  hipLaunchKernelGGL(xcd ? rounds_fold_kernel<true> : rounds_fold_kernel<false>, dim3(grid),
+                     dim3(256), 0, s, pt, n_pages, events, eoff,
                      n_rounds, chain->ws, err, n_nodes,
                      reinterpret_cast<unsigned long long*>(totals), epoch0, bar);
   return hipGetLastError();
@@ -1545,6 +1579,10 @@ hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t
 }  // namespace gdsm
 
 #ifdef GDSM_ROUNDS_STAMPS
+extern "C" int gdsm_debug_fold_spans(void* out, size_t bytes) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gdsm::g_fold_spans), bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -EIO;
+}
 extern "C" int gdsm_debug_round_stamps_pt(void* out, size_t bytes) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(gdsm::g_round_stamps), bytes, 0,
                              hipMemcpyDeviceToHost) == hipSuccess

@@ -50,6 +50,15 @@ __device__ __forceinline__ void st_(T* p, T v) {
   else
     *p = v;
 }
+// an add to a word other workgroups read: kL2 (every reader on this XCD) performed in the XCD's
+// L2 (workgroup scope: no sc1), else an agent-scope atomic
+template <bool kL2>
+__device__ __forceinline__ void add_u32(uint32_t* p, uint32_t v) {
+  if (kL2)
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    atomicAdd(p, v);
+}
 
 // ---- wave64 cross-lane primitives on DPP (VALU, no LDS traffic) -------------------------
 // gfx9-family DPP controls: row_shr:n = 0x110+n, row_bcast:15 = 0x142, row_bcast:31 = 0x143,
@@ -169,10 +178,18 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Split form: grid_arrive_wt drains the workgroup's stores and counts it in; loads issued between
 // it and grid_wait_wt (the next round's inputs) overlap the wait instead of delaying the arrival
 // (gfx9's vmcnt counts loads and stores alike, so a load issued before the drain is waited for).
+// kL2 (a one-XCD team, below): the arrival is added in the XCD's L2, where every member's sc1
+// polls read it.
+template <bool kL2 = false>
 __device__ __forceinline__ void grid_arrive_wt(uint32_t* __restrict__ bar) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    if (kL2)
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 __device__ __forceinline__ void grid_wait_wt(uint32_t* __restrict__ bar, uint32_t target,
                                              uint32_t* __restrict__ err, uint32_t err_bit) {
@@ -197,17 +214,80 @@ __device__ __forceinline__ void grid_barrier_wt(uint32_t* __restrict__ bar, uint
   grid_wait_wt(bar, target, err, err_bit);
 }
 
+// A one-XCD team of a persistent grid: of the launch's workgroups, those running on the XCD of
+// the workgroup that checked in first take part (member idx of n), the others leave at once. The
+// XCD is read from HW_REG_XCC_ID, so no dispatch order or placement is assumed; the members' hand-
+// offs then meet in that XCD's L2 (plain stores kept there, sc1 loads served from it, arrivals and
+// count adds performed there) instead of crossing to memory. ctl: 4 words zeroed before the launch
+// ([0] check-ins, [1] home XCC + 1, [2] members, [3] settled). A member waits for every
+// workgroup's check-in, so the launch must be resident at once (as every grid barrier needs).
+struct XcdTeam {
+  uint32_t idx, n;  // idx == ~0u: not a member
+};
+__device__ __forceinline__ XcdTeam xcd_team(uint32_t* __restrict__ ctl, uint32_t* __restrict__ err,
+                                            uint32_t err_bit) {
+  __shared__ uint32_t s_idx, s_n;
+  if (threadIdx.x == 0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 0xFu;
+    const uint32_t t = __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(ctl + 1, xcc + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t home, spins = 0;
+    while ((home = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {
+        atomicOr(err, err_bit);
+        break;
+      }
+    }
+    uint32_t idx = ~0u, n = 0;
+    if (home == xcc + 1u)
+      idx = __hip_atomic_fetch_add(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the member count is final before settling)
+    __hip_atomic_fetch_add(ctl + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (idx != ~0u) {
+      spins = 0;
+      while (__hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) {
+          atomicOr(err, err_bit);
+          idx = ~0u;
+          break;
+        }
+      }
+      n = __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_idx = idx;
+    s_n = n;
+  }
+  __syncthreads();
+  return XcdTeam{s_idx, s_n};
+}
+
 // Measurement builds only (-DGDSM_ROUNDS_STAMPS): s_memtime stamps of gdsm_rounds' grids,
 // workgroup 0, [kernel: 0 data, 1 page table][round][point], read by gdsm_debug_round_stamps
 // (gdsm_pages.hip's copy: the data side) and gdsm_debug_round_stamps_pt (the page-table side).
+// The stamping workgroup is the kernel's member 0 (GDSM_RSTAMP_WG, set and read by thread 0).
 #ifdef GDSM_ROUNDS_STAMPS
 static __device__ unsigned long long g_round_stamps[2][4096][4];  // (one copy per file)
+__device__ __forceinline__ uint32_t& gdsm_stamp_wg() {
+  __shared__ uint32_t f;
+  return f;
+}
+#define GDSM_RSTAMP_WG(is0_)                    \
+  do {                                          \
+    if (threadIdx.x == 0) gdsm_stamp_wg() = (is0_); \
+  } while (0)
 #define GDSM_RSTAMP(k_, r_, i_)                                                          \
   do {                                                                                  \
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (r_) < 4096)                             \
+    if (threadIdx.x == 0 && gdsm_stamp_wg() && (r_) < 4096)                             \
       g_round_stamps[k_][r_][i_] = __builtin_amdgcn_s_memtime();                        \
   } while (0)
 #else
+#define GDSM_RSTAMP_WG(is0_) \
+  do {                       \
+  } while (0)
 #define GDSM_RSTAMP(k_, r_, i_) \
   do {                          \
   } while (0)

@@ -78,17 +78,19 @@ struct DiffSplit {
 // One diff launch over arena pages [first[0], first[G]) (ids = identity) into sp's G streams.
 hipError_t launch_copy_batch(const uint64_t* desc, uint64_t n, hipStream_t s);
 // DSM rounds on the device (gdsm_rounds): the page-data side, one persistent launch of `grid`
-// workgroups: per round its copy descriptors [doff[r], doff[r+1]) of desc, a grid barrier, the
-// release of list entries [off[r], off[r+1]) of ids (home indices tids into target, re-twin),
-// a grid barrier. off / doff on the device; look-back granules in chain_ws (DiffChain layout)
-// with epochs epoch0 + r.
+// workgroups: per round the release of list entries [off[r], off[r+1]) of ids (home indices tids
+// into target, re-twin) with its copy descriptors [doff[r], doff[r+1]) of desc laid onto the
+// pages, then a grid barrier. off / doff on the device; look-back granules in chain_ws
+// (DiffChain layout) with epochs epoch0 + r; bar: kRoundsBarBytes zeroed by the launcher.
+// xcd: the rounds run on a one-XCD team of the grid (xcd_team: about grid / 8 members).
 hipError_t launch_rounds_data(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                               const uint32_t* tids, const int64_t* off, const uint64_t* desc,
                               const int64_t* doff, uint32_t n_rounds, uint32_t grid,
                               uint64_t* rec_off, uint8_t* data, uint64_t cap, uint64_t* chain_ws,
                               uint8_t* target, uint64_t n_pages, uint32_t* err, uint32_t epoch0,
-                              uint32_t* bar, hipStream_t s, Prof* prof = nullptr);
-const void* rounds_data_kernel_ptr();  // (for the occupancy query)
+                              uint32_t* bar, bool xcd, hipStream_t s, Prof* prof = nullptr);
+const void* rounds_data_kernel_ptr(bool xcd);  // (for the occupancy query)
+constexpr uint64_t kRoundsBarBytes = 256;      // a rounds grid's barrier and team words
 hipError_t launch_diff_split(const uint8_t* twin, const uint8_t* cur, DiffSplit sp, uint8_t* ws,
                              uint64_t ws_bytes, hipStream_t s, Prof* prof, uint32_t bpp_hint);
 hipError_t launch_apply(uint8_t* target, const uint32_t* ids, uint64_t n,
@@ -129,11 +131,12 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
 // DSM rounds on the device (gdsm_rounds): the page-table side, one persistent launch of `grid`
 // workgroups over n_rounds rounds (eoff: device, n_rounds + 1 event offsets; totals: 10 u64 per
 // round). Uses the chain's ws with epochs of its own; the chain restarts (zeroed) afterwards.
+// bar: kRoundsBarBytes zeroed by the launcher; xcd: a one-XCD team (as launch_rounds_data).
 hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                               const uint64_t* events, const int64_t* eoff, uint32_t n_rounds,
                               uint32_t grid, uint64_t* totals, uint32_t* err, CohChainState* chain,
-                              uint32_t* bar, hipStream_t s, Prof* prof = nullptr);
-const void* rounds_fold_kernel_ptr();  // (for the occupancy query)
+                              uint32_t* bar, bool xcd, hipStream_t s, Prof* prof = nullptr);
+const void* rounds_fold_kernel_ptr(bool xcd);  // (for the occupancy query)
 hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,
                              uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,
                              hipStream_t s);

@@ -887,14 +887,16 @@ __device__ __forceinline__ void lay_desc(uint64_t a, uint64_t dst, uint64_t src,
 // fences. kFuse: the round's writes (rw) that fall on this page are laid onto its CURRENT chunk
 // in registers and stored to CURRENT here, so the release needs no copy step and no barrier
 // before it (a word outside every released page is never written: `covered` falls short and the
-// launch flags it).
-template <bool kApply, bool kRetwin, bool kWT = false, bool kFuse = false>
+// launch flags it). kL2 (with kWT: a one-XCD team, xcd_team): the stores stay plain (kept in the
+// team's L2, where the sc1 loads of the other members find them).
+template <bool kApply, bool kRetwin, bool kWT = false, bool kFuse = false, bool kL2 = false>
 __device__ __forceinline__ void release_page_wg(
     const uint64_t u, const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const DiffSplit& sp, uint64_t* __restrict__ ws,
     uint8_t* __restrict__ target, const uint32_t* __restrict__ tids, const IdGuard& g,
     const RoundWrites& rw = RoundWrites{}, const int64_t pre_id = -1) {
   uint8_t* const twin_w = const_cast<uint8_t*>(twin);  // (kRetwin: see diff_single_kernel)
+  constexpr bool kWTs = kWT && !kL2;                  // write-through stores
   __shared__ uint32_t edge_first[4], edge_last[4], tot[4], lastst[4];
   __shared__ uint64_t rec_at;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -925,7 +927,7 @@ __device__ __forceinline__ void release_page_wg(
       uint8_t* const cw = const_cast<uint8_t*>(cur) + pj * kPage + ch * 16u;
 #pragma unroll
       for (uint32_t h = 0; h < 2; ++h)
-        if ((wm >> h) & 1u) st_<kWT>(reinterpret_cast<uint64_t*>(cw + 8 * h), hv[h]);
+        if ((wm >> h) & 1u) st_<kWTs>(reinterpret_cast<uint64_t*>(cw + 8 * h), hv[h]);
     }
     const uint32_t words = wave_sum((uint32_t)__popc(wm));
     if (words && lane == 0) atomicAdd(rw.covered, (unsigned long long)words);
@@ -933,9 +935,9 @@ __device__ __forceinline__ void release_page_wg(
   const uint32_t m = diffmask16(t, c);
   const uint64_t pt = kApply ? (tids ? (g.tids ? guarded_id(tids, i, g.n_pages, bad) : tids[i]) : pj)
                              : 0;  // page at target
-  if (kApply && m) store_masked16<kWT>(target + pt * kPage + ch * 16u, m, c);
+  if (kApply && m) store_masked16<kWTs>(target + pt * kPage + ch * 16u, m, c);
   if (ample && m && twin_ok(g, pj)) {
-    if (kWT)
+    if (kWTs)
       st_wt16(twin_w + pj * kPage + ch * 16u, c);
     else
       *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
@@ -1003,8 +1005,8 @@ __device__ __forceinline__ void release_page_wg(
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) {
-      st_<kWT>(sp.rec_off[0] + u + 1, (uint64_t)(excl + size));
-      if (u == 0) st_<kWT>(sp.rec_off[0], (uint64_t)0);
+      st_<kWTs>(sp.rec_off[0] + u + 1, (uint64_t)(excl + size));
+      if (u == 0) st_<kWTs>(sp.rec_off[0], (uint64_t)0);
       rec_at = excl;
     }
   }
@@ -1014,14 +1016,14 @@ __device__ __forceinline__ void release_page_wg(
   if (size) {
     uint8_t* rec = sp.data[0] + at;
     if (threadIdx.x == 0) {
-      st_<kWT>(reinterpret_cast<uint32_t*>(rec), NR);
-      for (uint32_t q = NP; q & 3u; ++q) st_<kWT>(rec + 4 + 4 * NR + q, (uint8_t)0);
+      st_<kWTs>(reinterpret_cast<uint32_t*>(rec), NR);
+      for (uint32_t q = NP; q & 3u; ++q) st_<kWTs>(rec + 4 + 4 * NR + q, (uint8_t)0);
     }
-    emit_chunk<kWT>(ch, st, en, m, max(cmax, from_prev_lane(mx)), carry + inc - v, c,
+    emit_chunk<kWTs>(ch, st, en, m, max(cmax, from_prev_lane(mx)), carry + inc - v, c,
                reinterpret_cast<uint32_t*>(rec + 4), rec + 4 + 4 * NR);
   }
   if (kRetwin && !ample && m && twin_ok(g, pj)) {
-    if (kWT)
+    if (kWTs)
       st_wt16(twin_w + pj * kPage + ch * 16u, c);
     else
       *reinterpret_cast<uint4*>(twin_w + pj * kPage + ch * 16u) = c;
@@ -1905,6 +1907,9 @@ __global__ __launch_bounds__(256) void copy_batch_kernel(const uint64_t* __restr
 // chain to be zeroed again by its next chained launch). Every byte one workgroup hands another
 // (CURRENT rows, TWIN, REPLICA, the stream) is stored write-through and the pages are loaded past
 // L1 (kWT), so the barriers need no L2 write-back or L1 invalidate.
+// kXcd: the rounds run on a one-XCD team (xcd_team, team control words at bar + 32): every hand-off
+// meets in that XCD's L2, so the stores stay plain and the arrivals are L2 atomics.
+template <bool kXcd>
 __global__ __launch_bounds__(256) void rounds_data_kernel(
     const uint8_t* __restrict__ twin, const uint8_t* __restrict__ cur,
     const uint32_t* __restrict__ ids, const uint32_t* __restrict__ tids,
@@ -1914,9 +1919,14 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
   // bar[0]: barrier arrivals; bar[2..3]: the words laid onto released pages minus the words
   // the descriptors hold (0 at the end, else a write fell outside the released pages)
   unsigned long long* const covered = reinterpret_cast<unsigned long long*>(bar + 2);
-  // workgroup 0's first wave accounts for each round's descriptors (their 8-B words, their
+  const XcdTeam team = kXcd ? xcd_team(bar + 32, g.err, kErrRoundsBarrier)
+                            : XcdTeam{blockIdx.x, gridDim.x};
+  if (team.idx == ~0u) return;  // (workgroup-uniform: not on the team's XCD)
+  const uint32_t wg = team.idx, nwg = team.n;
+  GDSM_RSTAMP_WG(team.idx == 0);
+  // member 0's first wave accounts for each round's descriptors (their 8-B words, their
   // alignment), lane-parallel, loaded one round ahead so the loads wait out a barrier
-  const bool acct = blockIdx.x == 0 && threadIdx.x < 64;
+  const bool acct = wg == 0 && threadIdx.x < 64;
   uint32_t acct_words = 0, acct_mis = 0;
   auto acct_load = [&](uint32_t r) {
     acct_words = acct_mis = 0;
@@ -1938,7 +1948,7 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
     nn = (uint64_t)off[r + 1] - na;
     nd0 = (uint64_t)doff[r];
     nd1 = (uint64_t)doff[r + 1];
-    next_id = blockIdx.x < nn ? (int64_t)ids[na + blockIdx.x] : -1;
+    next_id = wg < nn ? (int64_t)ids[na + wg] : -1;
   };
   if (n_rounds) load_ahead(0);
   uint32_t phase = 0;
@@ -1958,31 +1968,34 @@ __global__ __launch_bounds__(256) void rounds_data_kernel(
     rs.epoch = epoch0 + r;
     GDSM_RSTAMP(0, r, 1);
     GDSM_RSTAMP(0, r, 2);
-    for (uint64_t u = blockIdx.x; u < n; u += gridDim.x) {
-      release_page_wg<true, true, true, true>(u, twin, cur, ids + a, rs, ws, target, tids + a, g,
-                                              rw, u == blockIdx.x ? next_id : -1);
+    for (uint64_t u = wg; u < n; u += nwg) {
+      release_page_wg<true, true, true, true, kXcd>(u, twin, cur, ids + a, rs, ws, target,
+                                                    tids + a, g, rw, u == wg ? next_id : -1);
       __syncthreads();  // (the page's LDS exchange is reused by the workgroup's next page)
     }
-    if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) st_wt(rs.rec_off[0], (uint64_t)0);
+    if (n == 0 && wg == 0 && threadIdx.x == 0) st_<!kXcd>(rs.rec_off[0], (uint64_t)0);
     GDSM_RSTAMP(0, r, 3);
-    grid_arrive_wt(bar);
+    grid_arrive_wt<kXcd>(bar);
     if (acct && r + 1 < n_rounds) acct_load(r + 1);
     if (r + 1 < n_rounds) load_ahead(r + 1);  // (landed by the barrier's end)
-    grid_wait_wt(bar, ++phase * gridDim.x, g.err, kErrRoundsBarrier);
+    grid_wait_wt(bar, ++phase * nwg, g.err, kErrRoundsBarrier);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && g.err &&
+  if (wg == 0 && threadIdx.x == 0 && g.err &&
       __hip_atomic_load(covered, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
     atomicOr(g.err, kErrRoundsWrites);
 }
 
-const void* rounds_data_kernel_ptr() { return reinterpret_cast<const void*>(rounds_data_kernel); }
+const void* rounds_data_kernel_ptr(bool xcd) {
+  return xcd ? reinterpret_cast<const void*>(rounds_data_kernel<true>)
+             : reinterpret_cast<const void*>(rounds_data_kernel<false>);
+}
 
 hipError_t launch_rounds_data(const uint8_t* twin, const uint8_t* cur, const uint32_t* ids,
                               const uint32_t* tids, const int64_t* off, const uint64_t* desc,
                               const int64_t* doff, uint32_t n_rounds, uint32_t grid,
                               uint64_t* rec_off, uint8_t* data, uint64_t cap, uint64_t* chain_ws,
                               uint8_t* target, uint64_t n_pages, uint32_t* err, uint32_t epoch0,
-                              uint32_t* bar, hipStream_t s, Prof* prof) {
+                              uint32_t* bar, bool xcd, hipStream_t s, Prof* prof) {
   if (n_rounds == 0) return hipSuccess;
   DiffSplit sp{};
   sp.G = 1;
@@ -1990,11 +2003,13 @@ hipError_t launch_rounds_data(const uint8_t* twin, const uint8_t* cur, const uin
   sp.data[0] = data;
   sp.cap[0] = cap;
   const IdGuard g{ids, tids, nullptr, nullptr, n_pages, err};
-  hipError_t e = hipMemsetAsync(bar, 0, 16, s);  // arrivals + the coverage count
+  // arrivals, the coverage count and the team's control words (bar + 32)
+  hipError_t e = hipMemsetAsync(bar, 0, kRoundsBarBytes, s);
   if (e != hipSuccess) return e;
   ProfScope ps(prof, GDSM_PROF_DIFF, s);
-  hipLaunchKernelGGL(rounds_data_kernel, dim3(grid), dim3(256), 0, s, twin, cur, ids, tids, off,
-                     desc, doff, n_rounds, sp, chain_ws, target, g, epoch0, bar);
+  hipLaunchKernelGGL(xcd ? rounds_data_kernel<true> : rounds_data_kernel<false>, dim3(grid),
+                     dim3(256), 0, s, twin, cur, ids, tids, off, desc, doff, n_rounds, sp, chain_ws,
+                     target, g, epoch0, bar);
   return hipGetLastError();
 }
 

@@ -27,6 +27,35 @@ __device__ __forceinline__ void barrier_v(uint32_t* bar, uint32_t target, uint32
   __syncthreads();
 }
 
+// One XCD's workgroups only (blockIdx % 8 == 0 under round-robin dispatch, checked through
+// XCC_ID): arrivals as workgroup-scope atomics (performed in that XCD's L2), polls as sc0 loads.
+__device__ __forceinline__ void barrier_xcd(uint32_t* bar, uint32_t target, uint32_t* err) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+      if (++spins > (1u << 24)) {
+        atomicOr(err, 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void xcd_kernel(uint32_t* bar, uint32_t* err, uint32_t n,
+                                                  unsigned long long* t) {
+  if (blockIdx.x % 8 != 0) return;
+  uint32_t xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  if (threadIdx.x == 0 && (xcc & 0xF) != 0) atomicOr(err, 2u);  // not on XCD 0: the probe is void
+  const uint32_t parts = (gridDim.x + 7) / 8;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (uint32_t r = 0; r < n; ++r) barrier_xcd(bar, (r + 1) * parts, err);
+  if (blockIdx.x == 0 && threadIdx.x == 0) t[0] = __builtin_amdgcn_s_memtime() - t0;
+}
+
 template <int kMode>
 __global__ __launch_bounds__(256) void bar_kernel(uint32_t* bar, uint32_t* err, uint32_t n,
                                                   unsigned long long* t) {
@@ -78,6 +107,21 @@ int main() {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
       }
+    }
+  }
+  for (unsigned grid : {8u, 16u, 64u, 256u}) {
+    for (int rep = 0; rep < 2; ++rep) {
+      (void)hipMemset(bar, 0, 256);
+      (void)hipMemset(err, 0, 256);
+      hipLaunchKernelGGL(xcd_kernel, dim3(grid), dim3(256), 0, 0, bar, err, n, t);
+      (void)hipDeviceSynchronize();
+      unsigned long long ht = 0;
+      uint32_t he = 0;
+      (void)hipMemcpy(&ht, t, 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(&he, err, 4, hipMemcpyDeviceToHost);
+      if (rep == 1)
+        printf("one XCD, L2 atomics, %3u of %3u workgroups: %.3f us per barrier (memtime) err %u\n",
+               (grid + 7) / 8, grid, ht / 2400.0 / n, he);
     }
   }
   return 0;

@@ -28,23 +28,32 @@ def test_mmult_replay_end_to_end(ndim, nodes, graph, fused):
     (1000, 4, True, "python"), (257, 3, False, "python"), (64, 8, True, "python"),
     (1000, 4, True, "native2"), (257, 3, False, "native2"),
     (64, 1, True, "device"), (257, 3, True, "device"), (1000, 1, True, "device"),
-    (1000, 2, True, "device"), (1000, 4, True, "device"), (1000, 8, True, "device")])
-def test_mmult_replay_other_drivers(ndim, nodes, retwin, driver):
+    (1000, 2, True, "device"), (1000, 4, True, "device"), (1000, 8, True, "device"),
+    (1000, 1, True, "device-grid"), (1000, 4, True, "device-grid")])
+def test_mmult_replay_other_drivers(ndim, nodes, retwin, driver, monkeypatch):
     """The same replay with every round issued from Python (MmultReplay.round, driver="python"),
     by two C++ threads, one per context (driver="native2"), or on the device (driver="device":
     gdsm_rounds, one persistent launch per context with device-wide barriers between a round's
     steps), with and without the re-twinning release: the same home copies, totals and page
-    table."""
+    table. "device-grid": gdsm_rounds on the whole grid (GDSM_ROUNDS_XCD=0) instead of the
+    one-XCD team it takes for rounds this small."""
+    if driver == "device-grid":
+        monkeypatch.setenv("GDSM_ROUNDS_XCD", "0")
+        driver = "device"
     _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, retwin=retwin, driver=driver),
                   nodes, False)
 
 
+@pytest.mark.parametrize("xcd", ["0", "1"])
 @pytest.mark.parametrize("ndim,nodes", [(1000, 1), (257, 3), (1000, 8)])
-def test_device_rounds_stream_equals_the_issued_rounds(ndim, nodes):
-    """gdsm_rounds (every round in one persistent launch per context, write-through hand-offs
-    between its workgroups) leaves the same last-round stream, the same TWIN and CURRENT views
-    and the same home copy as the C++-issued rounds (one chained release launch per round): the
-    stream checks the record bytes and offsets that no home-copy comparison sees."""
+def test_device_rounds_stream_equals_the_issued_rounds(ndim, nodes, xcd, monkeypatch):
+    """gdsm_rounds (every round in one persistent launch per context) leaves the same last-round
+    stream, the same TWIN and CURRENT views and the same home copy as the C++-issued rounds (one
+    chained release launch per round): the stream checks the record bytes and offsets that no
+    home-copy comparison sees. Both forms of the launch: the whole grid with write-through
+    hand-offs (GDSM_ROUNDS_XCD=0) and the one-XCD team whose hand-offs meet in its L2 (=1, the
+    default at these round sizes)."""
+    monkeypatch.setenv("GDSM_ROUNDS_XCD", xcd)
     Rs = [MmultReplay(ndim=ndim, nodes=nodes, seed=11, driver=d) for d in ("native", "device")]
     try:
         out = []
