@@ -662,17 +662,26 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   COH_FSTAMP(4, __builtin_amdgcn_s_memtime());
 }
 
+// Waves per workgroup (GDSM_FOLD_WAVES, 1, 2 or 4; default 4). LDS is held by a workgroup until
+// its last wave ends, so a four-wave workgroup keeps its 32 KiB after its earlier waves' blocks are
+// done; smaller workgroups free it sooner but measured slower (config 4, same box, alternating,
+// 2 rounds: 1 wave 2.75-2.77 / 2.62 ms, 2 waves 2.51 / 2.40, 4 waves 2.27-2.28 / 2.34 uniform /
+// Zipf; bit-exact, profiles/r06_coh_wg_ab.txt).
+#ifndef GDSM_FOLD_WAVES
+#define GDSM_FOLD_WAVES 4
+#endif
+constexpr uint32_t kFoldWaves = GDSM_FOLD_WAVES;
+static_assert(kFoldWaves == 1 || kFoldWaves == 2 || kFoldWaves == 4, "fold workgroup");
+
 // kFull: the batch's whole blocks, one ticket per workgroup (tickets are drawn in dispatch
 // order, so a wave only ever waits for running waves); otherwise the single trailing partial
 // block `nb - 1`, launched after them.
 template <bool kVec, bool kFull, bool kNodes, int kM = 0>
-__global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt, uint64_t n_pages,
-                                                       const uint64_t* __restrict__ ev, uint64_t n,
-                                                       uint64_t nb, uint64_t* __restrict__ ws,
-                                                       uint32_t* __restrict__ partial,
-                                                       uint32_t* __restrict__ err,
-                                                       uint32_t n_nodes) {
-  __shared__ __attribute__((aligned(16))) uint32_t tr_all[4][kFBlock];
+__global__ __launch_bounds__(64 * kFoldWaves) void coh_fold_kernel(
+    uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev, uint64_t n,
+    uint64_t nb, uint64_t* __restrict__ ws, uint32_t* __restrict__ partial,
+    uint32_t* __restrict__ err, uint32_t n_nodes) {
+  __shared__ __attribute__((aligned(16))) uint32_t tr_all[kFoldWaves][kFBlock];
   uint64_t b;
   if (kFull) {
     // kFoldCtrs ticket counters (one 256-B line each) keyed by blockIdx % kFoldCtrs: one counter
@@ -688,7 +697,7 @@ __global__ __launch_bounds__(256) void coh_fold_kernel(uint64_t* __restrict__ pt
     const uint32_t ticket = __builtin_amdgcn_readfirstlane(tr_all[0][0]);
     __syncthreads();
     const uint64_t w = (uint64_t)ticket * kFoldCtrs + cls;
-    b = w * 4 + (threadIdx.x >> 6);
+    b = w * kFoldWaves + (threadIdx.x >> 6);
     if (b >= nb) return;
   } else {
     if (threadIdx.x >= 64) return;
@@ -1546,8 +1555,9 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
         if (vec && !nodes && cv == 6) kern = coh_fold_kernel<true, true, false, 3>;
         if (vec && !nodes && cv == 7) kern = coh_fold_kernel<true, true, false, 4>;
 #endif
-        hipLaunchKernelGGL(kern, dim3((unsigned)((full + 3) / 4)), dim3(256), 0, s, pt, n_pages,
-                           events, n_events, full, fws, fpart, err, n_nodes);
+        hipLaunchKernelGGL(kern, dim3((unsigned)((full + kFoldWaves - 1) / kFoldWaves)),
+                           dim3(64 * kFoldWaves), 0, s, pt, n_pages, events, n_events, full, fws,
+                           fpart, err, n_nodes);
       }
       if (nf > full) {
         auto kern = nodes ? coh_fold_kernel<false, false, true> : coh_fold_kernel<false, false, false>;
