@@ -46,7 +46,8 @@ __device__ unsigned long long g_fold_spans[1024][32][4];
 #ifdef GDSM_COH_STAMPS
 __device__ unsigned long long g_coh_stamps[8192 * 4 * 8];
 // Fold kernel: every 16th block b (by ticket), lane 0: [0] entry, [1] events in LDS, [2] walk
-// done, [3] look-back done, [4] end (s_memtime), [5] ordered | heads << 1 | look-back rounds << 16
+// done, [3] look-back done, [4] end (s_memtime), [5] ordered | heads << 1 | look-back rounds << 16,
+// [6] heads pass done, [7] the heads' page-table words landed (this build waits for them there)
 #define COH_FSTAMP(i, v)                                                                     \
   do {                                                                                        \
     if ((b & 15) == 0 && b / 16 < 32768 && lane == 0) g_coh_stamps[(b / 16) * 8 + (i)] = (v); \
@@ -340,6 +341,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   bool last_end = nh0 != 0;
   if (!kFull && nv > 0 && g0 + nv == n) last_end = true;
 
+  COH_FSTAMP(6, __builtin_amdgcn_s_memtime());
   // ---- page-table words of the lane's last and first heads (one gathered load each)
   uint64_t Wl = 0, Wf = 0, Ws = 0, Wt = 0;  // last, first, second, third heads (others: walk)
   {
@@ -361,6 +363,10 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   const uint32_t Hl = hit_seed(Bl), Ol = ((Bl >> 8) & 0xFFu) << 1;
   if ((GDSM_FOLD_PRIO & 5) == 5) __builtin_amdgcn_s_setprio(0);
   asm volatile("" : "+v"(Wf), "+v"(Ws), "+v"(Wt));  // waited for here, not inside the walk
+#ifdef GDSM_COH_STAMPS
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  COH_FSTAMP(7, __builtin_amdgcn_s_memtime());
+#endif
   // Early publication (see above): the words of every lane's first and last heads have landed
   // (the wave's last head's word is the only one another wave may store), so the head flag goes
   // out with it and ordered successors need not wait for this walk either.

@@ -37,6 +37,9 @@ ordered = (info & 1).astype(bool)
 heads = ((info >> 1) & 0x7F).astype(np.int64)
 rounds = (info >> 16).astype(np.int64)
 d = np.diff(t, axis=1)  # load, walk, look-back, tail
+# the walk phase split: heads pass [1 -> 6], gathers landed [6 -> 7], walk proper [7 -> 2]
+hp, ga, wk = st[:, 6].astype(np.int64) - t[:, 1], st[:, 7].astype(np.int64) - st[:, 6].astype(np.int64), t[:, 2] - st[:, 7].astype(np.int64)
+print(f"walk phase split (means): heads pass {hp.mean():.0f}  gathers landed {ga.mean():.0f}  walk {wk.mean():.0f}")
 start = t[:, 0] - t[:, 0].min()
 print(f"{dist}: waves sampled {len(t)}, span {(t[:, 4].max() - t[:, 0].min())} ticks")
 kinds = {
