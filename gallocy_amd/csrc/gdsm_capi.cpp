@@ -913,8 +913,15 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   const int xcd_env = xe && *xe ? (xe[0] == '1' ? 1 : 0) : -1;
   const bool xcd = xcd_env == 1 || (xcd_env < 0 && gd_n <= 32 && gp_n <= 32);
   const uint64_t gd_grid = xcd ? 8 * gd_n : gd_n, gp_grid = xcd ? 8 * gp_n : gp_n;
+  // a page table and rounds this small fold on ONE workgroup with the table in LDS (no grid
+  // barrier, no gathers); GDSM_ROUNDS_LDS=0 / 1 forces the choice (A/B runs, tests)
+  const char* le = getenv("GDSM_ROUNDS_LDS");  // (read per call: tests switch it)
+  const bool lds_fits = pt->n_pages <= gdsm::kRoundsLdsPages &&
+                        max_ev <= gdsm::kRoundsLdsEvents && n_rounds <= gdsm::kRoundsLdsRounds;
+  const bool lds = lds_fits && (le && *le ? *le == '1' : max_ev <= gdsm::kRoundsLdsAuto);
+  if (le && *le == '1' && !lds_fits) return -EINVAL;
   if (gd_grid > resident_grid(gdsm::rounds_data_kernel_ptr(xcd)) ||
-      gp_grid > resident_grid(gdsm::rounds_fold_kernel_ptr(xcd)))
+      (!lds && gp_grid > resident_grid(gdsm::rounds_fold_kernel_ptr(xcd))))
     return -EINVAL;
   gdsm::DiffChain& ch = data->chain;
   if (ch.epoch == 0 || ch.epoch + n_rounds >= (1u << 30)) {
@@ -926,7 +933,7 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   GDSM_TRY(gdsm::launch_rounds_fold(
       pt->coh_pt, pt->n_pages, pt->n_nodes, events,
       reinterpret_cast<const int64_t*>(pt->rounds_ws), n_rounds, (uint32_t)gp_grid, totals,
-      pt->err, &pt->coh_chain, reinterpret_cast<uint32_t*>(pt->rounds_ws + bar_at), xcd,
+      pt->err, &pt->coh_chain, reinterpret_cast<uint32_t*>(pt->rounds_ws + bar_at), xcd, lds,
       pt->stream, pt->P()));
   runs->n = (uint64_t)(id_off[n_rounds] - id_off[n_rounds - 1]);
   GDSM_TRY(gdsm::launch_rounds_data(

@@ -1319,6 +1319,159 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
   }
 }
 
+// ---- DSM rounds, page-table side on ONE workgroup (gdsm_rounds with a small page table and
+// small rounds, config 5): the page table sits in LDS for the whole launch, so a round needs no
+// page-table gathers, no look-back and no grid barrier — two workgroup barriers. Per round: the
+// round's events (loaded a round ahead, event 1024k + t in thread t) are checked (high dword,
+// node) and their low dwords staged in LDS; every thread then folds the segments (page runs)
+// whose head lies in its contiguous chunk of the round, each from its page's LDS word to the
+// segment's end (SPEC §5's rules one event at a time, as oracle/gdsm_oracle.c or_coherence), and
+// the round's totals are summed per wave, added in LDS and stored as row r. Pages are folded by
+// exactly one thread per round (a page's events are one run of the sorted round), so the rounds
+// need no other ordering. The page table is written back once, after the last round.
+constexpr uint32_t kRLThreads = 1024;
+constexpr uint32_t kRLEvents = kRoundsLdsEvents;    // a round's events staged (64 KiB)
+constexpr uint32_t kRLPer = kRLEvents / kRLThreads;  // of them loaded per thread
+
+__global__ __launch_bounds__(kRLThreads) void rounds_fold_lds_kernel(
+    uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev,
+    const int64_t* __restrict__ eoff, uint32_t n_rounds, uint32_t* __restrict__ err,
+    uint32_t n_nodes, unsigned long long* __restrict__ totals) {
+  __shared__ uint64_t spt[kRoundsLdsPages];
+  __shared__ uint32_t sev[kRLEvents];
+  __shared__ int64_t soff[kRoundsLdsRounds + 1];
+  __shared__ uint32_t red[10];
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  const uint32_t np = (uint32_t)n_pages;  // (<= kRoundsLdsPages, checked by the caller)
+  for (uint32_t i = t; i < np; i += kRLThreads) spt[i] = pt[i];
+  // every round's event offsets in LDS (n_rounds <= kRoundsLdsRounds, checked by the caller):
+  // read from memory inside the loop, their scalar loads shared lgkmcnt with the walk's LDS
+  // reads, and the first LDS wait of every round waited for them too (a memory round trip)
+  for (uint32_t i = t; i <= n_rounds; i += kRLThreads) soff[i] = eoff[i];
+  if (t < 10) red[t] = 0;
+  __syncthreads();
+  uint32_t bad = 0;
+  uint64_t X[kRLPer];
+  uint32_t nn = 0;
+  auto load = [&](uint32_t r) {
+    const uint64_t e0 = (uint64_t)soff[r];
+    nn = (uint32_t)((uint64_t)soff[r + 1] - e0);  // (<= kRLEvents, checked by the caller)
+#pragma unroll
+    for (uint32_t k = 0; k < kRLPer; ++k) {
+      const uint32_t g = k * kRLThreads + t;
+      X[k] = g < nn ? __builtin_nontemporal_load(ev + e0 + g) : 0ull;
+    }
+  };
+  if (n_rounds) load(0);
+  GDSM_RSTAMP_WG(true);
+  for (uint32_t r = 0; r < n_rounds; ++r) {
+    GDSM_RSTAMP(1, r, 0);
+    const uint32_t n = nn;
+#pragma unroll
+    for (uint32_t k = 0; k < kRLPer; ++k) {
+      const uint32_t g = k * kRLThreads + t;
+      if (g < n) {
+        const uint64_t x = X[k];
+        if ((x >> 32) || ((((uint32_t)x >> 1) & 7u) >= n_nodes)) bad = 1;
+        sev[g] = (uint32_t)x;
+      }
+    }
+    __syncthreads();  // the round staged; the previous round's words and totals settled
+    GDSM_RSTAMP(1, r, 2);
+    if (r + 1 < n_rounds) load(r + 1);  // in flight while this round is folded
+    // (an odd C, which puts the lanes' chunk starts on distinct LDS banks, measured 20-40 % slower
+    // on config 5 at 4 and 8 nodes: its rounds' page runs are P events long, which an even C
+    // splits evenly between threads and an odd one does not)
+    const uint32_t C = (n + kRLThreads - 1) / kRLThreads;
+    const uint32_t c0 = min(t * C, n), c1 = min(c0 + C, n);
+    uint32_t inv = 0, xfer = 0;
+    uint64_t nf_lo = 0, nf_hi = 0;  // fault counts of nodes 0-3 / 4-7, 16 bits each
+    // One flat walk per thread (a nested per-head loop diverged: every head position of the
+    // wave's lanes ran a whole segment walk): from the chunk's start, skipping the events of a
+    // segment headed before it, through every segment headed inside it to that segment's end.
+    uint32_t pp = c0 > 0 ? sev[c0 - 1] >> 4 : 0u;  // the page of the event before j
+    uint32_t cur = 0, f = 0, cs = 0, owner = 0, st = 0, dirty = 0;
+    bool have = false;  // folding the segment of page `cur`
+    uint32_t y = c0 < n ? sev[c0] : 0u;
+    for (uint32_t j = c0; j < n; ++j) {
+      const uint32_t x = y, yn = j + 1 < n ? sev[j + 1] : 0u;  // (read one event ahead)
+      const uint32_t pg = x >> 4;
+      const bool head = j == 0 || pg != pp;
+      if (j >= c1 && (head || !have)) break;  // the next segment is the next thread's
+      if (head) {
+        if (have)
+          spt[cur] = (uint64_t)(cs | (owner << 8) | (st << 16) | (dirty << 18)) | ((uint64_t)f << 32);
+        if (j > 0 && pg < pp) bad = 1;  // pages must not decrease
+        have = pg < np;
+        if (!have) bad = 1;
+        const uint64_t w = spt[have ? pg : 0u];
+        const uint32_t s = (uint32_t)w;
+        cur = pg;
+        f = (uint32_t)(w >> 32);
+        cs = s & 0xFFu;
+        owner = (s >> 8) & 0xFFu;
+        st = (s >> 16) & 3u;
+        dirty = (s >> 18) & 1u;
+      }
+      pp = pg;
+      y = yn;
+      if (!have) continue;
+      // (a select-only form of this step measured slower: 4.4 vs 3.7 us per 4-node round)
+      const uint32_t node = (x >> 1) & 7u, bit = 1u << node;
+      bool fault;
+      if (!(x & 1u)) {
+        fault = !(cs & bit);
+        if (fault) {
+          cs |= bit;
+          if (st == 2u) st = 1u;
+        }
+      } else {
+        dirty = 1u;
+        fault = !(st == 2u && owner == node);
+        if (fault) {
+          inv += (uint32_t)__popc(cs & ~bit);
+          xfer += owner != node ? 1u : 0u;
+        }
+        owner = node;
+        cs = bit;
+        st = 2u;
+      }
+      if (fault) {
+        ++f;
+        const uint64_t one = 1ull << (16u * (node & 3u));
+        if (node < 4u)
+          nf_lo += one;
+        else
+          nf_hi += one;
+      }
+    }
+    if (have) spt[cur] = (uint64_t)(cs | (owner << 8) | (st << 16) | (dirty << 18)) | ((uint64_t)f << 32);
+    GDSM_RSTAMP(1, r, 3);
+    // the round's totals: per wave, then in LDS (a thread's 16-bit node counts cannot overflow:
+    // a round holds at most kRLEvents events)
+    uint32_t v[10] = {inv, xfer};
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      v[2 + q] = (uint32_t)(nf_lo >> (16 * q)) & 0xFFFFu;
+      v[6 + q] = (uint32_t)(nf_hi >> (16 * q)) & 0xFFFFu;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 10; ++q) {
+      const uint32_t sq = wave_sum(v[q]);
+      if (lane == 0 && sq) atomicAdd(&red[q], sq);
+    }
+    __syncthreads();  // the round's words and totals are in LDS
+    GDSM_RSTAMP(1, r, 1);
+    if (t < 10) {
+      totals[10ull * r + t] = red[t];
+      red[t] = 0;  // (the next round adds after its first barrier)
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < np; i += kRLThreads) pt[i] = spt[i];
+  if (__syncthreads_or(bad) && t == 0) atomicOr(err, 2u);  // (kErrEvents)
+}
+
 const void* rounds_fold_kernel_ptr(bool xcd) {
   return xcd ? reinterpret_cast<const void*>(rounds_fold_kernel<true>)
              : reinterpret_cast<const void*>(rounds_fold_kernel<false>);
@@ -1327,8 +1480,16 @@ const void* rounds_fold_kernel_ptr(bool xcd) {
 hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                               const uint64_t* events, const int64_t* eoff, uint32_t n_rounds,
                               uint32_t grid, uint64_t* totals, uint32_t* err, CohChainState* chain,
-                              uint32_t* bar, bool xcd, hipStream_t s, Prof* prof) {
+                              uint32_t* bar, bool xcd, bool lds, hipStream_t s, Prof* prof) {
   if (n_rounds == 0) return hipSuccess;
+  if (lds) {  // one workgroup, the page table in LDS (no chain workspace, no barrier words)
+    if (n_pages > kRoundsLdsPages || n_rounds > kRoundsLdsRounds) return hipErrorInvalidValue;
+    ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
+    hipLaunchKernelGGL(rounds_fold_lds_kernel, dim3(1), dim3(kRLThreads), 0, s, pt, n_pages,
+                       events, eoff, n_rounds, err, n_nodes,
+                       reinterpret_cast<unsigned long long*>(totals));
+    return hipGetLastError();
+  }
   if (!chain || !chain->ws) return hipErrorInvalidValue;
   // the rounds take epochs [epoch0, epoch0 + n_rounds); the chain is zeroed again afterwards by
   // its next launch (its ticket sets are not kept in step here)

@@ -132,10 +132,20 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
 // workgroups over n_rounds rounds (eoff: device, n_rounds + 1 event offsets; totals: 10 u64 per
 // round). Uses the chain's ws with epochs of its own; the chain restarts (zeroed) afterwards.
 // bar: kRoundsBarBytes zeroed by the launcher; xcd: a one-XCD team (as launch_rounds_data).
+// lds: instead ONE workgroup with the page table in LDS (n_pages <= kRoundsLdsPages, every round
+// <= kRoundsLdsEvents events, n_rounds <= kRoundsLdsRounds; grid, chain and bar unused).
+constexpr uint64_t kRoundsLdsPages = 8192;    // 64 KiB of page-table words
+constexpr uint64_t kRoundsLdsEvents = 16384;  // 64 KiB of a round's staged events
+constexpr uint32_t kRoundsLdsRounds = 2048;   // 16 KiB of event offsets
+// gdsm_rounds takes the LDS form by itself up to this many events per round: one workgroup folds
+// a round in about 1 us per 1000 events, so beyond ~4000 the persistent grid is the faster form
+// (config 5, same box: 1 node +12 %, 2 nodes tied, 4 nodes tied, 8 nodes -27 %)
+constexpr uint64_t kRoundsLdsAuto = 4096;
 hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                               const uint64_t* events, const int64_t* eoff, uint32_t n_rounds,
                               uint32_t grid, uint64_t* totals, uint32_t* err, CohChainState* chain,
-                              uint32_t* bar, bool xcd, hipStream_t s, Prof* prof = nullptr);
+                              uint32_t* bar, bool xcd, bool lds, hipStream_t s,
+                              Prof* prof = nullptr);
 const void* rounds_fold_kernel_ptr(bool xcd);  // (for the occupancy query)
 hipError_t launch_gen_events(uint64_t* events, const uint64_t* offsets, uint64_t first_page,
                              uint64_t n, uint64_t seed, uint32_t n_nodes, uint32_t write_pct,

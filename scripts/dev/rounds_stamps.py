@@ -38,6 +38,8 @@ print("page data: copies", us(d[:, 1] - d[:, 0]), "barrier 1", us(d[:, 2] - d[:,
       "round", us(d[1:, 0] - d[:-1, 0]))
 print("page table: fold", us(f[:, 1] - f[:, 0]), "barrier", us(f[1:, 0] - f[:-1, 1]),
       "round", us(f[1:, 0] - f[:-1, 0]))
+print("  (one-workgroup LDS fold, GDSM_ROUNDS_LDS: staging + barrier", us(f[:, 2] - f[:, 0]),
+      "walk", us(f[:, 3] - f[:, 2]), "totals + barrier", us(f[:, 1] - f[:, 3]), ")")
 print("  span 0 of the fold: loads + gathers + scan", us(f[:, 2] - f[:, 0]),
       "look-back", us(f[:, 3] - f[:, 2]), "tail (corrections, totals)", us(f[:, 1] - f[:, 3]))
 # every span of the fold against its round's start (workgroup 0's point 0): entry, published,

@@ -29,16 +29,21 @@ def test_mmult_replay_end_to_end(ndim, nodes, graph, fused):
     (1000, 4, True, "native2"), (257, 3, False, "native2"),
     (64, 1, True, "device"), (257, 3, True, "device"), (1000, 1, True, "device"),
     (1000, 2, True, "device"), (1000, 4, True, "device"), (1000, 8, True, "device"),
-    (1000, 1, True, "device-grid"), (1000, 4, True, "device-grid")])
+    (1000, 1, True, "device-grid"), (1000, 4, True, "device-grid"),
+    (1000, 1, True, "device-gridfold"), (1000, 8, True, "device-gridfold")])
 def test_mmult_replay_other_drivers(ndim, nodes, retwin, driver, monkeypatch):
     """The same replay with every round issued from Python (MmultReplay.round, driver="python"),
     by two C++ threads, one per context (driver="native2"), or on the device (driver="device":
     gdsm_rounds, one persistent launch per context with device-wide barriers between a round's
     steps), with and without the re-twinning release: the same home copies, totals and page
     table. "device-grid": gdsm_rounds on the whole grid (GDSM_ROUNDS_XCD=0) instead of the
-    one-XCD team it takes for rounds this small."""
+    one-XCD team it takes for rounds this small; "device-gridfold": the page-table rounds on the
+    persistent grid (GDSM_ROUNDS_LDS=0) instead of one workgroup with the table in LDS."""
     if driver == "device-grid":
         monkeypatch.setenv("GDSM_ROUNDS_XCD", "0")
+        driver = "device"
+    if driver == "device-gridfold":
+        monkeypatch.setenv("GDSM_ROUNDS_LDS", "0")
         driver = "device"
     _check_replay(MmultReplay(ndim=ndim, nodes=nodes, seed=7, retwin=retwin, driver=driver),
                   nodes, False)
