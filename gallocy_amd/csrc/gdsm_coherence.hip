@@ -1366,7 +1366,10 @@ __global__ __launch_bounds__(kRLThreads) void rounds_fold_lds_kernel(
   GDSM_RSTAMP_WG(true);
   for (uint32_t r = 0; r < n_rounds; ++r) {
     GDSM_RSTAMP(1, r, 0);
-    const uint32_t n = nn;
+    // (a round past the staging area fails the call instead of walking past it; gdsm_rounds
+    // never picks this kernel for one)
+    const uint32_t n = nn <= kRLEvents ? nn : 0u;
+    if (nn > kRLEvents) bad = 1;
 #pragma unroll
     for (uint32_t k = 0; k < kRLPer; ++k) {
       const uint32_t g = k * kRLThreads + t;
