@@ -139,6 +139,16 @@ __global__ __launch_bounds__(256) void coh_init_kernel(uint64_t* __restrict__ pt
 #ifndef GDSM_FOLD_PRIO
 #define GDSM_FOLD_PRIO 5
 #endif
+// GDSM_FOLD_SPEC (whole blocks; 1: first and last heads, 2: the second head too): the heads'
+// page-table words guessed from the lane's first and last events and gathered before the heads
+// pass instead of after it (see the walk prologue). Bit-exact and slower, so off: the guesses
+// are live through the heads pass, which takes the fold to 102-106 VGPRs (4 waves/SIMD), or to
+// 96 with spills when held to 5 waves/SIMD; measured in that form (same box, alternating, 3
+// rounds): 2.34 / 2.47-2.49 ms against 2.27-2.28 / 2.34-2.35 (uniform / Zipf),
+// profiles/r06_coh_spec_ab.txt.
+#ifndef GDSM_FOLD_SPEC
+#define GDSM_FOLD_SPEC 0
+#endif
 constexpr uint32_t kFK = GDSM_FOLD_K;       // events per lane (16 or 32: hm is one 32-bit mask)
 constexpr uint32_t kFH = 16;                // of them held in registers at a time
 constexpr uint32_t kFBlock = 64 * kFK;
@@ -297,6 +307,27 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   uint32_t xp = from_prev_lane(tr[fold_slot(kFK * lane + kFK - 1)]);
   if (lane == 0) xp = xprev_w;
   const bool batch_first = lo == 0 && lane == 0;
+#if GDSM_FOLD_SPEC
+  // ---- the page-table words of the lane's heads, guessed and gathered BEFORE the heads pass, so
+  // their latency hides behind it: the lane's last head is the page of its last event (whenever
+  // the lane has a head), its first head the page of its first event or, when that event
+  // continues an earlier segment, the next page (right whenever the batch's pages are dense, as
+  // config 4's are), its second head the page after the first. A wrong guess is loaded again
+  // after the heads pass; a guessed word that is not one of the lane's heads is never used
+  // (another wave may be storing it).
+  uint64_t Wl_s = 0, Wf_s = 0, Ws_s = 0;
+  uint32_t pf_s = 0;
+  if (kFull) {
+    const uint32_t pg0 = tr[fold_slot(kFK * lane)] >> 4;
+    pf_s = (batch_first || pg0 != (xp >> 4)) ? pg0 : pg0 + 1u;
+    const uint32_t pl_s = xlast >> 4;
+    if (pl_s < n_pages) Wl_s = pt[pl_s];
+    if (pf_s < pl_s && pf_s < n_pages) Wf_s = pt[pf_s];
+#if GDSM_FOLD_SPEC > 1
+    if (pf_s + 1u < pl_s && pf_s + 1u < n_pages) Ws_s = pt[pf_s + 1u];
+#endif
+  }
+#endif
 
   // ---- heads (a new page), validity. (Sortedness inside a lane is checked where the walk meets
   // a head; the first / last head events are read back from LDS.)
@@ -344,6 +375,25 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   COH_FSTAMP(6, __builtin_amdgcn_s_memtime());
   // ---- page-table words of the lane's last and first heads (one gathered load each)
   uint64_t Wl = 0, Wf = 0, Ws = 0, Wt = 0;  // last, first, second, third heads (others: walk)
+#if GDSM_FOLD_SPEC
+  if (kFull) {  // the guesses above, and a load where one missed
+    const uint32_t pf = xf >> 4;
+    Wl = Wl_s;  // (pages of the lane's last head and last event are equal)
+    Wf = Wf_s;
+    if (hc > 1 && pf != pf_s && pf < n_pages) Wf = pt[pf];
+    if (GDSM_FOLD_PRE2 && hc > 2) {
+      const uint32_t h2 = hm & (hm - 1u);
+      const uint32_t p2 = tr[fold_slot(kFK * lane + (uint32_t)__builtin_ctz(h2))] >> 4;
+      Ws = Ws_s;
+      if ((GDSM_FOLD_SPEC < 2 || p2 != pf_s + 1u) && p2 < n_pages) Ws = pt[p2];
+      if (GDSM_FOLD_PRE2 > 1 && hc > 3) {
+        const uint32_t h3 = h2 & (h2 - 1u);
+        const uint32_t p3 = tr[fold_slot(kFK * lane + (uint32_t)__builtin_ctz(h3))] >> 4;
+        if (p3 < n_pages) Wt = pt[p3];
+      }
+    }
+  } else
+#endif
   {
     const uint32_t pl = xl >> 4, pf = xf >> 4;
     if (hc && pl < n_pages) Wl = pt[pl];
