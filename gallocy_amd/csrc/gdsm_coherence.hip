@@ -139,6 +139,15 @@ __global__ __launch_bounds__(256) void coh_init_kernel(uint64_t* __restrict__ pt
 #ifndef GDSM_FOLD_PRIO
 #define GDSM_FOLD_PRIO 5
 #endif
+// GDSM_FOLD_REGHEADS (whole blocks): events loaded as 128q + lane and 128q + 64 + lane (8-B
+// loads), their head flags taken in registers from the neighbouring lane's page, and two ballots
+// per 128 events written into the head masks of walk lanes 4q .. 4q + 3 (v_writelane) — the
+// heads pass over the LDS copy goes away. Bit-exact and slower, so off: without the heads pass the
+// walk's allocation grows to 111 VGPRs (4 waves/SIMD; held to 5 it spills): 2.42 / 2.50 ms
+// against 2.25 / 2.31 (uniform / Zipf, same box, alternating; profiles/r06_coh_regheads_ab.txt).
+#ifndef GDSM_FOLD_REGHEADS
+#define GDSM_FOLD_REGHEADS 0
+#endif
 // GDSM_FOLD_SPEC (whole blocks; 1: first and last heads, 2: the second head too): the heads'
 // page-table words guessed from the lane's first and last events and gathered before the heads
 // pass instead of after it (see the walk prologue). Bit-exact and slower, so off: the guesses
@@ -157,6 +166,13 @@ constexpr uint32_t kKr = kHRead | kHW | kPRE;  // kept by a read miss
 constexpr uint64_t kFAgg = 1ull << 62, kFIncl = 2ull << 62, kFHead = 1ull << 61;
 constexpr uint32_t kFoldCtrs = 8;                   // workgroup ticket counters
 constexpr uint64_t kFoldStatus = kFoldCtrs * 32;    // u64 index of block 0's status granule
+
+// v_writelane_b32 as the compiler's intrinsic (no __builtin in this clang; it owns M0)
+extern "C" __device__ int coh_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint2 ld_nt8(const uint64_t* p) {
+  const uint64_t v = __builtin_nontemporal_load(p);
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
 
 __device__ __forceinline__ uint32_t hit_seed(uint32_t w) {
   const uint32_t c = w & 0xFFu;
@@ -255,7 +271,62 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   uint32_t eagg = 0;
   bool early = false;
-  if (kVec && kFull) {
+  uint32_t hm_r = 0, dec_r = 0;  // GDSM_FOLD_REGHEADS: this lane's head mask, a page decreased
+  if (kVec && kFull && GDSM_FOLD_REGHEADS) {
+    // the page of the event before the block (uniform)
+    uint32_t pprev = (lo > 0 ? (uint32_t)ev[kM == 4 ? (lo_src ? lo_src - 1 : 0) : lo - 1] + padd : 0u) >> 4;
+    uint32_t ea = 0, eb = 0;  // events 1920 + lane and 1984 + lane
+    uint2 VA[kFBlock / 128], VB[kFBlock / 128];  // every load in flight at once
+#pragma unroll
+    for (uint32_t q = 0; q < kFBlock / 128; ++q) {
+      VA[q] = ld_nt8(ev + lo_src + 128 * q + lane);
+      VB[q] = ld_nt8(ev + lo_src + 128 * q + 64 + lane);
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kFBlock / 128; ++q) {
+      const uint2 va = VA[q], vb = VB[q];
+      hib |= va.y | vb.y;
+      const uint32_t xa = va.x + padd, xb = vb.x + padd;
+      tr[fold_slot(128 * q + lane)] = xa;
+      tr[fold_slot(128 * q + 64 + lane)] = xb;
+      const uint32_t pa = xa >> 4, pb = xb >> 4;
+      uint32_t qa = from_prev_lane(pa), qb = from_prev_lane(pb);
+      if (lane == 0) {
+        qa = pprev;
+        qb = lane_bcast(pa, 63);
+      }
+      pprev = lane_bcast(pb, 63);
+      const bool first = q == 0 && lo == 0 && lane == 0;  // the batch's first event
+      dec_r |= ((!first && pa < qa) || pb < qb) ? 1u : 0u;
+      asm volatile("" : "+v"(dec_r));  // now: sunk, it kept every chunk's pages live
+      const uint64_t Ma = __ballot(first || pa != qa), Mb = __ballot(pb != qb);
+      hm_r = (uint32_t)coh_writelane((int)(uint32_t)Ma, (int)(4 * q), (int)hm_r);
+      hm_r = (uint32_t)coh_writelane((int)(uint32_t)(Ma >> 32), (int)(4 * q + 1), (int)hm_r);
+      hm_r = (uint32_t)coh_writelane((int)(uint32_t)Mb, (int)(4 * q + 2), (int)hm_r);
+      hm_r = (uint32_t)coh_writelane((int)(uint32_t)(Mb >> 32), (int)(4 * q + 3), (int)hm_r);
+      if (q == kFBlock / 128 - 1) {
+        ea = xa;
+        eb = xb;
+      }
+    }
+    // ---- early aggregate (as below, in this layout: a = event 1920 + lane, b = 1984 + lane)
+    const uint64_t bwb = __ballot((eb & 1u) != 0), bwa = __ballot((ea & 1u) != 0);
+    if (kM == 0 && b > 0 && (bwa | bwb)) {
+      const bool inb = bwb != 0;
+      const uint32_t Lw = 63u - (uint32_t)__builtin_clzll(inb ? bwb : bwa);
+      const uint32_t xw = inb ? lane_bcast(eb, (int)Lw) : lane_bcast(ea, (int)Lw);
+      const uint32_t wi = (inb ? 64u : 0u) + Lw;
+      if ((xw >> 4) == (lane_bcast(eb, 63) >> 4)) {
+        const uint32_t r = (lane > wi ? 1u << ((ea >> 1) & 7u) : 0u) |
+                           (64u + lane > wi ? 1u << ((eb >> 1) & 7u) : 0u);
+        uint32_t R = 0;
+#pragma unroll
+        for (uint32_t nd = 0; nd < 8; ++nd) R |= __ballot((r >> nd) & 1u) ? 1u << nd : 0u;
+        eagg = tcompose(kConst | wr_word(xw), R);
+        early = true;
+      }
+    }
+  } else if (kVec && kFull) {
     uint32_t e0 = 0, e1 = 0;  // events 1920 + 2 * lane and the one after it
 #pragma unroll
     for (uint32_t q = 0; q < kFBlock / 128; ++q) {
@@ -334,8 +405,13 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
   uint32_t X[kFH];
   uint32_t hm = 0;
   uint32_t bad = hib ? 1u : 0u;
+  constexpr bool kRegHeads = kVec && kFull && GDSM_FOLD_REGHEADS;
+  if (kRegHeads) {
+    hm = hm_r;
+    if (dec_r) bad = 1;
+  }
 #pragma unroll
-  for (uint32_t h = 0; h < kFK / kFH; ++h) {
+  for (uint32_t h = 0; h < (kRegHeads ? 0u : kFK / kFH); ++h) {
     fold_half(tr, lane, h, X);
 #pragma unroll
     for (uint32_t j = 0; j < kFH; ++j) {
@@ -354,7 +430,7 @@ __device__ __forceinline__ void coh_fold_wave(uint64_t* __restrict__ pt, uint64_
     }
     xp = X[kFH - 1];
   }
-  if (kFull) hm = __brev(hm) >> (32u - kFK);
+  if (kFull && !kRegHeads) hm = __brev(hm) >> (32u - kFK);
   const uint32_t hc = (uint32_t)__popc(hm);
   uint32_t xf = 0, xl = 0;  // the lane's first and last head events
   if (hc) {
