@@ -913,12 +913,20 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   const int xcd_env = xe && *xe ? (xe[0] == '1' ? 1 : 0) : -1;
   const bool xcd = xcd_env == 1 || (xcd_env < 0 && gd_n <= 32 && gp_n <= 32);
   const uint64_t gd_grid = xcd ? 8 * gd_n : gd_n, gp_grid = xcd ? 8 * gp_n : gp_n;
-  // a page table and rounds this small fold on ONE workgroup with the table in LDS (no grid
-  // barrier, no gathers); GDSM_ROUNDS_LDS=0 / 1 forces the choice (A/B runs, tests)
+  // a page table and rounds this small fold on a few workgroups that keep slices of the table in
+  // LDS (no grid barrier, no gathers, no hand-off); GDSM_ROUNDS_LDS=0 / 1 forces the choice
   const char* le = getenv("GDSM_ROUNDS_LDS");  // (read per call: tests switch it)
-  const bool lds_fits = pt->n_pages <= gdsm::kRoundsLdsPages &&
+  // its workgroups: one per kRoundsLdsWGEvents of the largest round, and enough that every slice
+  // of the table fits (GDSM_ROUNDS_LDS_WG forces the count: A/B runs)
+  const char* lw = getenv("GDSM_ROUNDS_LDS_WG");
+  uint64_t lds_wg = std::max<uint64_t>(
+      std::max<uint64_t>((max_ev + gdsm::kRoundsLdsWGEvents - 1) / gdsm::kRoundsLdsWGEvents, 1),
+      (pt->n_pages + gdsm::kRoundsLdsPages - 1) / gdsm::kRoundsLdsPages);
+  if (lw && *lw) lds_wg = std::max<uint64_t>((uint64_t)atoll(lw), 1);
+  const bool lds_fits = lds_wg <= gdsm::kRoundsLdsMaxWGs &&
+                        (pt->n_pages + lds_wg - 1) / lds_wg <= gdsm::kRoundsLdsPages &&
                         max_ev <= gdsm::kRoundsLdsEvents && n_rounds <= gdsm::kRoundsLdsRounds;
-  const bool lds = lds_fits && (le && *le ? *le == '1' : max_ev <= gdsm::kRoundsLdsAuto);
+  const bool lds = lds_fits && !(le && *le == '0');
   if (le && *le == '1' && !lds_fits) return -EINVAL;
   if (gd_grid > resident_grid(gdsm::rounds_data_kernel_ptr(xcd)) ||
       (!lds && gp_grid > resident_grid(gdsm::rounds_fold_kernel_ptr(xcd))))
@@ -932,7 +940,8 @@ int gdsm_rounds(gdsm_ctx* data, gdsm_ctx* pt, uint32_t n_rounds, const uint64_t*
   ch.epoch = 0;  // the next chained release zeroes the workspace again (its ticket sets restart)
   GDSM_TRY(gdsm::launch_rounds_fold(
       pt->coh_pt, pt->n_pages, pt->n_nodes, events,
-      reinterpret_cast<const int64_t*>(pt->rounds_ws), n_rounds, (uint32_t)gp_grid, totals,
+      reinterpret_cast<const int64_t*>(pt->rounds_ws), n_rounds,
+      (uint32_t)(lds ? lds_wg : gp_grid), totals,
       pt->err, &pt->coh_chain, reinterpret_cast<uint32_t*>(pt->rounds_ws + bar_at), xcd, lds,
       pt->stream, pt->P()));
   runs->n = (uint64_t)(id_off[n_rounds] - id_off[n_rounds - 1]);

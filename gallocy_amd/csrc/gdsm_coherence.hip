@@ -1455,6 +1455,12 @@ __global__ __launch_bounds__(256) void rounds_fold_kernel(uint64_t* __restrict__
 // the round's totals are summed per wave, added in LDS and stored as row r. Pages are folded by
 // exactly one thread per round (a page's events are one run of the sorted round), so the rounds
 // need no other ordering. The page table is written back once, after the last round.
+// Several workgroups (gridDim.x = W): workgroup w keeps pages [w S, w S + S) (S = `slice`) and
+// folds the events of those pages only — every workgroup stages the whole round and counts the
+// events below its slice and below its slice's end (their index range, the round being sorted),
+// so a round's work is split W ways with no hand-off between workgroups; the totals are added to
+// row r by each workgroup (the launcher zeroes the rows). A page outside the folding workgroup's
+// slice (only an unsorted round puts one there) fails the call.
 constexpr uint32_t kRLThreads = 1024;
 constexpr uint32_t kRLEvents = kRoundsLdsEvents;    // a round's events staged (64 KiB)
 constexpr uint32_t kRLPer = kRLEvents / kRLThreads;  // of them loaded per thread
@@ -1462,19 +1468,24 @@ constexpr uint32_t kRLPer = kRLEvents / kRLThreads;  // of them loaded per threa
 __global__ __launch_bounds__(kRLThreads) void rounds_fold_lds_kernel(
     uint64_t* __restrict__ pt, uint64_t n_pages, const uint64_t* __restrict__ ev,
     const int64_t* __restrict__ eoff, uint32_t n_rounds, uint32_t* __restrict__ err,
-    uint32_t n_nodes, unsigned long long* __restrict__ totals) {
+    uint32_t n_nodes, unsigned long long* __restrict__ totals, uint32_t slice) {
   __shared__ uint64_t spt[kRoundsLdsPages];
   __shared__ uint32_t sev[kRLEvents];
   __shared__ int64_t soff[kRoundsLdsRounds + 1];
   __shared__ uint32_t red[10];
+  __shared__ uint32_t rng[2][2];  // per round parity: events below the slice, below its end
   const uint32_t t = threadIdx.x, lane = t & 63;
-  const uint32_t np = (uint32_t)n_pages;  // (<= kRoundsLdsPages, checked by the caller)
-  for (uint32_t i = t; i < np; i += kRLThreads) spt[i] = pt[i];
+  // this workgroup's slice of pages [base, base + np) (slice <= kRoundsLdsPages, by the caller)
+  const uint32_t base = blockIdx.x * slice;
+  const uint32_t np = base < n_pages ? (uint32_t)min((uint64_t)slice, n_pages - base) : 0u;
+  const uint32_t lim = base + slice;
+  for (uint32_t i = t; i < np; i += kRLThreads) spt[i] = pt[base + i];
   // every round's event offsets in LDS (n_rounds <= kRoundsLdsRounds, checked by the caller):
   // read from memory inside the loop, their scalar loads shared lgkmcnt with the walk's LDS
   // reads, and the first LDS wait of every round waited for them too (a memory round trip)
   for (uint32_t i = t; i <= n_rounds; i += kRLThreads) soff[i] = eoff[i];
   if (t < 10) red[t] = 0;
+  if (t < 4) rng[t >> 1][t & 1] = 0;
   __syncthreads();
   uint32_t bad = 0;
   uint64_t X[kRLPer];
@@ -1496,6 +1507,7 @@ __global__ __launch_bounds__(kRLThreads) void rounds_fold_lds_kernel(
     // never picks this kernel for one)
     const uint32_t n = nn <= kRLEvents ? nn : 0u;
     if (nn > kRLEvents) bad = 1;
+    uint32_t below = 0, below_end = 0;  // this thread's events of pages < base / < lim
 #pragma unroll
     for (uint32_t k = 0; k < kRLPer; ++k) {
       const uint32_t g = k * kRLThreads + t;
@@ -1503,16 +1515,31 @@ __global__ __launch_bounds__(kRLThreads) void rounds_fold_lds_kernel(
         const uint64_t x = X[k];
         if ((x >> 32) || ((((uint32_t)x >> 1) & 7u) >= n_nodes)) bad = 1;
         sev[g] = (uint32_t)x;
+        below += ((uint32_t)x >> 4) < base ? 1u : 0u;
+        below_end += ((uint32_t)x >> 4) < lim ? 1u : 0u;
+      }
+    }
+    if (gridDim.x > 1) {
+      const uint32_t b0 = wave_sum(below), b1 = wave_sum(below_end);
+      if (lane == 0) {
+        if (b0) atomicAdd(&rng[r & 1][0], b0);
+        if (b1) atomicAdd(&rng[r & 1][1], b1);
       }
     }
     __syncthreads();  // the round staged; the previous round's words and totals settled
+    uint32_t lo = 0, hi = n;  // this slice's events (the whole round for one workgroup)
+    if (gridDim.x > 1) {
+      lo = min(rng[r & 1][0], n);
+      hi = min(max(rng[r & 1][1], lo), n);
+      if (t < 2) rng[(r + 1) & 1][t] = 0;  // (round r - 1's pair: read before this barrier)
+    }
     GDSM_RSTAMP(1, r, 2);
     if (r + 1 < n_rounds) load(r + 1);  // in flight while this round is folded
     // (an odd C, which puts the lanes' chunk starts on distinct LDS banks, measured 20-40 % slower
     // on config 5 at 4 and 8 nodes: its rounds' page runs are P events long, which an even C
     // splits evenly between threads and an odd one does not)
-    const uint32_t C = (n + kRLThreads - 1) / kRLThreads;
-    const uint32_t c0 = min(t * C, n), c1 = min(c0 + C, n);
+    const uint32_t C = (hi - lo + kRLThreads - 1) / kRLThreads;
+    const uint32_t c0 = min(lo + t * C, hi), c1 = min(c0 + C, hi);
     uint32_t inv = 0, xfer = 0;
     uint64_t nf_lo = 0, nf_hi = 0;  // fault counts of nodes 0-3 / 4-7, 16 bits each
     // One flat walk per thread (a nested per-head loop diverged: every head position of the
@@ -1531,11 +1558,11 @@ __global__ __launch_bounds__(kRLThreads) void rounds_fold_lds_kernel(
         if (have)
           spt[cur] = (uint64_t)(cs | (owner << 8) | (st << 16) | (dirty << 18)) | ((uint64_t)f << 32);
         if (j > 0 && pg < pp) bad = 1;  // pages must not decrease
-        have = pg < np;
+        have = pg >= base && pg - base < np;  // (outside the slice: an unsorted round)
         if (!have) bad = 1;
-        const uint64_t w = spt[have ? pg : 0u];
+        const uint64_t w = spt[have ? pg - base : 0u];
         const uint32_t s = (uint32_t)w;
-        cur = pg;
+        cur = pg - base;
         f = (uint32_t)(w >> 32);
         cs = s & 0xFFu;
         owner = (s >> 8) & 0xFFu;
@@ -1592,12 +1619,12 @@ __global__ __launch_bounds__(kRLThreads) void rounds_fold_lds_kernel(
     __syncthreads();  // the round's words and totals are in LDS
     GDSM_RSTAMP(1, r, 1);
     if (t < 10) {
-      totals[10ull * r + t] = red[t];
+      if (red[t]) atomicAdd(totals + 10ull * r + t, (unsigned long long)red[t]);
       red[t] = 0;  // (the next round adds after its first barrier)
     }
   }
   __syncthreads();
-  for (uint32_t i = t; i < np; i += kRLThreads) pt[i] = spt[i];
+  for (uint32_t i = t; i < np; i += kRLThreads) pt[base + i] = spt[i];
   if (__syncthreads_or(bad) && t == 0) atomicOr(err, 2u);  // (kErrEvents)
 }
 
@@ -1611,12 +1638,17 @@ hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                               uint32_t grid, uint64_t* totals, uint32_t* err, CohChainState* chain,
                               uint32_t* bar, bool xcd, bool lds, hipStream_t s, Prof* prof) {
   if (n_rounds == 0) return hipSuccess;
-  if (lds) {  // one workgroup, the page table in LDS (no chain workspace, no barrier words)
-    if (n_pages > kRoundsLdsPages || n_rounds > kRoundsLdsRounds) return hipErrorInvalidValue;
+  if (lds) {  // `grid` workgroups, the page table in LDS slices (no chain workspace or barrier)
+    const uint64_t slice = (n_pages + grid - 1) / max(grid, 1u);
+    if (grid == 0 || grid > kRoundsLdsMaxWGs || slice > kRoundsLdsPages ||
+        n_rounds > kRoundsLdsRounds)
+      return hipErrorInvalidValue;
+    const hipError_t e = hipMemsetAsync(totals, 0, 80ull * n_rounds, s);  // rows: added to
+    if (e != hipSuccess) return e;
     ProfScope ps(prof, GDSM_PROF_COH_FOLD, s);
-    hipLaunchKernelGGL(rounds_fold_lds_kernel, dim3(1), dim3(kRLThreads), 0, s, pt, n_pages,
+    hipLaunchKernelGGL(rounds_fold_lds_kernel, dim3(grid), dim3(kRLThreads), 0, s, pt, n_pages,
                        events, eoff, n_rounds, err, n_nodes,
-                       reinterpret_cast<unsigned long long*>(totals));
+                       reinterpret_cast<unsigned long long*>(totals), (uint32_t)max(slice, (uint64_t)1));
     return hipGetLastError();
   }
   if (!chain || !chain->ws) return hipErrorInvalidValue;

@@ -132,15 +132,17 @@ hipError_t launch_coherence(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
 // workgroups over n_rounds rounds (eoff: device, n_rounds + 1 event offsets; totals: 10 u64 per
 // round). Uses the chain's ws with epochs of its own; the chain restarts (zeroed) afterwards.
 // bar: kRoundsBarBytes zeroed by the launcher; xcd: a one-XCD team (as launch_rounds_data).
-// lds: instead ONE workgroup with the page table in LDS (n_pages <= kRoundsLdsPages, every round
-// <= kRoundsLdsEvents events, n_rounds <= kRoundsLdsRounds; grid, chain and bar unused).
-constexpr uint64_t kRoundsLdsPages = 8192;    // 64 KiB of page-table words
+// lds: instead `grid` workgroups (<= kRoundsLdsMaxWGs) with the page table in LDS slices of
+// ceil(n_pages / grid) <= kRoundsLdsPages pages (every round <= kRoundsLdsEvents events, n_rounds
+// <= kRoundsLdsRounds; chain and bar unused).
+constexpr uint64_t kRoundsLdsPages = 8192;    // 64 KiB of page-table words per workgroup
+constexpr uint32_t kRoundsLdsMaxWGs = 16;     // workgroups (page-table slices) of the LDS form
+constexpr uint64_t kRoundsLdsWGEvents = 4096; // a round's events per workgroup the host aims at
 constexpr uint64_t kRoundsLdsEvents = 16384;  // 64 KiB of a round's staged events
 constexpr uint32_t kRoundsLdsRounds = 2048;   // 16 KiB of event offsets
-// gdsm_rounds takes the LDS form by itself up to this many events per round: one workgroup folds
-// a round in about 1 us per 1000 events, so beyond ~4000 the persistent grid is the faster form
-// (config 5, same box: 1 node +12 %, 2 nodes tied, 4 nodes tied, 8 nodes -27 %)
-constexpr uint64_t kRoundsLdsAuto = 4096;
+// (gdsm_rounds takes the LDS form whenever it fits: config 5, same box, against the grid fold,
+// 1 / 2 / 4 / 8 nodes on 1 / 1 / 2 / 4 workgroups: +12 % / tied / +12 % / +5 %; one workgroup
+// alone at 4 and 8 nodes was the slower form, -10 % / -25 %, profiles/r06_rounds_lds_ab.txt)
 hipError_t launch_rounds_fold(uint64_t* pt, uint64_t n_pages, uint32_t n_nodes,
                               const uint64_t* events, const int64_t* eoff, uint32_t n_rounds,
                               uint32_t grid, uint64_t* totals, uint32_t* err, CohChainState* chain,

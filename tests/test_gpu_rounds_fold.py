@@ -1,9 +1,9 @@
 """gdsm_rounds' page-table side on its own (docs/SPEC.md §5, rounds folded in order): random
 multi-round batches against the C oracle's sequential fold, round by round (page-table words,
-per-page faults, every round's totals row). Both forms of the launch: ONE workgroup with the page
-table in LDS (GDSM_ROUNDS_LDS=1: tables of <= 8192 pages, rounds of <= 16384 events; the
-default up to 4096 events per round) and the persistent grid (GDSM_ROUNDS_LDS=0, the form larger
-tables and rounds take). The data
+per-page faults, every round's totals row). Both forms of the launch: workgroups that keep
+slices of the page table in LDS (GDSM_ROUNDS_LDS=1, the default wherever it fits: up to 16 slices
+of <= 8192 pages, rounds of <= 16384 events, <= 2048 rounds) and the persistent grid
+(GDSM_ROUNDS_LDS=0, the form larger tables and rounds take). The data
 side gets empty rounds (no pages), so only the fold runs."""
 import ctypes as C
 
@@ -66,14 +66,18 @@ def _oracle_rounds(n_pages, n_nodes, rounds, st0=None, fl0=None):
     return st, fl, np.array(tots, np.uint64).reshape(len(rounds), 10)
 
 
-@pytest.mark.parametrize("lds", ["1", "0"])
+@pytest.mark.parametrize("lds", ["1", "0", "1-wg3"])
 @pytest.mark.parametrize("n_pages,n_nodes,sizes", [
     (6011, 8, [2012, 2012, 0, 16096, 1, 5000]),   # config 5's table; an empty and a 1-event round
     (LDS_PAGES, 5, [LDS_EVENTS, 3, LDS_EVENTS]),   # both LDS limits at once
     (100, 2, [900, 1200, 64, 7]),                 # long page runs across thread chunks
 ])
 def test_rounds_fold_matches_oracle(n_pages, n_nodes, sizes, lds, monkeypatch):
-    monkeypatch.setenv("GDSM_ROUNDS_LDS", lds)
+    """lds "1-wg3": the LDS form on three workgroups (GDSM_ROUNDS_LDS_WG=3), each folding the
+    events of its third of the table."""
+    monkeypatch.setenv("GDSM_ROUNDS_LDS", lds[0])
+    if lds.endswith("wg3"):
+        monkeypatch.setenv("GDSM_ROUNDS_LDS_WG", "3")
     rounds = [_round_events(n_pages, n, n_nodes, seed=40 + i, write_pct=(10, 35, 70)[i % 3])
               for i, n in enumerate(sizes)]
     got = _run_rounds(n_pages, n_nodes, rounds)
@@ -153,3 +157,38 @@ def test_rounds_fold_more_rounds_than_lds_offsets(lds, monkeypatch):
     want = _oracle_rounds(64, 4, rounds)
     for g, w in zip(got, want):
         assert np.array_equal(g, w)
+
+
+@pytest.mark.parametrize("wg", ["", "3"])
+def test_rounds_fold_lds_slices_a_larger_table(wg, monkeypatch):
+    """A table of 20000 pages (more than one workgroup's 8192) in the LDS form: three or four
+    slices, Zipf rounds whose runs cross the slices' edges, and 8192-page multiples."""
+    monkeypatch.setenv("GDSM_ROUNDS_LDS", "1")
+    if wg:
+        monkeypatch.setenv("GDSM_ROUNDS_LDS_WG", wg)
+    n = 20000
+    rounds = [_round_events(n, m, 8, seed=600 + i, write_pct=30)
+              for i, m in enumerate([16000, 9000, 1, 12000])]
+    got = _run_rounds(n, 8, rounds)
+    want = _oracle_rounds(n, 8, rounds)
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+
+
+@pytest.mark.parametrize("bad", ["unsorted", "across"])
+def test_rounds_fold_lds_slices_reject_unsorted_rounds(bad, monkeypatch):
+    """Unsorted rounds on three slices: a swap inside one slice, and one that moves an event into
+    another slice's index range."""
+    monkeypatch.setenv("GDSM_ROUNDS_LDS", "1")
+    monkeypatch.setenv("GDSM_ROUNDS_LDS_WG", "3")
+    good = _round_events(600, 6000, 4, seed=21, write_pct=25)
+    ev = good.copy()
+    if bad == "unsorted":
+        pg = ev >> np.uint64(4)
+        i = int(np.flatnonzero(pg[1:] != pg[:-1])[len(pg) // 4 // 100])  # a page change inside
+        ev[i], ev[i + 1] = ev[i + 1], ev[i]                              # the first slices
+    else:
+        ev[0], ev[-1] = ev[-1], ev[0]
+    with pytest.raises(GdsmError) as ei:
+        _run_rounds(600, 4, [good, ev])
+    assert ei.value.errno == 22
